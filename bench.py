@@ -1,0 +1,264 @@
+#!/usr/bin/env python3
+"""Benchmark: majority-rule rollout throughput on MI355X (BASELINE.json metric).
+
+Workload (one "step"): s_endstate + m for a batch of replicas — p+c-1 = 2
+synchronous majority sweeps of R = 4096 bit-packed replicas on a d=4 random
+regular graph with N = 1e6 nodes (configs[1]'s sizes, d=4 as the metric
+names), with the per-replica +1 count fused into the last sweep.  Every step
+starts from the same resident synthetic s0 (one SA-style scoring pass).
+Inputs are resident in HBM before the timed region.
+
+Multi-GPU (torch.distributed.run, one rank per GPU): each rank owns its own
+graph instance and replicas (weak scaling, no data-path collective); the
+timed region is bracketed by barrier + synchronize and the max over ranks is
+reported.
+
+Secondary line items in the same JSON object:
+  * roofline of the dominant kernel (k_sweep_ell_rp) from HIP events,
+  * cpu_baseline: the numpy restatement of the reference's onestep_majority
+    (oracle/majority.py, same numpy ops as code/SA_RRG.py:18-20) on the same
+    graph, one process per core, bounded sample, rank 0 at N=1 only,
+  * sa: SA proposals/s and sweeps/s on configs[1] (d=3, N=1e6, p=2, c=1,
+    4096 replicas, full rollout per proposal).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--d", type=int, default=4)
+    ap.add_argument("--replicas", type=int, default=4096)
+    ap.add_argument("--p", type=int, default=2)
+    ap.add_argument("--c", type=int, default=1)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sa-steps", type=int, default=20)
+    ap.add_argument("--no-sa", action="store_true")
+    return ap.parse_args()
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline (runs BEFORE the GPU is touched: forked workers, no exec)
+# ---------------------------------------------------------------------------
+def _cpu_worker(args):
+    adj, steps_per_rollout, seconds, seed = args
+    from oracle import majority as orc
+    rng = np.random.default_rng(seed)
+    n = adj.shape[0]
+    done = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        s = 2 * rng.integers(0, 2, n).astype(np.int64) - 1
+        orc.s_endstate(adj, s, steps_per_rollout, 1)
+        done += 1
+    return done, time.perf_counter() - t0
+
+
+def cpu_baseline(adj, T, seconds):
+    import multiprocessing as mp
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    cores = max(1, min(16, avail, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
+    for k in ("OMP_NUM_THREADS", "MKL_NUM_THREADS", "OPENBLAS_NUM_THREADS"):
+        os.environ[k] = "1"
+    ctx = mp.get_context("fork")
+    t0 = time.perf_counter()
+    with ctx.Pool(cores) as pool:
+        res = pool.map(_cpu_worker, [(adj, T, seconds, 1000 + i) for i in range(cores)])
+    wall = time.perf_counter() - t0
+    rollouts = sum(r[0] for r in res)
+    n = adj.shape[0]
+    value = rollouts * n * T / max(r[1] for r in res)
+    return {
+        "value": value, "unit": "node-updates/s", "cores": cores, "kind": "port",
+        "sample": (f"oracle/majority.py s_endstate (numpy, same ops as code/SA_RRG.py:18-26) on the bench graph "
+                   f"(d={adj.shape[1]}, N={n}), {T} sweeps per rollout, one replica per rollout, "
+                   f"{rollouts} rollouts in ~{seconds:.0f}s per process x {cores} processes "
+                   f"(wall {wall:.1f}s)"),
+    }
+
+
+# ---------------------------------------------------------------------------
+def rocprof_traffic(kernel_prefix="k_sweep_ell_rp"):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary, if any
+    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py)."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(kernel_prefix, {}).get("bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    n, d, R = args.n, args.d, args.replicas
+    T = args.p + args.c - 1
+    W = (R + 63) // 64
+
+    import mjx
+    adj = mjx.random_regular_graph(d, n, seed=args.seed + 1000 * rank)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(adj, T, args.cpu_seconds)
+
+    import torch
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+
+    g = mjx.Graph.ell(adj)
+    gen = torch.Generator(device=dev).manual_seed(args.seed + rank)
+    s0 = torch.randint(-2 ** 62, 2 ** 62, (n * W,), dtype=torch.int64, device=dev, generator=gen)
+    out = torch.empty_like(s0)
+    tmp = torch.empty_like(s0)
+    counts = torch.zeros(W * 64, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream()
+
+    def step():
+        counts.zero_()
+        mjx.rollout(g, s0, T, words=W, out=out, tmp=tmp, counts=counts)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ev_ms = ev0.elapsed_time(ev1)
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    updates = world * n * R * T * args.steps
+    value = updates / elapsed
+
+    # roofline of the sweep kernel: algorithmic bytes per launch / avg duration.
+    # The events bracket only this stream's work: K steps x T sweeps plus one
+    # tiny memset of the counts per step.
+    bytes_per_sweep = 4 * d * n + (R // 8) * n * (d + 2)
+    sweep_s = (ev_ms / 1e3) / (args.steps * T)
+    achieved = bytes_per_sweep / sweep_s / 1e9
+    traffic = rocprof_traffic()
+
+    # sanity: the rollout of a constant state is the same constant state
+    chk = torch.full_like(s0, -1)
+    ck = torch.zeros_like(counts)
+    o2 = mjx.rollout(g, chk, T, words=W, counts=ck)
+    assert torch.equal(o2, chk) and bool((ck == n).all()), "fixed-point check failed"
+
+    sa_res = None
+    if not args.no_sa and args.sa_steps > 0:
+        sa_n, sa_d, sa_p, sa_c, sa_R = 1_000_000, 3, 2, 1, 4096
+        sa_adj = mjx.random_regular_graph(sa_d, sa_n, seed=args.seed + 7 + 1000 * rank)
+        seeds = np.arange(sa_R, dtype=np.int64) + rank * sa_R
+        t_init = time.perf_counter()
+        sa = mjx.SAReplicas(sa_adj, sa_p, sa_c, seeds)
+        sa.steps(2)
+        torch.cuda.synchronize()
+        t_init = time.perf_counter() - t_init
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        ts = time.perf_counter()
+        sa.steps(args.sa_steps)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        sa_el = time.perf_counter() - ts
+        if dist:
+            tt = torch.tensor([sa_el], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            sa_el = float(tt.item())
+        props = world * sa_R * args.sa_steps / sa_el
+        sa_res = {
+            "config": "configs[1]: d=3 RRG N=1e6 p=2 c=1, 4096 bit-packed replicas per GPU, full rollout per proposal",
+            "proposals_per_s": props,
+            "sweeps_per_s": props / sa_n,
+            "ms_per_step": 1e3 * sa_el / args.sa_steps,
+            "reference_equivalent_node_updates_per_s": props * 3 * (sa_p + sa_c - 1) * sa_n,
+            "init_s": t_init,
+            "steps": args.sa_steps,
+        }
+
+    if rank == 0:
+        line = {
+            "metric": "node-updates/s, d=4 RRG majority rollout (s_endstate + m of bit-packed replicas)",
+            "value": value,
+            "unit": "node-updates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64 bit-packed spins (int32 indices)",
+            "data": "synthetic: own random d-regular graph per rank, random +-1 spins",
+            "config": {
+                "workload": f"d={d} RRG N={n}, R={R} replicas/GPU, p={args.p} c={args.c} "
+                            f"({T} sweeps per step) + fused per-replica +1 count",
+                "n": n, "d": d, "replicas_per_gpu": R, "sweeps_per_step": T,
+                "parallelism": f"replica/instance sharding x{world}",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "k_sweep_ell_rp<4,2,*>",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "bytes_per_launch": bytes_per_sweep,
+                "avg_launch_us": sweep_s * 1e6,
+            },
+            "cpu_baseline": cpu,
+            "sa": sa_res,
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

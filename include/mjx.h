@@ -1,0 +1,140 @@
+/*
+ * mjx.h — C ABI of the MI355X majority-dynamics engine (libmjx.so).
+ *
+ * Every entry point takes plain device pointers, sizes and a hipStream_t
+ * passed as `void*` (NULL = the default stream).  Nothing here allocates,
+ * synchronises the device or throws: errors come back as an int status
+ * (MJX_OK = 0).  Kernels are hand-written HIP for gfx950.
+ *
+ * Reference interfaces replaced (paths relative to the thesis repository
+ * MarekJankola/Master-Thesis-Optimizing-Initialization-in-Graph-Dynamics-
+ * from-Ferromagnetism-to-Opinion-Consensus, "nb" = code/ER_BDCM_entropy.ipynb
+ * cited by raw JSON line):
+ *
+ *   onestep_majority(N, s0)      code/SA_RRG.py:18-20, code/HPR_pytorch_RRG.py:169-171
+ *   s_endstate(N, s0, p, c)      code/SA_RRG.py:23-26, code/HPR_pytorch_RRG.py:174-177
+ *   onestep_majority (ER)        nb:113-117,  s_endstate (ER) nb:120-123
+ *   m(s)                         code/SA_RRG.py:39-40, code/HPR_pytorch_RRG.py:179-180, nb:125-126
+ *   E_delta + SA loop body       code/SA_RRG.py:32-37, 63-88
+ *
+ * Spin layouts in HBM (bit = 1 means spin +1, bit = 0 means spin -1):
+ *
+ *   node-packed ("np", one replica): word v>>6, bit v&63 holds node v.
+ *       n_words = ceil(n/64).
+ *   replica-packed ("rp", R = 64*W replicas): word v*W + (r>>6), bit r&63
+ *       holds node v of replica r.  One node's W words are contiguous, so a
+ *       neighbour gather moves 8*W contiguous bytes.
+ *
+ * Adjacency:
+ *   ELL (random regular graphs): int32 adj[n*d], row v = neighbours of v
+ *       (the reference's `N` array, code/SA_RRG.py:9-16).
+ *   CSR (Erdos-Renyi): int64 row_ptr[n+1], int32 col[nnz].
+ */
+#ifndef MJX_H
+#define MJX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------ */
+#define MJX_OK        0
+#define MJX_EINVAL    1   /* bad argument (size, degree, null pointer ...) */
+#define MJX_EHIP      2   /* a HIP runtime call failed                     */
+#define MJX_ERANGE    3   /* size outside what the kernels support         */
+
+/* element types for pack/unpack of +-1 spin arrays */
+#define MJX_I8   1
+#define MJX_I32  4
+#define MJX_I64  8
+
+int         mjx_abi_version(void);            /* bumps on any signature change */
+const char* mjx_strerror(int status);
+const char* mjx_last_hip_error(void);         /* text of the last failing HIP call */
+
+/* ---- pack / unpack between +-1 integer arrays and bit layouts ----------- */
+/* s: (n,) +-1 of element type `dtype` -> node-packed bits[ceil(n/64)] */
+int mjx_pack_np(const void* s, int dtype, int64_t n, uint64_t* bits, void* stream);
+int mjx_unpack_np(const uint64_t* bits, int64_t n, void* s, int dtype, void* stream);
+/* s: (R, n) row-major +-1 (replica r = row r) -> replica-packed bits[n*W],
+ * W = ceil(R/64); padding replicas are written as -1 (bit 0).            */
+int mjx_pack_rp(const void* s, int dtype, int64_t n, int64_t R, uint64_t* bits, void* stream);
+int mjx_unpack_rp(const uint64_t* bits, int64_t n, int64_t R, void* s, int dtype, void* stream);
+
+/* ---- majority rollout (M1 repeated `steps` times, M2) ------------------ */
+/*
+ * s_out = onestep^steps(s_in).  For steps >= 2 `tmp` must hold a buffer of
+ * the same size as s_in (ping-pong); it may be NULL when steps <= 1.
+ * s_in may not alias s_out or tmp.  steps == 0 copies.
+ * counts (nullable): per-replica number of +1 spins in s_out, ADDED into
+ * counts[R] (uint64; caller zeroes it) — the popcount is fused into the last
+ * sweep.  For the np layout R = 1 and counts[0] receives the total.
+ */
+int mjx_rollout_ell_np(const int32_t* adj, int64_t n, int d,
+                       const uint64_t* s_in, uint64_t* s_out, uint64_t* tmp,
+                       int steps, unsigned long long* counts, void* stream);
+int mjx_rollout_ell_rp(const int32_t* adj, int64_t n, int d, int64_t words,
+                       const uint64_t* s_in, uint64_t* s_out, uint64_t* tmp,
+                       int steps, unsigned long long* counts, void* stream);
+int mjx_rollout_csr_np(const int64_t* row_ptr, const int32_t* col, int64_t n,
+                       const uint64_t* s_in, uint64_t* s_out, uint64_t* tmp,
+                       int steps, unsigned long long* counts, void* stream);
+int mjx_rollout_csr_rp(const int64_t* row_ptr, const int32_t* col, int64_t n, int64_t words,
+                       const uint64_t* s_in, uint64_t* s_out, uint64_t* tmp,
+                       int steps, unsigned long long* counts, void* stream);
+
+/* per-replica count of +1 spins, ADDED into counts (m(s) = (2*count-n)/n) */
+int mjx_popcount_np(const uint64_t* bits, int64_t n, unsigned long long* counts, void* stream);
+int mjx_popcount_rp(const uint64_t* bits, int64_t n, int64_t words,
+                    unsigned long long* counts, void* stream);
+
+/* ---- simulated annealing (code/SA_RRG.py:44-92), R = 64*W replicas ------ */
+/*
+ * Per-replica state, all device arrays of length R unless noted.  Replica r
+ * replays numpy's legacy global MT19937 after np.random.seed(seeds[r]):
+ * binomial(1,.5,n) for s0 (code/SA_RRG.py:65), then per step
+ * randint(0,n) (:73) and rand() (:76).
+ */
+typedef struct mjx_sa_state {
+    uint32_t* mt;        /* [R*624] MT19937 words, replica-major: mt[r*624 + k] */
+    int32_t*  mt_idx;    /* [R] next word index (624 = twist pending)        */
+    double*   a;         /* [R] annealing weight a (code/SA_RRG.py:67,80)    */
+    double*   b;         /* [R] annealing weight b (:68,81)                  */
+    int64_t*  t;         /* [R] proposals made (:82)                         */
+    int64_t*  sum_end;   /* [R] sum of s_endstate(s) over nodes (+-1 sum)    */
+    int32_t*  done;      /* [R] 0 running, 1 consensus reached, 2 cap hit    */
+    int32_t*  prop_i;    /* [R] scratch: proposed node                       */
+    int8_t*   prop_s;    /* [R] scratch: spin of the proposed node before the flip */
+    double*   prop_u;    /* [R] scratch: accept uniform                      */
+    unsigned long long* cnt; /* [R] scratch: +1 count of the rolled-out proposal */
+    /* optional per-step trace (NULL to disable); row k = step k of this call */
+    int32_t*  tr_i;      /* [nsteps*R] proposed node (-1 if replica done)    */
+    int8_t*   tr_acc;    /* [nsteps*R] 1 accepted, 0 rejected, -1 done       */
+    int64_t*  tr_sum;    /* [nsteps*R] sum_end after the step               */
+    double*   tr_dE;     /* [nsteps*R] delta_H (code/SA_RRG.py:74)          */
+    int32_t*  tr_tie;    /* [R] count of |u - exp(-dE)| < 4 ulp near-ties    */
+} mjx_sa_state;
+
+/* Seed replica r with seeds[r] (device uint32[R]), draw s0 into the
+ * replica-packed spins s[n*W], set a=a0, b=b0, t=0, done=0, and
+ * sum_end = sum(s_endstate(s0)) using tmp1/tmp2 ([n*W] each). */
+int mjx_sa_init(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R,
+                const uint32_t* seeds, double a0, double b0,
+                uint64_t* s, uint64_t* tmp1, uint64_t* tmp2,
+                mjx_sa_state* st, void* stream);
+
+/* Advance every running replica by `nsteps` proposals (code/SA_RRG.py:72-85),
+ * full rollout of each proposal.  par_a/par_b: annealing factors (:49-50);
+ * a_cap = 4.5*n, b_cap = 5*n (:80-81); t_cap = 2*n**3 (:84). */
+int mjx_sa_steps(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R,
+                 uint64_t* s, uint64_t* tmp1, uint64_t* tmp2,
+                 mjx_sa_state* st, int64_t nsteps,
+                 double par_a, double par_b, double a_cap, double b_cap, int64_t t_cap,
+                 void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MJX_H */

@@ -1,0 +1,25 @@
+"""mjx — MI355X-native engine for majority-rule (zero-temperature Ising,
+always-stay) dynamics on random regular and Erdos-Renyi graphs, the
+data-parallel hot path of the thesis code.
+
+Every compute entry point calls hand-written HIP kernels (libmjx.so, gfx950)
+through the C ABI in include/mjx.h.  There is no CPU fallback.
+"""
+from . import _lib
+from ._lib import MjxError, lib_path
+from .graph import (Graph, neighbours, csr_from_networkx, random_regular_graph, random_regular_edges,
+                    erdos_renyi, erdos_renyi_edges, csr_from_edges, remove_isolated)
+from .dynamics import onestep_majority, s_endstate, m, pack, unpack, rollout, popcount, as_graph
+from .sa import SAReplicas, E_delta, sa_run, schedule_constants
+
+__all__ = [
+    "MjxError", "lib_path", "Graph", "neighbours", "csr_from_networkx", "random_regular_graph",
+    "random_regular_edges", "erdos_renyi", "erdos_renyi_edges", "csr_from_edges", "remove_isolated",
+    "onestep_majority", "s_endstate", "m", "pack", "unpack", "rollout", "popcount", "as_graph",
+    "SAReplicas", "E_delta", "sa_run", "schedule_constants",
+]
+
+
+def load_library():
+    """Load libmjx.so (raises MjxError if it has not been built)."""
+    return _lib.load()

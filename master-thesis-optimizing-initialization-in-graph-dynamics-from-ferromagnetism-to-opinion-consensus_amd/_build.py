@@ -1,0 +1,69 @@
+"""Build libmjx.so (hand-written HIP for gfx950) in-tree with hipcc.
+
+Each translation unit is compiled separately because the simulated-annealing
+unit needs ``-ffp-contract=off`` (delta_H must round each operation as numpy
+does, code/SA_RRG.py:37) while the dynamics unit does not care.
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG_DIR, "csrc")
+INCLUDE = os.path.normpath(os.path.join(PKG_DIR, "..", "include"))
+LIB = os.path.join(PKG_DIR, "libmjx.so")
+ARCH = "gfx950"
+
+# (source, extra flags)
+UNITS = [
+    ("mjx_dynamics.hip", []),
+    ("mjx_sa.hip", ["-ffp-contract=off"]),
+]
+
+
+def _hipcc():
+    for cand in (shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found: libmjx.so cannot be built")
+
+
+def _stale():
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)]
+    deps.append(os.path.join(INCLUDE, "mjx.h"))
+    deps.append(os.path.abspath(__file__))
+    return any(os.path.getmtime(p) > t for p in deps if os.path.exists(p))
+
+
+def build(force=False, verbose=True):
+    """Compile every HIP unit for gfx950 and link libmjx.so next to this file."""
+    if not force and not _stale():
+        return LIB
+    hipcc = _hipcc()
+    objdir = os.path.join(PKG_DIR, "build")
+    os.makedirs(objdir, exist_ok=True)
+    base = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
+            "-Wno-unused-function", "-I", INCLUDE]
+    objs = []
+    for src, extra in UNITS:
+        obj = os.path.join(objdir, src.replace(".hip", ".o"))
+        cmd = base + extra + ["-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        objs.append(obj)
+    tmp = LIB + ".tmp"
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

@@ -1,0 +1,93 @@
+"""ctypes binding of libmjx.so — the C ABI declared in include/mjx.h.
+
+This is exactly the binding a maintainer of the reference would add
+(INTEGRATION.md): plain pointers, sizes and a hipStream_t.  There is no CPU
+fallback: if the library or a GPU is missing every compute entry point raises.
+"""
+import ctypes
+import os
+
+from . import _build
+
+_LIB = None
+
+c_i64 = ctypes.c_int64
+c_int = ctypes.c_int
+c_dbl = ctypes.c_double
+c_vp = ctypes.c_void_p
+
+# name -> argtypes (restype is c_int unless listed in _RESTYPES)
+SIGNATURES = {
+    "mjx_abi_version": [],
+    "mjx_strerror": [c_int],
+    "mjx_last_hip_error": [],
+    "mjx_pack_np": [c_vp, c_int, c_i64, c_vp, c_vp],
+    "mjx_unpack_np": [c_vp, c_i64, c_vp, c_int, c_vp],
+    "mjx_pack_rp": [c_vp, c_int, c_i64, c_i64, c_vp, c_vp],
+    "mjx_unpack_rp": [c_vp, c_i64, c_i64, c_vp, c_int, c_vp],
+    "mjx_rollout_ell_np": [c_vp, c_i64, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp],
+    "mjx_rollout_ell_rp": [c_vp, c_i64, c_int, c_i64, c_vp, c_vp, c_vp, c_int, c_vp, c_vp],
+    "mjx_rollout_csr_np": [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_int, c_vp, c_vp],
+    "mjx_rollout_csr_rp": [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_int, c_vp, c_vp],
+    "mjx_popcount_np": [c_vp, c_i64, c_vp, c_vp],
+    "mjx_popcount_rp": [c_vp, c_i64, c_i64, c_vp, c_vp],
+    "mjx_sa_init": [c_vp, c_i64, c_int, c_int, c_int, c_i64, c_vp, c_dbl, c_dbl,
+                    c_vp, c_vp, c_vp, c_vp, c_vp],
+    "mjx_sa_steps": [c_vp, c_i64, c_int, c_int, c_int, c_i64, c_vp, c_vp, c_vp, c_vp,
+                     c_i64, c_dbl, c_dbl, c_dbl, c_dbl, c_i64, c_vp],
+}
+_RESTYPES = {"mjx_strerror": ctypes.c_char_p, "mjx_last_hip_error": ctypes.c_char_p}
+
+MJX_I8, MJX_I32, MJX_I64 = 1, 4, 8
+
+
+class MjxSaState(ctypes.Structure):
+    """Mirror of ``mjx_sa_state`` in include/mjx.h (field order matters)."""
+    _fields_ = [
+        ("mt", c_vp), ("mt_idx", c_vp), ("a", c_vp), ("b", c_vp), ("t", c_vp),
+        ("sum_end", c_vp), ("done", c_vp), ("prop_i", c_vp), ("prop_s", c_vp),
+        ("prop_u", c_vp), ("cnt", c_vp),
+        ("tr_i", c_vp), ("tr_acc", c_vp), ("tr_sum", c_vp), ("tr_dE", c_vp), ("tr_tie", c_vp),
+    ]
+
+
+class MjxError(RuntimeError):
+    pass
+
+
+def lib_path():
+    return _build.LIB
+
+
+def load(build_if_missing=False):
+    """Load libmjx.so and declare every entry point.  Raises if it is absent."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    path = _build.LIB
+    if not os.path.exists(path):
+        if build_if_missing:
+            _build.build()
+        else:
+            raise MjxError(f"libmjx.so not found at {path}: run __graft_entry__.build() "
+                           "(there is no CPU fallback for the majority-dynamics kernels)")
+    lib = ctypes.CDLL(path)
+    for name, argtypes in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = _RESTYPES.get(name, c_int)
+    _LIB = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != 0:
+        lib = load()
+        msg = lib.mjx_strerror(rc).decode()
+        hip = lib.mjx_last_hip_error().decode()
+        raise MjxError(f"{what} failed: {msg} (status {rc}){'; ' + hip if hip else ''}")
+
+
+def call(name, *args):
+    lib = load()
+    check(getattr(lib, name)(*args), name)

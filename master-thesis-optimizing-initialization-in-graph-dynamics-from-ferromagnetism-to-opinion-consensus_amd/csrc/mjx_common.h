@@ -1,0 +1,128 @@
+// Shared helpers for the libmjx HIP translation units (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/mjx.h"
+
+namespace mjx {
+
+typedef unsigned long long u64;
+
+// Records the text of the last failing HIP call (read via mjx_last_hip_error).
+void set_hip_error(hipError_t e, const char* where);
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Launch-check: kernel launches are asynchronous; only the launch itself is
+// checked here (no device synchronisation inside any entry point).
+#define MJX_LAUNCH_CHECK(where)                                   \
+    do {                                                          \
+        hipError_t _e = hipGetLastError();                        \
+        if (_e != hipSuccess) { mjx::set_hip_error(_e, where); return MJX_EHIP; } \
+    } while (0)
+
+#define MJX_HIP(call, where)                                      \
+    do {                                                          \
+        hipError_t _e = (call);                                   \
+        if (_e != hipSuccess) { mjx::set_hip_error(_e, where); return MJX_EHIP; } \
+    } while (0)
+
+constexpr int kBlock = 256;          // 4 waves of 64
+constexpr int kCUs = 256;            // MI355X: 8 XCDs x 32 CUs
+
+inline int grid_for(int64_t items, int per_cu = 8) {
+    int64_t g = (items + kBlock - 1) / kBlock;
+    int64_t cap = (int64_t)kCUs * per_cu;
+    if (g > cap) g = cap;
+    if (g < 1) g = 1;
+    return (int)g;
+}
+
+// Bit-sliced majority with always-stay tie breaking (code/SA_RRG.py:19-20):
+// new = +1 if 2*cnt > d, -1 if 2*cnt < d, old if 2*cnt == d, where cnt is the
+// number of +1 neighbours.  Every bit lane of a word is an independent node
+// (np layout) or replica (rp layout).
+template <int D>
+__device__ __forceinline__ u64 majority_fixed(const u64* x, u64 own) {
+    if constexpr (D == 1) {
+        return x[0];
+    } else if constexpr (D == 2) {
+        return (x[0] & x[1]) | ((x[0] ^ x[1]) & own);
+    } else if constexpr (D == 3) {
+        return (x[0] & x[1]) | (x[2] & (x[0] | x[1]));
+    } else if constexpr (D == 4) {
+        // ge3 = at least three ones; ge2 = at least two ones
+        u64 ab_and = x[0] & x[1], ab_or = x[0] | x[1];
+        u64 cd_and = x[2] & x[3], cd_or = x[2] | x[3];
+        u64 ge3 = (ab_and & cd_or) | (cd_and & ab_or);
+        u64 ge2 = ab_and | cd_and | (ab_or & cd_or);
+        return ge3 | (ge2 & own);
+    } else {
+        // generic: bit-sliced ripple counter then compare with d/2
+        constexpr int K = (D < 2) ? 1 : (D < 4) ? 2 : (D < 8) ? 3 : (D < 16) ? 4 : (D < 32) ? 5 : (D < 64) ? 6 : 7;
+        u64 c[K];
+#pragma unroll
+        for (int p = 0; p < K; ++p) c[p] = 0;
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            u64 carry = x[j];
+#pragma unroll
+            for (int p = 0; p < K; ++p) {
+                u64 t = c[p] & carry;
+                c[p] ^= carry;
+                carry = t;
+            }
+        }
+        constexpr int H = D / 2;     // compare cnt with floor(d/2)
+        u64 gt = 0, eq = ~0ull;
+#pragma unroll
+        for (int p = K - 1; p >= 0; --p) {
+            if ((H >> p) & 1) {
+                eq &= c[p];
+            } else {
+                gt |= eq & c[p];
+                eq &= ~c[p];
+            }
+        }
+        if constexpr ((D & 1) == 0) return gt | (eq & own);
+        else return gt;  // odd degree: 2*cnt == d impossible (eq means cnt == floor(d/2) -> minority)
+    }
+}
+
+// Runtime-degree version for CSR rows (nb:113-117, sign(2S+s)): counter with
+// KB bit planes (degree <= 2^KB - 1).
+template <int KB>
+struct BitCounter {
+    u64 c[KB];
+    __device__ __forceinline__ void reset() {
+#pragma unroll
+        for (int p = 0; p < KB; ++p) c[p] = 0;
+    }
+    __device__ __forceinline__ void add(u64 x) {
+        u64 carry = x;
+#pragma unroll
+        for (int p = 0; p < KB; ++p) {
+            u64 t = c[p] & carry;
+            c[p] ^= carry;
+            carry = t;
+        }
+    }
+    // new spin word for a node of degree `deg`
+    __device__ __forceinline__ u64 majority(int deg, u64 own) const {
+        const int h = deg >> 1;
+        u64 gt = 0, eq = ~0ull;
+#pragma unroll
+        for (int p = KB - 1; p >= 0; --p) {
+            if ((h >> p) & 1) {
+                eq &= c[p];
+            } else {
+                gt |= eq & c[p];
+                eq &= ~c[p];
+            }
+        }
+        // cnt == floor(d/2): for even d a tie (keep own), for odd d a loss
+        return (deg & 1) ? gt : (gt | (eq & own));
+    }
+};
+
+}  // namespace mjx

@@ -1,0 +1,770 @@
+// Majority-rule dynamics on bit-packed spins: pack/unpack, ELL (RRG) and CSR
+// (Erdos-Renyi) rollouts, fused per-replica magnetisation counts.
+//
+// Semantics (M1/M2 of SURVEY.md 0.1): one synchronous step sets
+//   s'_i = sign(S_i) if S_i != 0 else s_i,  S_i = sum_{k in N(i)} s_k
+// (code/SA_RRG.py:18-20, code/HPR_pytorch_RRG.py:169-171, nb:113-117), and a
+// rollout applies p+c-1 such steps (code/SA_RRG.py:23-26).  Integer exact, so
+// the only thing parity depends on is the edge set.
+//
+// HBM-bound by design: per node and sweep the kernels read d int32 indices,
+// gather d neighbour state rows, read the node's own row and write one row.
+#include "mjx_common.h"
+#include <string.h>
+#include <stdio.h>
+
+namespace mjx {
+
+static thread_local char g_hip_err[256] = "";
+
+void set_hip_error(hipError_t e, const char* where) {
+    snprintf(g_hip_err, sizeof(g_hip_err), "%s: %s (%d)", where, hipGetErrorString(e), (int)e);
+}
+
+// ---------------------------------------------------------------------------
+// pack / unpack
+// ---------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ bool is_plus(const T* s, int64_t i) { return s[i] > 0; }
+
+template <typename T>
+__global__ void __launch_bounds__(kBlock) k_pack_np(const T* __restrict__ s, int64_t n, u64* __restrict__ bits) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nwords = (n + 63) >> 6;
+    const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
+    for (int64_t w = wave; w < nwords; w += nwaves) {
+        int64_t v = (w << 6) + lane;
+        bool b = (v < n) && is_plus(s, v);
+        u64 word = __ballot(b);
+        if (lane == 0) bits[w] = word;
+    }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kBlock) k_unpack_np(const u64* __restrict__ bits, int64_t n, T* __restrict__ s) {
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x; v < n; v += stride) {
+        u64 w = bits[v >> 6];
+        s[v] = ((w >> (v & 63)) & 1ull) ? T(1) : T(-1);
+    }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kBlock) k_pack_rp(const T* __restrict__ s, int64_t n, int64_t R, int64_t W,
+                                                    u64* __restrict__ bits) {
+    const int64_t total = n * W;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x; t < total; t += stride) {
+        const int64_t v = t % n, w = t / n;   // node fastest: coalesced reads of s
+        u64 word = 0;
+        for (int b = 0; b < 64; ++b) {
+            int64_t r = w * 64 + b;
+            if (r < R && is_plus(s, r * n + v)) word |= (1ull << b);
+        }
+        bits[v * W + w] = word;
+    }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kBlock) k_unpack_rp(const u64* __restrict__ bits, int64_t n, int64_t R, int64_t W,
+                                                      T* __restrict__ s) {
+    const int64_t total = n * W;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x; t < total; t += stride) {
+        const int64_t v = t % n, w = t / n;
+        const u64 word = bits[v * W + w];
+        for (int b = 0; b < 64; ++b) {
+            int64_t r = w * 64 + b;
+            if (r < R) s[r * n + v] = ((word >> b) & 1ull) ? T(1) : T(-1);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// per-thread vertical counter: counts, per bit position, the ones seen in the
+// words added to it (bit-sliced ripple counter, KC planes, flushed to LDS
+// before it can overflow).
+// ---------------------------------------------------------------------------
+constexpr int KC = 8;                 // planes -> up to 255 words between flushes
+constexpr int kMaxLdsReplicas = 8192; // 32 KiB of LDS counters per block
+
+template <int VW>
+struct VertCounter {
+    u64 c[VW][KC];
+    int added;
+    __device__ __forceinline__ void reset() {
+#pragma unroll
+        for (int j = 0; j < VW; ++j)
+#pragma unroll
+            for (int p = 0; p < KC; ++p) c[j][p] = 0;
+        added = 0;
+    }
+    __device__ __forceinline__ void add(const u64* x) {
+#pragma unroll
+        for (int j = 0; j < VW; ++j) {
+            u64 carry = x[j];
+#pragma unroll
+            for (int p = 0; p < KC; ++p) {
+                u64 t = c[j][p] & carry;
+                c[j][p] ^= carry;
+                carry = t;
+            }
+        }
+        ++added;
+    }
+    // add the per-bit counts into dst[j*64 + b] (LDS or global)
+    template <typename DST>
+    __device__ __forceinline__ void flush(DST* dst) {
+#pragma unroll
+        for (int j = 0; j < VW; ++j) {
+            for (int b = 0; b < 64; ++b) {
+                unsigned cnt = 0;
+#pragma unroll
+                for (int p = 0; p < KC; ++p) cnt |= (unsigned)((c[j][p] >> b) & 1ull) << p;
+                if (cnt) atomicAdd(&dst[j * 64 + b], (DST)cnt);
+            }
+        }
+        reset();
+    }
+};
+
+// ---------------------------------------------------------------------------
+// node-packed (one replica) ELL sweep: a wave owns 64 consecutive nodes = one
+// output word; each lane gathers its node's d neighbour bits.
+// ---------------------------------------------------------------------------
+template <int D>
+__device__ __forceinline__ void load_adj(const int32_t* __restrict__ adj, int64_t v, int32_t* k) {
+    if constexpr (D == 4) {
+        int4 a = *reinterpret_cast<const int4*>(adj + v * 4);
+        k[0] = a.x; k[1] = a.y; k[2] = a.z; k[3] = a.w;
+    } else if constexpr (D == 2) {
+        int2 a = *reinterpret_cast<const int2*>(adj + v * 2);
+        k[0] = a.x; k[1] = a.y;
+    } else if constexpr (D == 6) {
+        const int2* p = reinterpret_cast<const int2*>(adj + v * 6);
+        int2 a = p[0], b = p[1], c = p[2];
+        k[0] = a.x; k[1] = a.y; k[2] = b.x; k[3] = b.y; k[4] = c.x; k[5] = c.y;
+    } else {
+#pragma unroll
+        for (int j = 0; j < D; ++j) k[j] = adj[v * D + j];
+    }
+}
+
+template <int D>
+__global__ void __launch_bounds__(kBlock) k_sweep_ell_np(const int32_t* __restrict__ adj, int64_t n,
+                                                         const uint32_t* __restrict__ s_in32,
+                                                         u64* __restrict__ s_out,
+                                                         unsigned long long* __restrict__ counts) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nwords = (n + 63) >> 6;
+    const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
+    unsigned long long ones = 0;
+    for (int64_t w = wave; w < nwords; w += nwaves) {
+        const int64_t v = (w << 6) + lane;
+        bool nb = false;
+        if (v < n) {
+            int32_t k[D];
+            load_adj<D>(adj, v, k);
+            int cnt = 0;
+#pragma unroll
+            for (int j = 0; j < D; ++j) cnt += (s_in32[k[j] >> 5] >> (k[j] & 31)) & 1u;
+            const int own = (s_in32[v >> 5] >> (v & 31)) & 1u;
+            nb = (2 * cnt > D) || ((2 * cnt == D) && own);
+        }
+        const u64 word = __ballot(nb);
+        if (lane == 0) {
+            s_out[w] = word;
+            ones += __popcll(word);
+        }
+    }
+    if (counts) {
+        __shared__ unsigned long long red[kBlock / 64];
+        if (lane == 0) red[threadIdx.x >> 6] = ones;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long tot = 0;
+            for (int i = 0; i < kBlock / 64; ++i) tot += red[i];
+            if (tot) atomicAdd(counts, tot);
+        }
+    }
+}
+
+// runtime-degree node-packed ELL sweep (degrees other than the specialised ones)
+__global__ void __launch_bounds__(kBlock) k_sweep_ell_np_dyn(const int32_t* __restrict__ adj, int64_t n, int d,
+                                                             const uint32_t* __restrict__ s_in32,
+                                                             u64* __restrict__ s_out,
+                                                             unsigned long long* __restrict__ counts) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nwords = (n + 63) >> 6;
+    const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
+    unsigned long long ones = 0;
+    for (int64_t w = wave; w < nwords; w += nwaves) {
+        const int64_t v = (w << 6) + lane;
+        bool nb = false;
+        if (v < n) {
+            int cnt = 0;
+            for (int j = 0; j < d; ++j) {
+                int32_t k = adj[v * d + j];
+                cnt += (s_in32[k >> 5] >> (k & 31)) & 1u;
+            }
+            const int own = (s_in32[v >> 5] >> (v & 31)) & 1u;
+            nb = (2 * cnt > d) || ((2 * cnt == d) && own);
+        }
+        const u64 word = __ballot(nb);
+        if (lane == 0) {
+            s_out[w] = word;
+            ones += __popcll(word);
+        }
+    }
+    if (counts) {
+        __shared__ unsigned long long red[kBlock / 64];
+        if (lane == 0) red[threadIdx.x >> 6] = ones;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long tot = 0;
+            for (int i = 0; i < kBlock / 64; ++i) tot += red[i];
+            if (tot) atomicAdd(counts, tot);
+        }
+    }
+}
+
+// node-packed CSR sweep (nb:113-117: sign(2S+s), same as always-stay)
+__global__ void __launch_bounds__(kBlock) k_sweep_csr_np(const int64_t* __restrict__ row_ptr,
+                                                         const int32_t* __restrict__ col, int64_t n,
+                                                         const uint32_t* __restrict__ s_in32,
+                                                         u64* __restrict__ s_out,
+                                                         unsigned long long* __restrict__ counts) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nwords = (n + 63) >> 6;
+    const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
+    unsigned long long ones = 0;
+    for (int64_t w = wave; w < nwords; w += nwaves) {
+        const int64_t v = (w << 6) + lane;
+        bool nb = false;
+        if (v < n) {
+            const int64_t b = row_ptr[v], e = row_ptr[v + 1];
+            const int d = (int)(e - b);
+            int cnt = 0;
+            for (int64_t j = b; j < e; ++j) {
+                int32_t k = col[j];
+                cnt += (s_in32[k >> 5] >> (k & 31)) & 1u;
+            }
+            const int own = (s_in32[v >> 5] >> (v & 31)) & 1u;
+            nb = (2 * cnt > d) || ((2 * cnt == d) && own);
+        }
+        const u64 word = __ballot(nb);
+        if (lane == 0) {
+            s_out[w] = word;
+            ones += __popcll(word);
+        }
+    }
+    if (counts) {
+        __shared__ unsigned long long red[kBlock / 64];
+        if (lane == 0) red[threadIdx.x >> 6] = ones;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long tot = 0;
+            for (int i = 0; i < kBlock / 64; ++i) tot += red[i];
+            if (tot) atomicAdd(counts, tot);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// replica-packed sweeps.  A node's W words are split into U = W/VW units of
+// VW words (16-B loads when VW == 2).  Thread t owns unit t % U of the nodes
+// slot, slot+slots, ... so its replica range is fixed (needed by the fused
+// counter).
+// ---------------------------------------------------------------------------
+template <int VW> struct VecT;
+template <> struct VecT<1> { typedef u64 T; };
+template <> struct VecT<2> { typedef ulonglong2 T; };
+
+template <int VW>
+__device__ __forceinline__ void ldv(const u64* __restrict__ p, u64* x) {
+    if constexpr (VW == 2) {
+        ulonglong2 v = *reinterpret_cast<const ulonglong2*>(p);
+        x[0] = v.x; x[1] = v.y;
+    } else {
+        x[0] = *p;
+    }
+}
+template <int VW>
+__device__ __forceinline__ void stv(u64* __restrict__ p, const u64* x) {
+    if constexpr (VW == 2) {
+        *reinterpret_cast<ulonglong2*>(p) = make_ulonglong2(x[0], x[1]);
+    } else {
+        *p = x[0];
+    }
+}
+
+template <int VW>
+__device__ __forceinline__ void flush_to(VertCounter<VW>& vc, int use_lds, unsigned* lds,
+                                         unsigned long long* counts, int64_t unit) {
+    if (use_lds) vc.flush(lds + unit * VW * 64);
+    else vc.flush(counts + unit * VW * 64);
+}
+
+// Shared epilogue for the fused per-replica counts.
+template <int VW, bool COUNT>
+__device__ __forceinline__ void count_epilogue(VertCounter<VW>& vc, bool active, int64_t unit, int64_t W,
+                                               unsigned* lds, bool use_lds,
+                                               unsigned long long* __restrict__ counts) {
+    if constexpr (COUNT) {
+        const int64_t R = W * 64;
+        if (use_lds) {
+            if (active && vc.added) vc.flush(lds + unit * VW * 64);
+            __syncthreads();  // every thread of the block reaches this (no early return)
+            for (int64_t r = threadIdx.x; r < R; r += kBlock) {
+                unsigned x = lds[r];
+                if (x) atomicAdd(&counts[r], (unsigned long long)x);
+            }
+        } else {
+            if (active && vc.added) vc.flush(counts + unit * VW * 64);
+        }
+    }
+}
+
+template <int D, int VW, bool COUNT>
+__global__ void __launch_bounds__(kBlock) k_sweep_ell_rp(const int32_t* __restrict__ adj, int64_t n, int64_t W,
+                                                         const u64* __restrict__ s_in, u64* __restrict__ s_out,
+                                                         unsigned long long* __restrict__ counts, int use_lds) {
+    extern __shared__ unsigned lds_cnt[];
+    const int64_t U = W / VW;
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t slots = ((int64_t)gridDim.x * kBlock) / U;
+    const int64_t unit = t % U, slot = t / U;
+    const bool active = slot < slots;
+    VertCounter<VW> vc;
+    if constexpr (COUNT) {
+        vc.reset();
+        if (use_lds) {
+            for (int64_t r = threadIdx.x; r < W * 64; r += kBlock) lds_cnt[r] = 0;
+            __syncthreads();
+        }
+    }
+    if (active) {
+        for (int64_t v = slot; v < n; v += slots) {
+            int32_t k[D];
+            load_adj<D>(adj, v, k);
+            u64 x[D][VW], own[VW], out[VW];
+#pragma unroll
+            for (int j = 0; j < D; ++j) ldv<VW>(s_in + (int64_t)k[j] * W + unit * VW, x[j]);
+            ldv<VW>(s_in + v * W + unit * VW, own);
+#pragma unroll
+            for (int q = 0; q < VW; ++q) {
+                u64 xs[D];
+#pragma unroll
+                for (int j = 0; j < D; ++j) xs[j] = x[j][q];
+                out[q] = majority_fixed<D>(xs, own[q]);
+            }
+            stv<VW>(s_out + v * W + unit * VW, out);
+            if constexpr (COUNT) {
+                vc.add(out);
+                if (vc.added == (1 << KC) - 1) flush_to<VW>(vc, use_lds, lds_cnt, counts, unit);
+            }
+        }
+    }
+    count_epilogue<VW, COUNT>(vc, active, unit, W, lds_cnt, use_lds, counts);
+}
+
+// runtime degree (ELL rows of length d) and CSR rows; KB counter planes
+template <int VW, bool COUNT, bool CSR>
+__global__ void __launch_bounds__(kBlock) k_sweep_gen_rp(const int32_t* __restrict__ adj, int d,
+                                                         const int64_t* __restrict__ row_ptr,
+                                                         const int32_t* __restrict__ col, int64_t n, int64_t W,
+                                                         const u64* __restrict__ s_in, u64* __restrict__ s_out,
+                                                         unsigned long long* __restrict__ counts, int use_lds) {
+    extern __shared__ unsigned lds_cnt[];
+    const int64_t U = W / VW;
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t slots = ((int64_t)gridDim.x * kBlock) / U;
+    const int64_t unit = t % U, slot = t / U;
+    const bool active = slot < slots;
+    VertCounter<VW> vc;
+    if constexpr (COUNT) {
+        vc.reset();
+        if (use_lds) {
+            for (int64_t r = threadIdx.x; r < W * 64; r += kBlock) lds_cnt[r] = 0;
+            __syncthreads();
+        }
+    }
+    if (active) {
+        for (int64_t v = slot; v < n; v += slots) {
+            int64_t b, e;
+            const int32_t* nbr;
+            if constexpr (CSR) {
+                b = row_ptr[v]; e = row_ptr[v + 1]; nbr = col;
+            } else {
+                b = v * d; e = b + d; nbr = adj;
+            }
+            const int deg = (int)(e - b);
+            BitCounter<8> bc[VW];
+#pragma unroll
+            for (int q = 0; q < VW; ++q) bc[q].reset();
+            for (int64_t j = b; j < e; ++j) {
+                u64 x[VW];
+                ldv<VW>(s_in + (int64_t)nbr[j] * W + unit * VW, x);
+#pragma unroll
+                for (int q = 0; q < VW; ++q) bc[q].add(x[q]);
+            }
+            u64 own[VW], out[VW];
+            ldv<VW>(s_in + v * W + unit * VW, own);
+#pragma unroll
+            for (int q = 0; q < VW; ++q) out[q] = bc[q].majority(deg, own[q]);
+            stv<VW>(s_out + v * W + unit * VW, out);
+            if constexpr (COUNT) {
+                vc.add(out);
+                if (vc.added == (1 << KC) - 1) flush_to<VW>(vc, use_lds, lds_cnt, counts, unit);
+            }
+        }
+    }
+    count_epilogue<VW, COUNT>(vc, active, unit, W, lds_cnt, use_lds, counts);
+}
+
+}  // namespace mjx
+
+// ---------------------------------------------------------------------------
+// standalone per-replica popcount
+// ---------------------------------------------------------------------------
+namespace mjx {
+
+__global__ void __launch_bounds__(kBlock) k_popcount_np(const u64* __restrict__ bits, int64_t n,
+                                                        unsigned long long* __restrict__ counts) {
+    const int64_t nwords = (n + 63) >> 6;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    unsigned long long ones = 0;
+    for (int64_t w = (int64_t)blockIdx.x * kBlock + threadIdx.x; w < nwords; w += stride) {
+        u64 x = bits[w];
+        if (w == nwords - 1 && (n & 63)) x &= (1ull << (n & 63)) - 1ull;  // padding nodes
+        ones += __popcll(x);
+    }
+    // wave reduction then one atomic per wave
+    for (int off = 32; off > 0; off >>= 1) ones += __shfl_down(ones, off, 64);
+    if ((threadIdx.x & 63) == 0 && ones) atomicAdd(counts, ones);
+}
+
+template <int VW>
+__global__ void __launch_bounds__(kBlock) k_popcount_rp(const u64* __restrict__ bits, int64_t n, int64_t W,
+                                                        unsigned long long* __restrict__ counts, int use_lds) {
+    extern __shared__ unsigned lds_cnt[];
+    const int64_t U = W / VW;
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t slots = ((int64_t)gridDim.x * kBlock) / U;
+    const int64_t unit = t % U, slot = t / U;
+    const bool active = slot < slots;
+    VertCounter<VW> vc;
+    vc.reset();
+    if (use_lds) {
+        for (int64_t r = threadIdx.x; r < W * 64; r += kBlock) lds_cnt[r] = 0;
+        __syncthreads();
+    }
+    if (active) {
+        for (int64_t v = slot; v < n; v += slots) {
+            u64 x[VW];
+            ldv<VW>(bits + v * W + unit * VW, x);
+            vc.add(x);
+            if (vc.added == (1 << KC) - 1) flush_to<VW>(vc, use_lds, lds_cnt, counts, unit);
+        }
+    }
+    count_epilogue<VW, true>(vc, active, unit, W, lds_cnt, use_lds, counts);
+}
+
+}  // namespace mjx
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+using namespace mjx;
+
+extern "C" int mjx_abi_version(void) { return 1; }
+
+extern "C" const char* mjx_strerror(int status) {
+    switch (status) {
+        case MJX_OK: return "ok";
+        case MJX_EINVAL: return "invalid argument";
+        case MJX_EHIP: return "HIP runtime error";
+        case MJX_ERANGE: return "size out of supported range";
+        default: return "unknown status";
+    }
+}
+
+extern "C" const char* mjx_last_hip_error(void) { return g_hip_err; }
+
+template <typename F8, typename F32, typename F64>
+static int dispatch_dtype(int dtype, F8 f8, F32 f32, F64 f64) {
+    switch (dtype) {
+        case MJX_I8: return f8();
+        case MJX_I32: return f32();
+        case MJX_I64: return f64();
+        default: return MJX_EINVAL;
+    }
+}
+
+extern "C" int mjx_pack_np(const void* s, int dtype, int64_t n, uint64_t* bits, void* stream) {
+    if (n < 0 || (n > 0 && (!s || !bits))) return MJX_EINVAL;
+    if (n == 0) return MJX_OK;
+    const int64_t nwords = (n + 63) / 64;
+    const int grid = grid_for(nwords * 64);
+    hipStream_t st = as_stream(stream);
+    int rc = dispatch_dtype(dtype,
+        [&] { k_pack_np<int8_t><<<grid, kBlock, 0, st>>>((const int8_t*)s, n, (u64*)bits); return 0; },
+        [&] { k_pack_np<int32_t><<<grid, kBlock, 0, st>>>((const int32_t*)s, n, (u64*)bits); return 0; },
+        [&] { k_pack_np<int64_t><<<grid, kBlock, 0, st>>>((const int64_t*)s, n, (u64*)bits); return 0; });
+    if (rc) return rc;
+    MJX_LAUNCH_CHECK("mjx_pack_np");
+    return MJX_OK;
+}
+
+extern "C" int mjx_unpack_np(const uint64_t* bits, int64_t n, void* s, int dtype, void* stream) {
+    if (n < 0 || (n > 0 && (!s || !bits))) return MJX_EINVAL;
+    if (n == 0) return MJX_OK;
+    const int grid = grid_for(n);
+    hipStream_t st = as_stream(stream);
+    int rc = dispatch_dtype(dtype,
+        [&] { k_unpack_np<int8_t><<<grid, kBlock, 0, st>>>((const u64*)bits, n, (int8_t*)s); return 0; },
+        [&] { k_unpack_np<int32_t><<<grid, kBlock, 0, st>>>((const u64*)bits, n, (int32_t*)s); return 0; },
+        [&] { k_unpack_np<int64_t><<<grid, kBlock, 0, st>>>((const u64*)bits, n, (int64_t*)s); return 0; });
+    if (rc) return rc;
+    MJX_LAUNCH_CHECK("mjx_unpack_np");
+    return MJX_OK;
+}
+
+extern "C" int mjx_pack_rp(const void* s, int dtype, int64_t n, int64_t R, uint64_t* bits, void* stream) {
+    if (n < 0 || R < 1 || (n > 0 && (!s || !bits))) return MJX_EINVAL;
+    if (n == 0) return MJX_OK;
+    const int64_t W = (R + 63) / 64;
+    const int grid = grid_for(n * W);
+    hipStream_t st = as_stream(stream);
+    int rc = dispatch_dtype(dtype,
+        [&] { k_pack_rp<int8_t><<<grid, kBlock, 0, st>>>((const int8_t*)s, n, R, W, (u64*)bits); return 0; },
+        [&] { k_pack_rp<int32_t><<<grid, kBlock, 0, st>>>((const int32_t*)s, n, R, W, (u64*)bits); return 0; },
+        [&] { k_pack_rp<int64_t><<<grid, kBlock, 0, st>>>((const int64_t*)s, n, R, W, (u64*)bits); return 0; });
+    if (rc) return rc;
+    MJX_LAUNCH_CHECK("mjx_pack_rp");
+    return MJX_OK;
+}
+
+extern "C" int mjx_unpack_rp(const uint64_t* bits, int64_t n, int64_t R, void* s, int dtype, void* stream) {
+    if (n < 0 || R < 1 || (n > 0 && (!s || !bits))) return MJX_EINVAL;
+    if (n == 0) return MJX_OK;
+    const int64_t W = (R + 63) / 64;
+    const int grid = grid_for(n * W);
+    hipStream_t st = as_stream(stream);
+    int rc = dispatch_dtype(dtype,
+        [&] { k_unpack_rp<int8_t><<<grid, kBlock, 0, st>>>((const u64*)bits, n, R, W, (int8_t*)s); return 0; },
+        [&] { k_unpack_rp<int32_t><<<grid, kBlock, 0, st>>>((const u64*)bits, n, R, W, (int32_t*)s); return 0; },
+        [&] { k_unpack_rp<int64_t><<<grid, kBlock, 0, st>>>((const u64*)bits, n, R, W, (int64_t*)s); return 0; });
+    if (rc) return rc;
+    MJX_LAUNCH_CHECK("mjx_unpack_rp");
+    return MJX_OK;
+}
+
+// ---- sweep launchers -------------------------------------------------------
+
+static int launch_sweep_ell_np(const int32_t* adj, int64_t n, int d, const u64* in, u64* out,
+                               unsigned long long* counts, hipStream_t st) {
+    const int64_t nwords = (n + 63) / 64;
+    const int grid = grid_for(nwords * 64);
+    const uint32_t* in32 = reinterpret_cast<const uint32_t*>(in);
+    switch (d) {
+        case 3: k_sweep_ell_np<3><<<grid, kBlock, 0, st>>>(adj, n, in32, out, counts); break;
+        case 4: k_sweep_ell_np<4><<<grid, kBlock, 0, st>>>(adj, n, in32, out, counts); break;
+        case 6: k_sweep_ell_np<6><<<grid, kBlock, 0, st>>>(adj, n, in32, out, counts); break;
+        default: k_sweep_ell_np_dyn<<<grid, kBlock, 0, st>>>(adj, n, d, in32, out, counts); break;
+    }
+    MJX_LAUNCH_CHECK("sweep_ell_np");
+    return MJX_OK;
+}
+
+static int launch_sweep_csr_np(const int64_t* rp, const int32_t* col, int64_t n, const u64* in, u64* out,
+                               unsigned long long* counts, hipStream_t st) {
+    const int64_t nwords = (n + 63) / 64;
+    const int grid = grid_for(nwords * 64);
+    k_sweep_csr_np<<<grid, kBlock, 0, st>>>(rp, col, n, reinterpret_cast<const uint32_t*>(in), out, counts);
+    MJX_LAUNCH_CHECK("sweep_csr_np");
+    return MJX_OK;
+}
+
+template <int VW, bool COUNT>
+static void launch_ell_rp_vw(const int32_t* adj, int64_t n, int d, int64_t W, const u64* in, u64* out,
+                             unsigned long long* counts, int grid, size_t lds, int use_lds, hipStream_t st) {
+    switch (d) {
+        case 3: k_sweep_ell_rp<3, VW, COUNT><<<grid, kBlock, lds, st>>>(adj, n, W, in, out, counts, use_lds); break;
+        case 4: k_sweep_ell_rp<4, VW, COUNT><<<grid, kBlock, lds, st>>>(adj, n, W, in, out, counts, use_lds); break;
+        case 6: k_sweep_ell_rp<6, VW, COUNT><<<grid, kBlock, lds, st>>>(adj, n, W, in, out, counts, use_lds); break;
+        default:
+            k_sweep_gen_rp<VW, COUNT, false><<<grid, kBlock, lds, st>>>(adj, d, nullptr, nullptr, n, W, in, out,
+                                                                       counts, use_lds);
+            break;
+    }
+}
+
+static int rp_geometry(int64_t n, int64_t W, int* grid, int* vw, int* use_lds, size_t* lds) {
+    *vw = (W % 2 == 0) ? 2 : 1;
+    const int64_t U = W / *vw;
+    *grid = grid_for(n * U);
+    const int64_t threads = (int64_t)(*grid) * kBlock;
+    if (threads / U < 1) return MJX_ERANGE;
+    *use_lds = (W * 64 <= kMaxLdsReplicas) ? 1 : 0;
+    *lds = *use_lds ? (size_t)(W * 64 * sizeof(unsigned)) : 0;
+    return MJX_OK;
+}
+
+static int launch_sweep_ell_rp(const int32_t* adj, int64_t n, int d, int64_t W, const u64* in, u64* out,
+                               unsigned long long* counts, hipStream_t st) {
+    int grid, vw, use_lds; size_t lds;
+    int rc = rp_geometry(n, W, &grid, &vw, &use_lds, &lds);
+    if (rc) return rc;
+    if (!counts) { lds = 0; use_lds = 0; }
+    if (vw == 2) {
+        if (counts) launch_ell_rp_vw<2, true>(adj, n, d, W, in, out, counts, grid, lds, use_lds, st);
+        else launch_ell_rp_vw<2, false>(adj, n, d, W, in, out, counts, grid, lds, use_lds, st);
+    } else {
+        if (counts) launch_ell_rp_vw<1, true>(adj, n, d, W, in, out, counts, grid, lds, use_lds, st);
+        else launch_ell_rp_vw<1, false>(adj, n, d, W, in, out, counts, grid, lds, use_lds, st);
+    }
+    MJX_LAUNCH_CHECK("sweep_ell_rp");
+    return MJX_OK;
+}
+
+static int launch_sweep_csr_rp(const int64_t* rp, const int32_t* col, int64_t n, int64_t W, const u64* in,
+                               u64* out, unsigned long long* counts, hipStream_t st) {
+    int grid, vw, use_lds; size_t lds;
+    int rc = rp_geometry(n, W, &grid, &vw, &use_lds, &lds);
+    if (rc) return rc;
+    if (!counts) { lds = 0; use_lds = 0; }
+    if (vw == 2) {
+        if (counts) k_sweep_gen_rp<2, true, true><<<grid, kBlock, lds, st>>>(nullptr, 0, rp, col, n, W, in, out, counts, use_lds);
+        else k_sweep_gen_rp<2, false, true><<<grid, kBlock, lds, st>>>(nullptr, 0, rp, col, n, W, in, out, counts, use_lds);
+    } else {
+        if (counts) k_sweep_gen_rp<1, true, true><<<grid, kBlock, lds, st>>>(nullptr, 0, rp, col, n, W, in, out, counts, use_lds);
+        else k_sweep_gen_rp<1, false, true><<<grid, kBlock, lds, st>>>(nullptr, 0, rp, col, n, W, in, out, counts, use_lds);
+    }
+    MJX_LAUNCH_CHECK("sweep_csr_rp");
+    return MJX_OK;
+}
+
+// Runs `steps` sweeps in -> ... -> out, ping-ponging through tmp so that the
+// last sweep writes `out`; the fused count rides on the last sweep.
+template <typename SWEEP>
+static int run_rollout(int steps, const u64* in, u64* out, u64* tmp, unsigned long long* counts, SWEEP sweep) {
+    if (steps < 1) return MJX_EINVAL;
+    if (steps >= 2 && !tmp) return MJX_EINVAL;
+    const u64* src = in;
+    for (int k = 0; k < steps; ++k) {
+        u64* dst = (((steps - 1 - k) & 1) == 0) ? out : tmp;
+        int rc = sweep(src, dst, (k == steps - 1) ? counts : nullptr);
+        if (rc) return rc;
+        src = dst;
+    }
+    return MJX_OK;
+}
+
+extern "C" int mjx_popcount_np(const uint64_t* bits, int64_t n, unsigned long long* counts, void* stream) {
+    if (n < 0 || !counts || (n > 0 && !bits)) return MJX_EINVAL;
+    if (n == 0) return MJX_OK;
+    const int64_t nwords = (n + 63) / 64;
+    k_popcount_np<<<grid_for(nwords), kBlock, 0, as_stream(stream)>>>((const u64*)bits, n, counts);
+    MJX_LAUNCH_CHECK("mjx_popcount_np");
+    return MJX_OK;
+}
+
+extern "C" int mjx_popcount_rp(const uint64_t* bits, int64_t n, int64_t words, unsigned long long* counts,
+                               void* stream) {
+    if (n < 0 || words < 1 || !counts || (n > 0 && !bits)) return MJX_EINVAL;
+    if (n == 0) return MJX_OK;
+    int grid, vw, use_lds; size_t lds;
+    int rc = rp_geometry(n, words, &grid, &vw, &use_lds, &lds);
+    if (rc) return rc;
+    hipStream_t st = as_stream(stream);
+    if (vw == 2) k_popcount_rp<2><<<grid, kBlock, lds, st>>>((const u64*)bits, n, words, counts, use_lds);
+    else k_popcount_rp<1><<<grid, kBlock, lds, st>>>((const u64*)bits, n, words, counts, use_lds);
+    MJX_LAUNCH_CHECK("mjx_popcount_rp");
+    return MJX_OK;
+}
+
+static bool overlaps(const void* a, const void* b) { return a && b && a == b; }
+
+extern "C" int mjx_rollout_ell_np(const int32_t* adj, int64_t n, int d, const uint64_t* s_in, uint64_t* s_out,
+                                  uint64_t* tmp, int steps, unsigned long long* counts, void* stream) {
+    if (n < 0 || d < 0 || d > 255 || (n > 0 && (!adj && d > 0)) || (n > 0 && (!s_in || !s_out))) return MJX_EINVAL;
+    if (n > (int64_t)INT32_MAX) return MJX_ERANGE;
+    if (overlaps(s_in, s_out) || overlaps(s_in, tmp) || overlaps(s_out, tmp)) return MJX_EINVAL;
+    if (n == 0) return MJX_OK;
+    hipStream_t st = as_stream(stream);
+    const size_t bytes = (size_t)((n + 63) / 64) * 8;
+    auto sweep = [&](const u64* a, u64* b, unsigned long long* c) {
+        return launch_sweep_ell_np(adj, n, d, a, b, c, st);
+    };
+    if (steps < 0) return MJX_EINVAL;
+    if (steps == 0) {
+        MJX_HIP(hipMemcpyAsync(s_out, s_in, bytes, hipMemcpyDeviceToDevice, st), "rollout copy");
+        return counts ? mjx_popcount_np(s_out, n, counts, stream) : MJX_OK;
+    }
+    return run_rollout(steps, (const u64*)s_in, (u64*)s_out, (u64*)tmp, counts, sweep);
+}
+
+extern "C" int mjx_rollout_ell_rp(const int32_t* adj, int64_t n, int d, int64_t words, const uint64_t* s_in,
+                                  uint64_t* s_out, uint64_t* tmp, int steps, unsigned long long* counts,
+                                  void* stream) {
+    if (n < 0 || d < 0 || d > 255 || words < 1 || (n > 0 && (!s_in || !s_out || (!adj && d > 0)))) return MJX_EINVAL;
+    if (n > (int64_t)INT32_MAX) return MJX_ERANGE;
+    if (overlaps(s_in, s_out) || overlaps(s_in, tmp) || overlaps(s_out, tmp)) return MJX_EINVAL;
+    if (n == 0) return MJX_OK;
+    hipStream_t st = as_stream(stream);
+    const size_t bytes = (size_t)n * (size_t)words * 8;
+    if (steps < 0) return MJX_EINVAL;
+    if (steps == 0) {
+        MJX_HIP(hipMemcpyAsync(s_out, s_in, bytes, hipMemcpyDeviceToDevice, st), "rollout copy");
+        return counts ? mjx_popcount_rp(s_out, n, words, counts, stream) : MJX_OK;
+    }
+    auto sweep = [&](const u64* a, u64* b, unsigned long long* c) {
+        return launch_sweep_ell_rp(adj, n, d, words, a, b, c, st);
+    };
+    return run_rollout(steps, (const u64*)s_in, (u64*)s_out, (u64*)tmp, counts, sweep);
+}
+
+extern "C" int mjx_rollout_csr_np(const int64_t* row_ptr, const int32_t* col, int64_t n, const uint64_t* s_in,
+                                  uint64_t* s_out, uint64_t* tmp, int steps, unsigned long long* counts,
+                                  void* stream) {
+    if (n < 0 || (n > 0 && (!row_ptr || !s_in || !s_out))) return MJX_EINVAL;
+    if (n > (int64_t)INT32_MAX) return MJX_ERANGE;
+    if (overlaps(s_in, s_out) || overlaps(s_in, tmp) || overlaps(s_out, tmp)) return MJX_EINVAL;
+    if (n == 0) return MJX_OK;
+    hipStream_t st = as_stream(stream);
+    const size_t bytes = (size_t)((n + 63) / 64) * 8;
+    if (steps < 0) return MJX_EINVAL;
+    if (steps == 0) {
+        MJX_HIP(hipMemcpyAsync(s_out, s_in, bytes, hipMemcpyDeviceToDevice, st), "rollout copy");
+        return counts ? mjx_popcount_np(s_out, n, counts, stream) : MJX_OK;
+    }
+    auto sweep = [&](const u64* a, u64* b, unsigned long long* c) {
+        return launch_sweep_csr_np(row_ptr, col, n, a, b, c, st);
+    };
+    return run_rollout(steps, (const u64*)s_in, (u64*)s_out, (u64*)tmp, counts, sweep);
+}
+
+extern "C" int mjx_rollout_csr_rp(const int64_t* row_ptr, const int32_t* col, int64_t n, int64_t words,
+                                  const uint64_t* s_in, uint64_t* s_out, uint64_t* tmp, int steps,
+                                  unsigned long long* counts, void* stream) {
+    if (n < 0 || words < 1 || (n > 0 && (!row_ptr || !s_in || !s_out))) return MJX_EINVAL;
+    if (n > (int64_t)INT32_MAX) return MJX_ERANGE;
+    if (overlaps(s_in, s_out) || overlaps(s_in, tmp) || overlaps(s_out, tmp)) return MJX_EINVAL;
+    if (n == 0) return MJX_OK;
+    hipStream_t st = as_stream(stream);
+    const size_t bytes = (size_t)n * (size_t)words * 8;
+    if (steps < 0) return MJX_EINVAL;
+    if (steps == 0) {
+        MJX_HIP(hipMemcpyAsync(s_out, s_in, bytes, hipMemcpyDeviceToDevice, st), "rollout copy");
+        return counts ? mjx_popcount_rp(s_out, n, words, counts, stream) : MJX_OK;
+    }
+    auto sweep = [&](const u64* a, u64* b, unsigned long long* c) {
+        return launch_sweep_csr_rp(row_ptr, col, n, words, a, b, c, st);
+    };
+    return run_rollout(steps, (const u64*)s_in, (u64*)s_out, (u64*)tmp, counts, sweep);
+}

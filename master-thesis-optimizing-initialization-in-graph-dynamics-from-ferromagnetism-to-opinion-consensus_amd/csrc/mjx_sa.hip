@@ -1,0 +1,317 @@
+// Simulated annealing over bit-packed replicas (code/SA_RRG.py:44-92).
+//
+// Replica r replays numpy's legacy global MT19937 after np.random.seed(seed_r)
+// (SURVEY.md 0.1 SA3):
+//   * init_genrand(seed) state, 32-bit tempered outputs;
+//   * binomial(1, .5) consumes one double U per node and returns U > 0.5
+//     (code/SA_RRG.py:65, s0 = 2*binomial - 1);
+//   * randint(0, n): masked rejection on 32-bit words (code/SA_RRG.py:73);
+//   * rand(): ((w1>>5)*67108864 + (w2>>6)) / 2^53 (code/SA_RRG.py:76).
+// The draw sequence does not depend on accept decisions, so each replica's
+// (i_t, u_t) tape is a pure function of its seed.
+//
+// One proposal of every running replica per step, evaluated by a full
+// rollout of the flipped configuration (one rollout instead of the
+// reference's three: sum(s_endstate(s)) of the current state is cached from
+// the previous step's consensus check, code/SA_RRG.py:85).
+//
+// This translation unit is compiled with -ffp-contract=off: delta_H must be
+// evaluated as ((-2*a)*s_i + b*D)/n with separately rounded operations, as
+// numpy does (code/SA_RRG.py:37).
+#include "mjx_common.h"
+#include <math.h>
+
+#pragma clang fp contract(off)
+
+namespace mjx {
+
+constexpr int MT_N = 624;
+constexpr int MT_M = 397;
+constexpr uint32_t MT_MATRIX_A = 0x9908b0dfu;
+constexpr uint32_t MT_UPPER = 0x80000000u;
+constexpr uint32_t MT_LOWER = 0x7fffffffu;
+
+__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+}
+
+__device__ __forceinline__ uint32_t mt_mix(uint32_t cur, uint32_t nxt, uint32_t far) {
+    uint32_t y = (cur & MT_UPPER) | (nxt & MT_LOWER);
+    return far ^ (y >> 1) ^ ((y & 1u) ? MT_MATRIX_A : 0u);
+}
+
+__device__ __forceinline__ double mt_double(uint32_t w1, uint32_t w2) {
+    return ((double)(w1 >> 5) * 67108864.0 + (double)(w2 >> 6)) / 9007199254740992.0;
+}
+
+// ---------------------------------------------------------------------------
+// init: 64 replicas per block (one wave); their MT states live in LDS laid out
+// [k][lane] (conflict-free), every lane consumes exactly 2 words per node so
+// the wave twists in lockstep.  Bits are packed by ballot: the wave's 64
+// replicas are exactly one replica-packed word column.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_sa_init_draw(int64_t n, int64_t R, int64_t W,
+                                                     const uint32_t* __restrict__ seeds,
+                                                     u64* __restrict__ s, uint32_t* __restrict__ mt_out,
+                                                     int32_t* __restrict__ idx_out) {
+    __shared__ uint32_t st[MT_N * 64];
+    const int lane = threadIdx.x;
+    const int64_t w = blockIdx.x;
+    const int64_t r = w * 64 + lane;
+    const bool live = r < R;
+    uint32_t x = live ? seeds[r] : 0u;
+    for (int k = 0; k < MT_N; ++k) {       // init_genrand / numpy mt19937_seed
+        st[k * 64 + lane] = x;
+        x = 1812433253u * (x ^ (x >> 30)) + (uint32_t)(k + 1);
+    }
+    int idx = MT_N;
+    auto next = [&]() -> uint32_t {
+        if (idx >= MT_N) {
+            for (int k = 0; k < MT_N - MT_M; ++k)
+                st[k * 64 + lane] = mt_mix(st[k * 64 + lane], st[(k + 1) * 64 + lane], st[(k + MT_M) * 64 + lane]);
+            for (int k = MT_N - MT_M; k < MT_N - 1; ++k)
+                st[k * 64 + lane] = mt_mix(st[k * 64 + lane], st[(k + 1) * 64 + lane],
+                                           st[(k + MT_M - MT_N) * 64 + lane]);
+            st[(MT_N - 1) * 64 + lane] = mt_mix(st[(MT_N - 1) * 64 + lane], st[lane], st[(MT_M - 1) * 64 + lane]);
+            idx = 0;
+        }
+        return mt_temper(st[(idx++) * 64 + lane]);
+    };
+    for (int64_t v = 0; v < n; ++v) {
+        uint32_t a = next();
+        uint32_t b = next();
+        bool plus = live && (mt_double(a, b) > 0.5);
+        u64 word = __ballot(plus);
+        if (lane == 0) s[v * W + w] = word;
+    }
+    if (live) {
+        for (int k = 0; k < MT_N; ++k) mt_out[r * MT_N + k] = st[k * 64 + lane];
+        idx_out[r] = idx;
+    }
+}
+
+__global__ void k_sa_init_state(int64_t n, int64_t R, double a0, double b0,
+                                const unsigned long long* __restrict__ cnt, mjx_sa_state st) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= R) return;
+    st.a[r] = a0;
+    st.b[r] = b0;
+    st.t[r] = 0;
+    const int64_t sum = 2 * (int64_t)cnt[r] - n;
+    st.sum_end[r] = sum;
+    st.done[r] = (sum == n) ? 1 : 0;   // m(s_endstate(s0)) == 1: loop never runs
+    if (st.tr_tie) st.tr_tie[r] = 0;
+}
+
+// ---------------------------------------------------------------------------
+// step kernels: one thread per replica, MT state replica-major in global
+// memory mt[r*624 + k].  A lane that runs out of words gets its state twisted
+// cooperatively by its whole wave through a 624-word LDS buffer.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t ld_nc(const uint32_t* p) {
+    // bypass the CU's L1: the words may have been rewritten by this wave's
+    // own cooperative twist earlier in this launch
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ void coop_twist(uint32_t* __restrict__ g, uint32_t* buf, int lane) {
+    for (int k = lane; k < MT_N; k += 64) buf[k] = ld_nc(g + k);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // phase A: k in [0, 227): every input is an old word
+    for (int k = lane; k < MT_N - MT_M; k += 64) {
+        uint32_t v = mt_mix(buf[k], buf[k + 1], buf[k + MT_M]);
+        __builtin_amdgcn_wave_barrier();
+        buf[k] = v;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+    // phase B: k in [227, 454): far word k-227 is new (phase A)
+    for (int k = MT_N - MT_M + lane; k < 2 * (MT_N - MT_M); k += 64) {
+        uint32_t v = mt_mix(buf[k], buf[k + 1], buf[k + MT_M - MT_N]);
+        __builtin_amdgcn_wave_barrier();
+        buf[k] = v;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+    // phase C: k in [454, 623): far word k-227 in [227, 396) is new (phase B)
+    for (int k = 2 * (MT_N - MT_M) + lane; k < MT_N - 1; k += 64) {
+        uint32_t v = mt_mix(buf[k], buf[k + 1], buf[k + MT_M - MT_N]);
+        __builtin_amdgcn_wave_barrier();
+        buf[k] = v;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+    // phase D: k = 623 uses the new word 0 and the new word 396
+    if (lane == 0) buf[MT_N - 1] = mt_mix(buf[MT_N - 1], buf[0], buf[MT_M - 1]);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    for (int k = lane; k < MT_N; k += 64) g[k] = buf[k];
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+struct WaveMT {
+    uint32_t* mt;      // all replicas
+    uint32_t* buf;     // this wave's LDS twist buffer
+    int64_t r;
+    int idx;
+    int lane;
+    // wave-uniform call: lanes with want == false still participate
+    __device__ __forceinline__ uint32_t draw(bool want) {
+        const bool tw = want && idx >= MT_N;
+        u64 m = __ballot(tw);
+        const int64_t base = r - lane;
+        while (m) {
+            const int l = __ffsll((unsigned long long)m) - 1;
+            coop_twist(mt + (base + l) * MT_N, buf, lane);
+            m &= m - 1;
+        }
+        if (tw) idx = 0;
+        uint32_t y = 0;
+        if (want) y = mt_temper(ld_nc(mt + r * MT_N + idx++));
+        return y;
+    }
+};
+
+__global__ void __launch_bounds__(kBlock) k_sa_propose(int64_t n, int64_t R, int64_t W, u64* __restrict__ s,
+                                                       mjx_sa_state st, int64_t step) {
+    __shared__ uint32_t twist_buf[kBlock / 64][MT_N];
+    const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const bool live = r < R;
+    const bool active = live && st.done[r] == 0;
+    WaveMT g{st.mt, twist_buf[threadIdx.x >> 6], r, live ? st.mt_idx[r] : MT_N, lane};
+    // randint(low=0, high=n): numpy legacy masked rejection
+    const uint64_t rng = (uint64_t)(n - 1);
+    uint32_t mask = (uint32_t)rng;
+    mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+    bool pending = active && rng > 0;
+    uint32_t i = 0;
+    while (__ballot(pending)) {
+        uint32_t y = g.draw(pending);
+        if (pending) {
+            uint32_t v = y & mask;
+            if (v <= (uint32_t)rng) { i = v; pending = false; }
+        }
+    }
+    // rand()
+    uint32_t w1 = g.draw(active);
+    uint32_t w2 = g.draw(active);
+    if (live) st.mt_idx[r] = g.idx;
+    if (active) {
+        const double u = mt_double(w1, w2);
+        const u64 bit = 1ull << (r & 63);
+        const u64 old = atomicXor((unsigned long long*)&s[(int64_t)i * W + (r >> 6)], (unsigned long long)bit);
+        st.prop_i[r] = (int32_t)i;
+        st.prop_s[r] = (old & bit) ? 1 : -1;   // s0[i] before the flip
+        st.prop_u[r] = u;
+    }
+    if (live && st.tr_i) st.tr_i[step * R + r] = active ? (int32_t)i : -1;
+}
+
+__global__ void __launch_bounds__(kBlock) k_sa_accept(int64_t n, int64_t R, int64_t W, u64* __restrict__ s,
+                                                      mjx_sa_state st, int64_t step, double par_a, double par_b,
+                                                      double a_cap, double b_cap, int64_t t_cap) {
+    const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (r >= R) return;
+    if (st.done[r] != 0) {
+        if (st.tr_acc) st.tr_acc[step * R + r] = -1;
+        if (st.tr_sum) st.tr_sum[step * R + r] = st.sum_end[r];
+        if (st.tr_dE) st.tr_dE[step * R + r] = 0.0;
+        return;
+    }
+    const int64_t sum_new = 2 * (int64_t)st.cnt[r] - n;        // sum(s_endstate(s with i flipped))
+    const int64_t sum_old = st.sum_end[r];                      // sum(s_endstate(s))
+    const double a = st.a[r], b = st.b[r];
+    const double si = (double)st.prop_s[r];
+    // delta_H = (-2*a*s0[i] + b*(sum(s_end1) - sum(s_end2)))/n   (code/SA_RRG.py:37)
+    const double t1 = (-2.0 * a) * si;
+    const double t2 = b * (double)(sum_old - sum_new);
+    const double dE = (t1 + t2) / (double)n;
+    // prob_accept = min([1, np.exp(-delta_H)])                 (code/SA_RRG.py:75)
+    const double e = exp(-dE);
+    const double prob = (e < 1.0) ? e : 1.0;
+    const double u = st.prop_u[r];
+    const bool acc = u < prob;                                  // (code/SA_RRG.py:76)
+    if (st.tr_tie && e < 1.0) {
+        const double gap = fabs(u - e);
+        if (gap <= 4.0 * (nextafter(e, 2.0) - e)) st.tr_tie[r] += 1;
+    }
+    int64_t sum_cur = sum_old;
+    if (acc) {
+        sum_cur = sum_new;
+    } else {
+        const int32_t i = st.prop_i[r];
+        atomicXor((unsigned long long*)&s[(int64_t)i * W + (r >> 6)], (unsigned long long)(1ull << (r & 63)));
+    }
+    // annealing schedule (code/SA_RRG.py:80-81)
+    double an = a, bn = b;
+    if (a < a_cap) an = par_a * a;
+    if (b < b_cap) bn = par_b * b;
+    st.a[r] = an;
+    st.b[r] = bn;
+    const int64_t t = st.t[r] + 1;                               // (code/SA_RRG.py:82)
+    st.t[r] = t;
+    st.sum_end[r] = sum_cur;
+    if (t > t_cap) st.done[r] = 2;                              // m_final = 2 (code/SA_RRG.py:84)
+    else if (sum_cur == n) st.done[r] = 1;                      // m(s_endstate(s)) == 1
+    if (st.tr_acc) st.tr_acc[step * R + r] = acc ? 1 : 0;
+    if (st.tr_sum) st.tr_sum[step * R + r] = sum_cur;
+    if (st.tr_dE) st.tr_dE[step * R + r] = dE;
+}
+
+}  // namespace mjx
+
+using namespace mjx;
+
+extern "C" int mjx_sa_init(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R, const uint32_t* seeds,
+                           double a0, double b0, uint64_t* s, uint64_t* tmp1, uint64_t* tmp2, mjx_sa_state* stp,
+                           void* stream) {
+    if (!stp || n < 2 || R < 1 || d < 1 || p < 0 || c < 0 || p + c < 1 || !adj || !seeds || !s || !tmp1) return MJX_EINVAL;
+    if (n > (int64_t)INT32_MAX) return MJX_ERANGE;
+    mjx_sa_state st = *stp;
+    if (!st.mt || !st.mt_idx || !st.a || !st.b || !st.t || !st.sum_end || !st.done || !st.prop_i || !st.prop_s ||
+        !st.prop_u || !st.cnt)
+        return MJX_EINVAL;
+    const int64_t W = (R + 63) / 64;
+    const int T = p + c - 1;
+    if (T >= 2 && !tmp2) return MJX_EINVAL;
+    hipStream_t hs = as_stream(stream);
+    k_sa_init_draw<<<(unsigned)W, 64, 0, hs>>>(n, R, W, seeds, (u64*)s, st.mt, st.mt_idx);
+    MJX_LAUNCH_CHECK("k_sa_init_draw");
+    MJX_HIP(hipMemsetAsync(st.cnt, 0, (size_t)R * sizeof(unsigned long long), hs), "sa_init memset");
+    int rc = mjx_rollout_ell_rp(adj, n, d, W, s, tmp1, tmp2, T, st.cnt, stream);
+    if (rc) return rc;
+    k_sa_init_state<<<(unsigned)((R + 255) / 256), 256, 0, hs>>>(n, R, a0, b0, st.cnt, st);
+    MJX_LAUNCH_CHECK("k_sa_init_state");
+    return MJX_OK;
+}
+
+extern "C" int mjx_sa_steps(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R, uint64_t* s,
+                            uint64_t* tmp1, uint64_t* tmp2, mjx_sa_state* stp, int64_t nsteps, double par_a,
+                            double par_b, double a_cap, double b_cap, int64_t t_cap, void* stream) {
+    if (!stp || n < 2 || R < 1 || d < 1 || p < 0 || c < 0 || p + c < 1 || !adj || !s || !tmp1 || nsteps < 0)
+        return MJX_EINVAL;
+    if (n > (int64_t)INT32_MAX) return MJX_ERANGE;
+    mjx_sa_state st = *stp;
+    const int64_t W = (R + 63) / 64;
+    const int T = p + c - 1;
+    if (T >= 2 && !tmp2) return MJX_EINVAL;
+    hipStream_t hs = as_stream(stream);
+    const unsigned gridR = (unsigned)((R + kBlock - 1) / kBlock);
+    for (int64_t k = 0; k < nsteps; ++k) {
+        k_sa_propose<<<gridR, kBlock, 0, hs>>>(n, R, W, (u64*)s, st, k);
+        MJX_LAUNCH_CHECK("k_sa_propose");
+        MJX_HIP(hipMemsetAsync(st.cnt, 0, (size_t)R * sizeof(unsigned long long), hs), "sa_steps memset");
+        int rc = mjx_rollout_ell_rp(adj, n, d, W, s, tmp1, tmp2, T, st.cnt, stream);
+        if (rc) return rc;
+        k_sa_accept<<<gridR, kBlock, 0, hs>>>(n, R, W, (u64*)s, st, k, par_a, par_b, a_cap, b_cap, t_cap);
+        MJX_LAUNCH_CHECK("k_sa_accept");
+    }
+    return MJX_OK;
+}

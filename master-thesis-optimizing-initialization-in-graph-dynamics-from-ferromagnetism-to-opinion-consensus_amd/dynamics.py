@@ -1,0 +1,149 @@
+"""Majority-rule dynamics: the reference's entry points backed by HIP kernels.
+
+Reference-shaped functions (same names, same argument meaning):
+
+  onestep_majority(N, s0)   code/SA_RRG.py:18-20, code/HPR_pytorch_RRG.py:169-171
+  s_endstate(N, s0, p, c)   code/SA_RRG.py:23-26, code/HPR_pytorch_RRG.py:174-177
+  m(s)                      code/SA_RRG.py:39-40, code/HPR_pytorch_RRG.py:179-180
+
+``N`` is the (n, d) neighbour array (or a ``graph.Graph``, which may also be
+CSR for Erdos-Renyi graphs, nb:113-123).  ``s0`` is a +-1 integer vector (n,)
+or a batch (R, n) of replicas.  Results are int64 like the reference's
+(numpy in -> numpy out, tensor in -> tensor out on the same device).
+
+The bit-packed API (``pack``/``unpack``/``rollout``) is what the hot loops
+use: spins stay packed in HBM between calls.
+"""
+import numpy as np
+import torch
+
+from . import _device, _lib
+from .graph import Graph
+
+
+# ---------------------------------------------------------------------------
+# packed layer
+# ---------------------------------------------------------------------------
+def pack(s):
+    """+-1 int tensor (n,) -> node-packed bits; (R, n) -> replica-packed bits."""
+    s = _device.to_device(s)
+    code = _device.dtype_code(s)
+    st = _device.stream_handle()
+    if s.dim() == 1:
+        n = s.shape[0]
+        bits = torch.empty((n + 63) // 64, dtype=torch.int64, device=s.device)
+        _lib.call("mjx_pack_np", _device.ptr(s), code, n, _device.ptr(bits), st)
+        return bits
+    if s.dim() == 2:
+        R, n = s.shape
+        bits = torch.empty(n * _device.words_for(R), dtype=torch.int64, device=s.device)
+        _lib.call("mjx_pack_rp", _device.ptr(s), code, n, R, _device.ptr(bits), st)
+        return bits
+    raise ValueError("spins must be (n,) or (R, n)")
+
+
+def unpack(bits, n, R=None, dtype=torch.int64):
+    """Inverse of ``pack``: (n,) for R=None, else (R, n)."""
+    st = _device.stream_handle()
+    if R is None:
+        s = torch.empty(n, dtype=dtype, device=bits.device)
+        _lib.call("mjx_unpack_np", _device.ptr(bits), n, _device.ptr(s), _device.dtype_code(s), st)
+        return s
+    s = torch.empty((R, n), dtype=dtype, device=bits.device)
+    _lib.call("mjx_unpack_rp", _device.ptr(bits), n, R, _device.ptr(s), _device.dtype_code(s), st)
+    return s
+
+
+def rollout(graph, bits, steps, words=None, out=None, tmp=None, counts=None):
+    """Apply ``steps`` synchronous majority sweeps to packed spins.
+
+    words=None: node-packed single replica; else replica-packed with ``words``
+    64-bit words per node.  ``counts`` (uint64 tensor viewed as int64, length
+    R or 1) receives, added, the number of +1 spins of the result.
+    """
+    st = _device.stream_handle()
+    out = torch.empty_like(bits) if out is None else out
+    if steps >= 2 and tmp is None:
+        tmp = torch.empty_like(bits)
+    cptr = _device.ptr(counts) if counts is not None else None
+    tptr = _device.ptr(tmp) if tmp is not None else None
+    if graph.kind == "ell":
+        if words is None:
+            _lib.call("mjx_rollout_ell_np", _device.ptr(graph.adj), graph.n, graph.d, _device.ptr(bits),
+                      _device.ptr(out), tptr, int(steps), cptr, st)
+        else:
+            _lib.call("mjx_rollout_ell_rp", _device.ptr(graph.adj), graph.n, graph.d, int(words),
+                      _device.ptr(bits), _device.ptr(out), tptr, int(steps), cptr, st)
+    else:
+        if words is None:
+            _lib.call("mjx_rollout_csr_np", _device.ptr(graph.row_ptr), _device.ptr(graph.col), graph.n,
+                      _device.ptr(bits), _device.ptr(out), tptr, int(steps), cptr, st)
+        else:
+            _lib.call("mjx_rollout_csr_rp", _device.ptr(graph.row_ptr), _device.ptr(graph.col), graph.n,
+                      int(words), _device.ptr(bits), _device.ptr(out), tptr, int(steps), cptr, st)
+    return out
+
+
+def popcount(bits, n, words=None, counts=None):
+    """Number of +1 spins (per replica for the replica-packed layout)."""
+    st = _device.stream_handle()
+    if counts is None:
+        counts = torch.zeros(1 if words is None else words * 64, dtype=torch.int64, device=bits.device)
+    if words is None:
+        _lib.call("mjx_popcount_np", _device.ptr(bits), n, _device.ptr(counts), st)
+    else:
+        _lib.call("mjx_popcount_rp", _device.ptr(bits), n, int(words), _device.ptr(counts), st)
+    return counts
+
+
+# ---------------------------------------------------------------------------
+# reference-shaped layer
+# ---------------------------------------------------------------------------
+def as_graph(N):
+    if isinstance(N, Graph):
+        return N
+    return Graph.ell(N)
+
+
+def _return_like(x, like):
+    if isinstance(like, np.ndarray):
+        return x.cpu().numpy()
+    if isinstance(like, torch.Tensor):
+        return x.to(like.device)
+    return x.cpu().numpy()
+
+
+def s_endstate(N, s0, p, c):
+    """s after p+c-1 synchronous majority steps (code/SA_RRG.py:23-26)."""
+    steps = int(p) + int(c) - 1
+    if steps < 0:
+        raise ValueError("p + c - 1 must be >= 0")
+    g = as_graph(N)
+    s = _device.to_device(s0)
+    if s.shape[-1] != g.n:
+        raise ValueError(f"spin vector length {s.shape[-1]} != n = {g.n}")
+    if s.dim() == 1:
+        bits = pack(s)
+        out = rollout(g, bits, steps) if steps else bits
+        res = unpack(out, g.n)
+    else:
+        R = s.shape[0]
+        bits = pack(s)
+        out = rollout(g, bits, steps, words=_device.words_for(R)) if steps else bits
+        res = unpack(out, g.n, R)
+    return _return_like(res, s0)
+
+
+def onestep_majority(N, s0):
+    """One synchronous majority step, always-stay ties (code/SA_RRG.py:18-20)."""
+    return s_endstate(N, s0, 1, 1)
+
+
+def m(s, n=None):
+    """Magnetisation sum(s)/n (code/SA_RRG.py:39-40; nb:125-126 passes n)."""
+    if isinstance(s, torch.Tensor):
+        n = s.shape[-1] if n is None else n
+        return torch.sum(s, dim=-1) / n
+    s = np.asarray(s)
+    n = s.shape[-1] if n is None else n
+    return np.sum(s, axis=-1) / n

@@ -1,0 +1,196 @@
+"""Simulated annealing for strategic initialisations (code/SA_RRG.py:44-92).
+
+``SAReplicas`` runs R independent replicas of the reference's SA loop on one
+graph, all replicas bit-packed into one spin array (64 per 64-bit word).
+Replica r is bit-identical to the reference run
+
+    np.random.seed(seeds[r])
+    s = 2*np.random.binomial(n=1, p=0.5, size=[n]) - 1      # code/SA_RRG.py:65
+    ... while(m_final<1): ...                                # code/SA_RRG.py:72-85
+
+on the same neighbour array ``N`` — same proposals, same accept decisions,
+same final ``conf``, ``num_steps`` and ``mag_reached``.  (The reference runs
+its N_stat replicas back to back on one global numpy stream and a fresh graph
+each; here each replica owns a seed, which is what makes them independent and
+parallel.)
+
+Per step the device does: draw (i, u) and flip s[i] for every running replica
+(k_sa_propose), roll out the flipped configuration with the fused per-replica
++1 count (mjx_rollout_ell_rp), then the Metropolis test, annealing schedule
+and consensus check (k_sa_accept), un-flipping rejected proposals.
+"""
+import numpy as np
+import torch
+
+from . import _device, _lib
+from .dynamics import as_graph, rollout, pack, unpack
+from .graph import Graph
+
+PAR_A = 1.0005   # code/SA_RRG.py:49
+PAR_B = 1.0005   # code/SA_RRG.py:50
+
+
+def schedule_constants(n):
+    """(a0, b0, a_cap, b_cap, t_cap) exactly as the reference computes them
+    in Python floats/ints (code/SA_RRG.py:67-68, 80-81, 84)."""
+    return 0.015 * n, 0.01 * n, 4.5 * n, float(5 * n), 2 * n ** 3
+
+
+class SAReplicas:
+    """R bit-packed SA replicas on one random regular graph (device resident)."""
+
+    def __init__(self, N, p, c, seeds, par_a=PAR_A, par_b=PAR_B, a0=None, b0=None):
+        self.graph = as_graph(N)
+        if self.graph.kind != "ell":
+            raise ValueError("SA runs on random regular graphs (ELL adjacency), code/SA_RRG.py:59-61")
+        dev = _device.require_gpu()
+        self.p, self.c = int(p), int(c)
+        self.n = n = self.graph.n
+        if n < 2:
+            raise ValueError("n must be >= 2")
+        seeds = np.asarray(seeds, dtype=np.int64).reshape(-1)
+        if seeds.size == 0 or seeds.min() < 0 or seeds.max() > 0xFFFFFFFF:
+            raise ValueError("seeds must be in [0, 2**32)")  # np.random.seed's range
+        self.R = R = int(seeds.size)
+        self.W = W = _device.words_for(R)
+        a0d, b0d, self.a_cap, self.b_cap, self.t_cap = schedule_constants(n)
+        self.a0 = a0d if a0 is None else float(a0)
+        self.b0 = b0d if b0 is None else float(b0)
+        self.par_a, self.par_b = float(par_a), float(par_b)
+        if self.t_cap > 2 ** 63 - 1:
+            self.t_cap = 2 ** 63 - 1
+        i64 = torch.int64
+        self.s = torch.zeros(n * W, dtype=i64, device=dev)
+        self.tmp1 = torch.empty_like(self.s)
+        self.tmp2 = torch.empty_like(self.s)
+        self.seeds = torch.from_numpy(seeds.astype(np.uint32).view(np.int32)).to(dev)
+        self.mt = torch.empty(R * 624, dtype=torch.int32, device=dev)
+        self.mt_idx = torch.empty(R, dtype=torch.int32, device=dev)
+        self.a = torch.empty(R, dtype=torch.float64, device=dev)
+        self.b = torch.empty(R, dtype=torch.float64, device=dev)
+        self.t = torch.zeros(R, dtype=i64, device=dev)
+        self.sum_end = torch.zeros(R, dtype=i64, device=dev)
+        self.done = torch.zeros(R, dtype=torch.int32, device=dev)
+        self.prop_i = torch.empty(R, dtype=torch.int32, device=dev)
+        self.prop_s = torch.empty(R, dtype=torch.int8, device=dev)
+        self.prop_u = torch.empty(R, dtype=torch.float64, device=dev)
+        self.cnt = torch.zeros(R, dtype=i64, device=dev)
+        self.ties = torch.zeros(R, dtype=torch.int32, device=dev)
+        self._state = _lib.MjxSaState()
+        for f in ("mt", "mt_idx", "a", "b", "t", "sum_end", "done", "prop_i", "prop_s", "prop_u", "cnt"):
+            setattr(self._state, f, getattr(self, f).data_ptr())
+        self._state.tr_tie = self.ties.data_ptr()
+        T = self.p + self.c - 1
+        _lib.call("mjx_sa_init", _device.ptr(self.graph.adj), n, self.graph.d, self.p, self.c, R,
+                  _device.ptr(self.seeds), self.a0, self.b0, _device.ptr(self.s), _device.ptr(self.tmp1),
+                  _device.ptr(self.tmp2) if T >= 2 else None, _lib.ctypes.byref(self._state),
+                  _device.stream_handle())
+
+    # -- stepping -----------------------------------------------------------
+    def steps(self, k, trace=False):
+        """Advance every running replica by k proposals.  With ``trace`` the
+        per-step (i, accept, sum_end, delta_H) arrays of shape (k, R) are
+        returned (i = -1 / accept = -1 once a replica is done)."""
+        k = int(k)
+        st = self._state
+        tr = None
+        if trace:
+            dev = self.s.device
+            tr = {
+                "i": torch.empty((k, self.R), dtype=torch.int32, device=dev),
+                "accept": torch.empty((k, self.R), dtype=torch.int8, device=dev),
+                "sum_end": torch.empty((k, self.R), dtype=torch.int64, device=dev),
+                "dE": torch.empty((k, self.R), dtype=torch.float64, device=dev),
+            }
+            st.tr_i, st.tr_acc = tr["i"].data_ptr(), tr["accept"].data_ptr()
+            st.tr_sum, st.tr_dE = tr["sum_end"].data_ptr(), tr["dE"].data_ptr()
+        else:
+            st.tr_i = st.tr_acc = st.tr_sum = st.tr_dE = None
+        T = self.p + self.c - 1
+        _lib.call("mjx_sa_steps", _device.ptr(self.graph.adj), self.n, self.graph.d, self.p, self.c, self.R,
+                  _device.ptr(self.s), _device.ptr(self.tmp1), _device.ptr(self.tmp2) if T >= 2 else None,
+                  _lib.ctypes.byref(st), k, self.par_a, self.par_b, self.a_cap, self.b_cap,
+                  int(self.t_cap), _device.stream_handle())
+        st.tr_i = st.tr_acc = st.tr_sum = st.tr_dE = None
+        return tr
+
+    def all_done(self):
+        return bool((self.done != 0).all().item())
+
+    def run(self, max_steps=None, chunk=256):
+        """Step until every replica has reached consensus or the t cap
+        (``while(m_final<1)``, code/SA_RRG.py:72), or ``max_steps``."""
+        taken = 0
+        while not self.all_done():
+            k = chunk if max_steps is None else min(chunk, max_steps - taken)
+            if k <= 0:
+                break
+            self.steps(k)
+            taken += k
+        return taken
+
+    # -- results (code/SA_RRG.py:86-88) ---------------------------------------
+    def conf(self):
+        """(R, n) int64 +-1 current configurations."""
+        return unpack(self.s, self.n, self.R)
+
+    def results(self):
+        conf = self.conf()
+        return {
+            "mag_reached": (conf.sum(dim=1).double() / self.n).cpu().numpy(),
+            "num_steps": self.t.cpu().numpy().astype(np.float64),
+            "conf": conf.cpu().numpy(),
+            "done": self.done.cpu().numpy(),
+            "near_ties": self.ties.cpu().numpy(),
+        }
+
+
+def _sum_end(g, s, T):
+    """sum(s_endstate(s)) via one device rollout with the fused +1 count."""
+    from .dynamics import popcount
+    bits = pack(s)
+    cnt = torch.zeros(1, dtype=torch.int64, device=bits.device)
+    if T:
+        rollout(g, bits, T, counts=cnt)
+    else:
+        popcount(bits, g.n, counts=cnt)
+    return 2 * int(cnt.item()) - g.n
+
+
+def E_delta(N, s0, a, b, p, c, i):
+    """E(s with s_i flipped) - E(s) (code/SA_RRG.py:32-37), two device rollouts.
+
+    The integer sums come from the kernels; the float combination keeps the
+    reference's operation order ((-2*a)*s_i + b*D)/n in Python floats.
+    """
+    g = as_graph(N)
+    s = _device.to_device(s0)
+    T = int(p) + int(c) - 1
+    s1 = s.clone()
+    s1[int(i)] = -s1[int(i)]
+    sum1 = _sum_end(g, s, T)
+    sum2 = _sum_end(g, s1, T)
+    si = int(s[int(i)].item())
+    return (-2 * a * si + b * (sum1 - sum2)) / g.n
+
+
+def sa_run(d, n, p, c, par_a=PAR_A, par_b=PAR_B, N_stat=5, seed=0, seeds=None, N=None, graph_seed=None,
+           max_steps=None):
+    """Drop-in for the SA_RRG.py experiment (code/SA_RRG.py:44-92).
+
+    Returns the reference's output arrays ``mag_reached, num_steps, conf,
+    graphs`` (the np.savez keys of code/SA_RRG.py:92).  All N_stat replicas
+    share one graph (``N`` if given, else a random d-regular graph) and replica
+    k uses numpy seed ``seeds[k]`` (default seed + k).
+    """
+    from .graph import random_regular_graph
+    if N is None:
+        N = random_regular_graph(d, n, seed=graph_seed)
+    N = np.asarray(N)
+    if seeds is None:
+        seeds = [seed + k for k in range(N_stat)]
+    sa = SAReplicas(N, p, c, seeds, par_a=par_a, par_b=par_b)
+    sa.run(max_steps=max_steps)
+    res = sa.results()
+    res["graphs"] = np.broadcast_to(N.astype(int), (len(seeds),) + N.shape).copy()
+    return res

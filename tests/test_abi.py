@@ -1,0 +1,64 @@
+"""The C ABI library loads and exports every symbol include/mjx.h declares.
+CPU only: no compute call is made (argument validation only)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "mjx.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(mjx_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_entry_points():
+    names = declared_functions()
+    for must in ("mjx_rollout_ell_rp", "mjx_rollout_ell_np", "mjx_rollout_csr_rp", "mjx_rollout_csr_np",
+                 "mjx_sa_init", "mjx_sa_steps", "mjx_pack_rp", "mjx_popcount_rp"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol(mjx_mod):
+    lib = mjx_mod.load_library()
+    raw = ctypes.CDLL(mjx_mod.lib_path())
+    for name in declared_functions():
+        assert hasattr(raw, name), f"{name} declared in mjx.h but not exported"
+        assert name in mjx_mod._lib.SIGNATURES, f"{name} has no ctypes signature"
+    assert lib.mjx_abi_version() == 1
+
+
+def test_sa_state_struct_matches_header(mjx_mod):
+    src = open(HEADER).read()
+    body = src[src.index("typedef struct mjx_sa_state"):src.index("} mjx_sa_state;")]
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    fields = re.findall(r"\*\s*([A-Za-z_]+);", body)
+    assert fields == [f for f, _ in mjx_mod._lib.MjxSaState._fields_]
+
+
+def test_invalid_arguments_return_status_without_gpu(mjx_mod):
+    lib = mjx_mod.load_library()
+    EINVAL = 1
+    assert lib.mjx_pack_np(None, 4, 10, None, None) == EINVAL
+    assert lib.mjx_pack_np(None, 3, 0, None, None) == 0          # n == 0: nothing to do
+    assert lib.mjx_rollout_ell_rp(None, 10, 4, 0, None, None, None, 1, None, None) == EINVAL
+    assert lib.mjx_rollout_ell_np(None, -1, 4, None, None, None, 1, None, None) == EINVAL
+    assert lib.mjx_sa_steps(None, 10, 4, 1, 1, 64, None, None, None, None, 1, 1.0, 1.0, 1.0, 1.0, 1, None) == EINVAL
+    assert lib.mjx_strerror(EINVAL) == b"invalid argument"
+
+
+def test_product_path_fails_loudly_without_gpu(mjx_mod):
+    import numpy as np
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    adj = mjx_mod.random_regular_graph(4, 64, seed=0)
+    with pytest.raises(mjx_mod.MjxError):
+        mjx_mod.onestep_majority(adj, np.ones(64, dtype=np.int64))
+    with pytest.raises(mjx_mod.MjxError):
+        mjx_mod.SAReplicas(adj, 1, 1, [0])

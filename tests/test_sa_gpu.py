@@ -1,0 +1,107 @@
+"""GPU parity of the simulated-annealing path (rows a5-a6 of SURVEY.md 8a).
+
+Bar: bit-exact — the proposal sequence i_t, every accept decision, every
+sum(s_endstate) and delta_H (float64, same operation order), the final conf,
+num_steps and mag_reached equal the reference's (tests/golden/sa_*.npz were
+produced by the reference's own SA code on numpy's seeded global stream).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+from oracle import majority as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def test_sa_init_draws_reference_s0(mjx_mod):
+    z = load_golden("sa_d4_n200_p3c1.npz")
+    seeds = [int(s) for s in z["seeds"]]
+    sa = mjx_mod.SAReplicas(z["N"], 3, 1, seeds)
+    conf = sa.conf().cpu().numpy()
+    for r, sd in enumerate(seeds):
+        assert np.array_equal(conf[r], z[f"seed{sd}_s0"])
+    # s0 of many seeds against numpy directly (ragged R, n not multiple of 64)
+    n = 777
+    adj = mjx_mod.random_regular_graph(4, n, seed=1)
+    seeds = list(range(1000, 1000 + 150))
+    sa = mjx_mod.SAReplicas(adj, 1, 1, seeds)
+    conf = sa.conf().cpu().numpy()
+    for r, sd in enumerate(seeds):
+        rs = np.random.RandomState(sd)
+        assert np.array_equal(conf[r], 2 * rs.binomial(n=1, p=0.5, size=[n]) - 1)
+
+
+@pytest.mark.parametrize("name", ["sa_d4_n200_p3c1.npz", "sa_d3_n300_p2c1.npz", "sa_d4_n200_p1c1.npz",
+                                  "sa_d4_n1000_p2c2.npz"])
+def test_sa_trace_bit_exact(mjx_mod, name):
+    z = load_golden(name)
+    N, p, c = z["N"], int(z["p"]), int(z["c"])
+    seeds = [int(s) for s in z["seeds"]]
+    sa = mjx_mod.SAReplicas(N, p, c, seeds)
+    lens = [len(z[f"seed{sd}_i"]) for sd in seeds]
+    steps = max(lens)
+    done_at = 0
+    chunk = 2000
+    while done_at < steps:
+        k = min(chunk, steps - done_at)
+        tr = {key: v.cpu().numpy() for key, v in sa.steps(k, trace=True).items()}
+        for r, sd in enumerate(seeds):
+            L = lens[r]
+            lo, hi = done_at, min(done_at + k, L)
+            if hi > lo:
+                sl = slice(0, hi - lo)
+                assert np.array_equal(tr["i"][sl, r], z[f"seed{sd}_i"][lo:hi]), (sd, lo)
+                assert np.array_equal(tr["accept"][sl, r], z[f"seed{sd}_accept"][lo:hi]), (sd, lo)
+                assert np.array_equal(tr["sum_end"][sl, r], z[f"seed{sd}_sum_end"][lo:hi]), (sd, lo)
+                assert np.array_equal(tr["dE"][sl, r], z[f"seed{sd}_dE"][lo:hi]), (sd, lo)
+            if hi - lo < k and int(z[f"seed{sd}_converged"]):
+                # replica finished inside this chunk: it must be frozen afterwards
+                assert (tr["i"][hi - lo:, r] == -1).all()
+                assert (tr["accept"][hi - lo:, r] == -1).all()
+        done_at += k
+    res = sa.results()
+    for r, sd in enumerate(seeds):
+        if int(z[f"seed{sd}_converged"]):
+            assert res["done"][r] == 1
+            assert res["num_steps"][r] == float(z[f"seed{sd}_num_steps"])
+            assert np.array_equal(res["conf"][r], z[f"seed{sd}_conf"])
+            assert res["mag_reached"][r] == float(z[f"seed{sd}_mag_reached"])
+        else:
+            assert np.array_equal(res["conf"][r], z[f"seed{sd}_conf"])
+    assert int(res["near_ties"].sum()) == 0
+
+
+def test_sa_run_matches_full_reference_script(mjx_mod):
+    full = load_golden("sa_fullscript.npz")
+    N = full["n200_d4_p3_graphs"][0]
+    res = mjx_mod.sa_run(4, 200, 3, 1, N_stat=1, seeds=[0], N=N)
+    assert res["num_steps"][0] == full["n200_d4_p3_num_steps"][0]
+    assert np.array_equal(res["conf"][0], full["n200_d4_p3_conf"][0])
+    assert res["mag_reached"][0] == full["n200_d4_p3_mag_reached"][0]
+    assert np.array_equal(res["graphs"][0], N)
+
+
+def test_sa_many_replicas_vs_oracle(mjx_mod):
+    """R = 200 replicas (ragged: 4 words, 56 padding bits) on a fresh graph,
+    3000 steps, every replica's accept sequence against the oracle."""
+    n, d, p, c = 500, 3, 2, 1
+    adj = mjx_mod.random_regular_graph(d, n, seed=42)
+    seeds = list(range(200))
+    sa = mjx_mod.SAReplicas(adj, p, c, seeds)
+    tr = {k: v.cpu().numpy() for k, v in sa.steps(600, trace=True).items()}
+    for r in (0, 1, 63, 64, 127, 199):
+        o = orc.sa_loop(adj, p, c, seeds[r], max_steps=600, trace=True)["trace"]
+        L = len(o["i"])
+        assert np.array_equal(tr["i"][:L, r], o["i"])
+        assert np.array_equal(tr["accept"][:L, r], o["accept"])
+        assert np.array_equal(tr["sum_end"][:L, r], o["sum_end"])
+        assert np.array_equal(tr["dE"][:L, r], o["dE"])
+
+
+def test_E_delta_matches_oracle(mjx_mod):
+    z = load_golden("rrg_dyn.npz")
+    N, s0 = z["d4_n1000_N"], z["d4_n1000_s0"][0]
+    for (a, b, p, c, i) in [(15.0, 10.0, 1, 1, 3), (150.3, 77.7, 2, 1, 999), (1.5, 4000.0, 3, 1, 0)]:
+        assert mjx_mod.E_delta(N, s0, a, b, p, c, i) == orc.E_delta(N, s0, a, b, p, c, i)

@@ -1,0 +1,37 @@
+#!/bin/bash
+# One GPU-box session: parity tests, bench, rocprofv3 kernel-trace summary.
+# Every GPU step has its own time limit; a crash/timeout (exit status other
+# than 0 = pass or 1 = test failures) ends the script before the next step.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out
+mkdir -p $OUT
+export PYTHONUNBUFFERED=1
+stop_if_fatal() {  # $1 = status, $2 = step name
+  if [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; then
+    echo "FATAL: step $2 exited with $1; no further GPU steps" | tee -a $OUT/steps.log
+    exit "$1"
+  fi
+  echo "step $2 -> $1" | tee -a $OUT/steps.log
+}
+STEPS="${STEPS:-tests bench prof}"
+for s in $STEPS; do
+  case $s in
+    tests)
+      timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+        ${PYTEST_ARGS:-} > $OUT/pytest_gpu.log 2>&1
+      stop_if_fatal $? tests ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
+      stop_if_fatal $? smoke ;;
+    bench)
+      timeout -k 10 400 python -u bench.py ${BENCH_ARGS:-} > $OUT/bench.log 2>&1
+      stop_if_fatal $? bench ;;
+    prof)
+      ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats \
+          -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run --output-format csv -- \
+          python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline ${BENCH_ARGS:-} ) > $OUT/prof.log 2>&1
+      stop_if_fatal $? prof ;;
+  esac
+done
+echo done
