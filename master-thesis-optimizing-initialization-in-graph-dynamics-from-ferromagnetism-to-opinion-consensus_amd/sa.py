@@ -135,11 +135,12 @@ class SAReplicas:
         return unpack(self.s, self.n, self.R)
 
     def results(self):
-        conf = self.conf()
+        conf = self.conf().cpu().numpy()
         return {
-            "mag_reached": (conf.sum(dim=1).double() / self.n).cpu().numpy(),
+            # m(s) = np.sum(s)/n with numpy's true division (code/SA_RRG.py:39-40,86)
+            "mag_reached": np.sum(conf, axis=1) / self.n,
             "num_steps": self.t.cpu().numpy().astype(np.float64),
-            "conf": conf.cpu().numpy(),
+            "conf": conf,
             "done": self.done.cpu().numpy(),
             "near_ties": self.ties.cpu().numpy(),
         }
