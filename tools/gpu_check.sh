@@ -32,6 +32,16 @@ for s in $STEPS; do
           -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run --output-format csv -- \
           python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline ${BENCH_ARGS:-} ) > $OUT/prof.log 2>&1
       stop_if_fatal $? prof ;;
+    pmc)
+      R="$GRAFT_REPO_ROOT"
+      ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE \
+          -d "$R/$OUT/pmc_fetch" -o run --output-format csv -- python3 "$R/tools/pmc_run.py" ) > $OUT/pmc_fetch.log 2>&1
+      stop_if_fatal $? pmc_fetch
+      ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE \
+          -d "$R/$OUT/pmc_write" -o run --output-format csv -- python3 "$R/tools/pmc_run.py" ) > $OUT/pmc_write.log 2>&1
+      stop_if_fatal $? pmc_write
+      python3 tools/pmc_parse.py $OUT/pmc_fetch $OUT/pmc_write $((1024*1024*1024)) $OUT/pmc_traffic.json > $OUT/pmc_parse.log 2>&1
+      echo "pmc parse -> $?" | tee -a $OUT/steps.log ;;
   esac
 done
 echo done

@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Turn rocprofv3 --pmc CSVs (FETCH_SIZE pass, WRITE_SIZE pass) into
+profiles/pmc_traffic.json: measured HBM bytes per launch of each kernel.
+
+Correction (MI355X_MICROARCH.md, HBM): FETCH_SIZE/WRITE_SIZE are in KiB;
+on gfx950 FETCH_SIZE reads half the bytes of a wide (16 B/lane) coalesced
+stream, so the read side is doubled.  The calibration copy of tools/pmc_run.py
+(known byte count) is reported beside it so the factor can be checked on the
+same box: calib.read_factor = known read bytes / (FETCH_SIZE*1024).
+
+usage: pmc_parse.py FETCH_DIR WRITE_DIR CALIB_BYTES OUT_JSON
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def load(dirname, counter):
+    """kernel name -> list of counter values (one per dispatch)."""
+    vals = defaultdict(list)
+    files = glob.glob(os.path.join(dirname, "**", "*counter_collection*.csv"), recursive=True)
+    for f in files:
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row.get("Counter_Name") != counter:
+                    continue
+                vals[row["Kernel_Name"]].append(float(row["Counter_Value"]))
+    return vals
+
+
+def short(name):
+    return name.split("(")[0].replace("void ", "").strip()
+
+
+def main():
+    fdir, wdir, calib_bytes, out = sys.argv[1], sys.argv[2], float(sys.argv[3]), sys.argv[4]
+    fetch = load(fdir, "FETCH_SIZE")
+    write = load(wdir, "WRITE_SIZE")
+    res = {"_method": ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
+                       "tools/pmc_run.py; bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 per dispatch "
+                       "(gfx950 FETCH_SIZE half-count correction), averaged over dispatches")}
+    for k in sorted(set(fetch) | set(write)):
+        f = fetch.get(k, [])
+        w = write.get(k, [])
+        fk = sum(f) / len(f) if f else 0.0
+        wk = sum(w) / len(w) if w else 0.0
+        entry = {"dispatches": max(len(f), len(w)), "fetch_kib": fk, "write_kib": wk,
+                 "read_bytes_corrected": 2 * fk * 1024, "write_bytes": wk * 1024,
+                 "bytes_per_launch": 2 * fk * 1024 + wk * 1024}
+        res[short(k)] = entry
+    # calibration: the copy dispatch with the largest write
+    cands = [(v["write_bytes"], k) for k, v in res.items() if not k.startswith("_") and "copy" in k.lower()]
+    if cands:
+        _, ck = max(cands)
+        c = res[ck]
+        res["_calibration"] = {
+            "kernel": ck, "known_read_bytes": calib_bytes, "known_write_bytes": calib_bytes,
+            "fetch_bytes_raw": c["fetch_kib"] * 1024, "write_bytes_raw": c["write_bytes"],
+            "read_factor": calib_bytes / max(1.0, c["fetch_kib"] * 1024),
+            "write_factor": calib_bytes / max(1.0, c["write_bytes"]),
+        }
+    # bench.py key: the fused-count sweep and the plain sweep of the rollout
+    sweeps = [v for k, v in res.items() if k.startswith("mjx::k_sweep_ell_rp") or "k_sweep_ell_rp" in k]
+    if sweeps:
+        tot = sum(v["bytes_per_launch"] * v["dispatches"] for v in sweeps)
+        cnt = sum(v["dispatches"] for v in sweeps)
+        res["k_sweep_ell_rp"] = {"bytes_per_launch": tot / cnt, "dispatches": cnt}
+    os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
