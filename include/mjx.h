@@ -49,6 +49,9 @@ extern "C" {
 #define MJX_I8   1
 #define MJX_I32  4
 #define MJX_I64  8
+/* floating-point element types (HPR / BDCM message arrays) */
+#define MJX_F32  104
+#define MJX_F64  108
 
 int         mjx_abi_version(void);            /* bumps on any signature change */
 const char* mjx_strerror(int status);
@@ -133,6 +136,38 @@ int mjx_sa_steps(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R,
                  mjx_sa_state* st, int64_t nsteps,
                  double par_a, double par_b, double a_cap, double b_cap, int64_t t_cap,
                  void* stream);
+
+/* ---- history-passing reinforcement on d-regular graphs ------------------ */
+/*
+ * Message arrays use the reference's layout (code/HPR_pytorch_RRG.py:277-285, 46-61):
+ * chi[2E][4^T], T = p+c, E = n*d/2; row r < E is G.edges[r] = (u,v) as the
+ * message u->v, row r+E is v->u; column of (x_a, x_b) is idx(x_a)*2^T + idx(x_b)
+ * with idx(x) = sum_k [x_k = -1] 2^(T-1-k).  Node-major plan arrays, all [n*d]:
+ *   nbr[a*d+m]     = m-th neighbour k_m of a
+ *   in_row[a*d+m]  = row of the message k_m -> a
+ *   out_row[a*d+m] = row of the message a -> k_m   (the reference's N_edges_pos)
+ * biases[n][2]: column 0 = bias of spin +1.  dtype MJX_F32 or MJX_F64 for chi,
+ * biases, marginals and zwork.
+ */
+/* HPr_dp (code/HPR_pytorch_RRG.py:183-218): chi_out = damp*chi_new/rowsum +
+ * (1-damp)*chi_in, where chi_new carries the reinforced incoming messages
+ * (new_biases_chi, :128-133) and the trajectory factor A (:14-39).
+ * w_plus / w_minus = exp(-lmbd_in*x_a[0]/n) for x_a[0] = +1 / -1.
+ * Supported: 2 <= p+c <= 4, 2 <= d <= 6 (MJX_ERANGE otherwise).
+ * chi_in may not alias chi_out. */
+int mjx_hpr_update(int dtype, const void* chi_in, void* chi_out, const void* biases,
+                   const int32_t* nbr, const int32_t* in_row, const int32_t* out_row,
+                   int64_t n, int d, int p, int c, int attr_value,
+                   double w_plus, double w_minus, double damp, void* stream);
+/* marginals_comp (code/HPR_pytorch_RRG.py:147-167): marg[n][2] (column 0 = +1).
+ * zwork: 4E elements of dtype (per-row normalised Z+, Z-). */
+int mjx_hpr_marginals(int dtype, const void* chi, const int32_t* out_row, int64_t n, int d,
+                      int p, int c, double eps, void* zwork, void* marg, void* stream);
+/* new_biases_i (code/HPR_pytorch_RRG.py:137-145) with the uniforms u[n] (float64) the
+ * reference draws by torch.rand(n); thresh = 1-(1+t)^(-gamma).  Updates biases in
+ * place and writes s[n] = +-1 (int32, nullable). */
+int mjx_hpr_new_biases(int dtype, void* biases, const void* marg, const double* u, double thresh,
+                       double pie, int64_t n, int32_t* s, void* stream);
 
 #ifdef __cplusplus
 }

@@ -11,12 +11,14 @@ from .graph import (Graph, neighbours, csr_from_networkx, random_regular_graph, 
                     erdos_renyi, erdos_renyi_edges, csr_from_edges, remove_isolated)
 from .dynamics import onestep_majority, s_endstate, m, pack, unpack, rollout, popcount, as_graph
 from .sa import SAReplicas, E_delta, sa_run, schedule_constants
+from .hpr import HPRPlan, HPRState, HPr_dp, marginals_comp, new_biases_i, hpr_run
 
 __all__ = [
     "MjxError", "lib_path", "Graph", "neighbours", "csr_from_networkx", "random_regular_graph",
     "random_regular_edges", "erdos_renyi", "erdos_renyi_edges", "csr_from_edges", "remove_isolated",
     "onestep_majority", "s_endstate", "m", "pack", "unpack", "rollout", "popcount", "as_graph",
     "SAReplicas", "E_delta", "sa_run", "schedule_constants",
+    "HPRPlan", "HPRState", "HPr_dp", "marginals_comp", "new_biases_i", "hpr_run",
 ]
 
 

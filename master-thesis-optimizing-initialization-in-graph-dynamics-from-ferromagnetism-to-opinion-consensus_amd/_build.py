@@ -19,6 +19,9 @@ ARCH = "gfx950"
 UNITS = [
     ("mjx_dynamics.hip", []),
     ("mjx_sa.hip", ["-ffp-contract=off"]),
+    ("mjx_hpr.hip", []),
+    ("mjx_hpr_f32.hip", []),
+    ("mjx_hpr_f64.hip", []),
 ]
 
 
@@ -48,14 +51,22 @@ def build(force=False, verbose=True):
     os.makedirs(objdir, exist_ok=True)
     base = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
             "-Wno-unused-function", "-I", INCLUDE]
-    objs = []
+    objs, cmds = [], []
     for src, extra in UNITS:
         obj = os.path.join(objdir, src.replace(".hip", ".o"))
-        cmd = base + extra + ["-c", os.path.join(CSRC, src), "-o", obj]
+        cmds.append(base + extra + ["-c", os.path.join(CSRC, src), "-o", obj])
+        objs.append(obj)
+    # translation units compile in parallel (the HPR instantiation units dominate)
+    from concurrent.futures import ThreadPoolExecutor
+    jobs = max(1, min(len(cmds), os.cpu_count() or 1, 8))
+
+    def run(cmd):
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
-        objs.append(obj)
+
+    with ThreadPoolExecutor(jobs) as ex:
+        list(ex.map(run, cmds))
     tmp = LIB + ".tmp"
     cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
     if verbose:

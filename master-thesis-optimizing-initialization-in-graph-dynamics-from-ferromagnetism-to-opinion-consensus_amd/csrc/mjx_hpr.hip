@@ -1,0 +1,66 @@
+// C ABI of the HPR kernels (code/HPR_pytorch_RRG.py:137-218); kernels in mjx_hpr_impl.h.
+#include "mjx_hpr_impl.h"
+
+
+using namespace mjx;
+using namespace mjx::hpr;
+
+extern "C" int mjx_hpr_update(int dtype, const void* chi_in, void* chi_out, const void* biases, const int32_t* nbr,
+                              const int32_t* in_row, const int32_t* out_row, int64_t n, int d, int p, int c,
+                              int attr_value, double w_plus, double w_minus, double damp, void* stream) {
+    if (n < 1 || d < 2 || p < 1 || c < 1 || (attr_value != 1 && attr_value != -1)) return MJX_EINVAL;
+    if (!chi_in || !chi_out || !biases || !nbr || !in_row || !out_row || chi_in == chi_out) return MJX_EINVAL;
+    if (n * (int64_t)d > (int64_t)INT32_MAX) return MJX_ERANGE;
+    const int ap = attr_value > 0 ? 1 : 0;
+    hipStream_t st = as_stream(stream);
+    if (dtype == MJX_F32)
+        return update_f32(chi_in, chi_out, biases, nbr, in_row, out_row, n, d, p, c, ap, w_plus, w_minus, damp, st);
+    if (dtype == MJX_F64)
+        return update_f64(chi_in, chi_out, biases, nbr, in_row, out_row, n, d, p, c, ap, w_plus, w_minus, damp, st);
+    return MJX_EINVAL;
+}
+
+template <typename S>
+static int marginals_impl(const void* chi, const int32_t* out_row, int64_t n, int d, int T, double eps, void* zwork,
+                          void* marg, hipStream_t st) {
+    const int64_t E = n * (int64_t)d / 2;
+    S* zp = (S*)zwork;
+    S* zm = zp + 2 * E;
+    const int grid = grid_for(E * 64 / 4);
+    switch (T) {
+        case 2: k_hpr_edge_z<S, 2><<<grid, 256, 0, st>>>((const S*)chi, E, (S)eps, zp, zm); break;
+        case 3: k_hpr_edge_z<S, 3><<<grid, 256, 0, st>>>((const S*)chi, E, (S)eps, zp, zm); break;
+        case 4: k_hpr_edge_z<S, 4><<<grid, 256, 0, st>>>((const S*)chi, E, (S)eps, zp, zm); break;
+        case 5: k_hpr_edge_z<S, 5><<<grid, 256, 0, st>>>((const S*)chi, E, (S)eps, zp, zm); break;
+        default: return MJX_ERANGE;
+    }
+    MJX_LAUNCH_CHECK("k_hpr_edge_z");
+    k_hpr_node_marg<S><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(zp, zm, out_row, n, d, (S*)marg);
+    MJX_LAUNCH_CHECK("k_hpr_node_marg");
+    return MJX_OK;
+}
+
+extern "C" int mjx_hpr_marginals(int dtype, const void* chi, const int32_t* out_row, int64_t n, int d, int p, int c,
+                                 double eps, void* zwork, void* marg, void* stream) {
+    if (n < 1 || d < 1 || p < 1 || c < 1 || !chi || !out_row || !zwork || !marg) return MJX_EINVAL;
+    if ((n * (int64_t)d) % 2) return MJX_EINVAL;
+    hipStream_t st = as_stream(stream);
+    if (dtype == MJX_F32) return marginals_impl<float>(chi, out_row, n, d, p + c, eps, zwork, marg, st);
+    if (dtype == MJX_F64) return marginals_impl<double>(chi, out_row, n, d, p + c, eps, zwork, marg, st);
+    return MJX_EINVAL;
+}
+
+extern "C" int mjx_hpr_new_biases(int dtype, void* biases, const void* marg, const double* u, double thresh,
+                                  double pie, int64_t n, int32_t* s, void* stream) {
+    if (n < 1 || !biases || !marg || !u) return MJX_EINVAL;
+    hipStream_t st = as_stream(stream);
+    const unsigned grid = (unsigned)((n + 255) / 256);
+    if (dtype == MJX_F32)
+        k_hpr_new_biases<float><<<grid, 256, 0, st>>>((float*)biases, (const float*)marg, u, thresh, (float)pie, n, s);
+    else if (dtype == MJX_F64)
+        k_hpr_new_biases<double><<<grid, 256, 0, st>>>((double*)biases, (const double*)marg, u, thresh, pie, n, s);
+    else
+        return MJX_EINVAL;
+    MJX_LAUNCH_CHECK("k_hpr_new_biases");
+    return MJX_OK;
+}

@@ -1,0 +1,435 @@
+// History-passing reinforcement (HPR) on d-regular graphs: the edge-message
+// update, node marginals and bias refresh of code/HPR_pytorch_RRG.py.
+//
+// Message layout (the reference's, so chi arrays are drop-in):
+//   row r < E  : G.edges[r] = (u, v), message u -> v;  row r + E: v -> u
+//                (code/HPR_pytorch_RRG.py:277-285)
+//   column of (x_a, x_b) = idx(x_a) * 2^T + idx(x_b), idx(x) = sum_k [x_k = -1] 2^(T-1-k)
+//                (order_gpu, code/HPR_pytorch_RRG.py:46-61)
+//
+// HPr_dp (code/HPR_pytorch_RRG.py:183-218) for the message a -> b:
+//   chi_new(x_a, x_b) = w(x_a[0]) [x_a[T-1] = attr] sum_{x_k1..} prod_m M_m(x_km, x_a)
+//                        * prod_t allowed_t(rho_t, x_b[t])
+//   M_m(x_k, x_a) = bias_{k_m}(x_k[0]) chi^{k_m -> a}(x_k, x_a), rho_t = number of +1
+//   among the d-1 incoming neighbours at time t, allowed_t = the majority /
+//   always-stay trajectory condition (t < T-1) or the attractor condition
+//   (t = T-1) of code/HPR_pytorch_RRG.py:14-29, w = exp(-lmbd x_a[0]/n).
+//
+// Evaluation here (exact rearrangement of the same sum, no approximation):
+//   * the count table of the first d-2 incoming neighbours is built by direct
+//     convolution in registers (base d-1 digits per time step);
+//   * allowed_t is a one-sided interval in rho_t whose direction depends only on
+//     x_a, so the table is turned into directional cumulative sums once per x_a;
+//   * the last neighbour is folded in as out(x_b) = sum_x M_last(x) CS[corner(x, x_b)].
+//   x_a is a compile-time constant per wave (template), so every index above is
+//   resolved at compile time and the state never leaves VGPRs.
+// Work per (edge, valid x_a) at d=4, T=4: 256 + ~220 + <=256 FMAs/adds.
+//
+// Kernel geometry: a workgroup owns a tile of NT = 64/d nodes; lane = one
+// outgoing message (node a, neighbour slot m) of the tile; wave w handles the
+// valid x_a values 2q(+1), q in [w*XPW, (w+1)*XPW).  The d incoming rows of each
+// tile node (every incoming message is read once per update) are staged in LDS
+// with a +1 pad per row (conflict-free strided reads).
+#pragma once
+#include "mjx_common.h"
+#include <type_traits>
+#include <utility>
+
+namespace mjx {
+namespace hpr {
+
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+
+constexpr int ipow(int b, int e) { return e == 0 ? 1 : b * ipow(b, e - 1); }
+// spin (+1/-1) of trajectory index x at time t (index bit = 1 means -1)
+constexpr int spin(int x, int t, int T) { return ((x >> (T - 1 - t)) & 1) ? -1 : 1; }
+constexpr int bit01(int x, int t, int T) { return spin(x, t, T) > 0 ? 1 : 0; }
+constexpr int digit(int idx, int t, int T, int base) { return (idx / ipow(base, T - 1 - t)) % base; }
+constexpr int maxdigit(int idx, int T, int base) {
+    int m = 0;
+    for (int t = 0; t < T; ++t) m = digit(idx, t, T, base) > m ? digit(idx, t, T, base) : m;
+    return m;
+}
+constexpr int xoff(int x, int T, int base) {
+    int o = 0;
+    for (int t = 0; t < T; ++t) o += bit01(x, t, T) * ipow(base, T - 1 - t);
+    return o;
+}
+constexpr int floor_div2(int a) { return a >= 0 ? a / 2 : -((-a + 1) / 2); }
+constexpr int ceil_div2(int a) { return -floor_div2(-a); }
+
+// target spin s_t and reference spin prev_t of the condition on time t
+constexpr int cond_s(int XA, int t, int T, int P) { return t < T - 1 ? spin(XA, t + 1, T) : spin(XA, P, T); }
+constexpr int cond_prev(int XA, int t, int T) { return t < T - 1 ? spin(XA, t, T) : spin(XA, T - 1, T); }
+
+// Corner of the table box for last-neighbour trajectory x and receiver x_b, or -1
+// when the box is empty.  Table digits rho_t in [0, K] count the +1 spins of the
+// first K = d-2 incoming neighbours; the last one adds bit01(x, t).
+// sigma_t = 2(rho_t + b) - (d-1) + y_t  (code/HPR_pytorch_RRG.py:212, rho -> 2 rho - d + 1).
+constexpr int corner(int XA, int x, int XB, int T, int P, int D) {
+    const int K = D - 2, base = K + 1;
+    int idx = 0;
+    for (int t = 0; t < T; ++t) {
+        const int s = cond_s(XA, t, T, P), prev = cond_prev(XA, t, T);
+        const int b = bit01(x, t, T), y = spin(XB, t, T);
+        int dg;
+        if (s > 0) {   // sigma > 0, or sigma == 0 and prev == +1
+            const int thr = prev > 0 ? 0 : 1;
+            int lo = ceil_div2(D - 1 - y + thr) - b;
+            if (lo > K) return -1;
+            dg = lo < 0 ? 0 : lo;
+        } else {       // sigma < 0, or sigma == 0 and prev == -1
+            const int thr = prev < 0 ? 0 : -1;
+            int hi = floor_div2(D - 1 - y + thr) - b;
+            if (hi < 0) return -1;
+            dg = hi > K ? K : hi;
+        }
+        idx += dg * ipow(base, T - 1 - t);
+    }
+    return idx;
+}
+
+template <typename S> struct Vec16;
+template <> struct Vec16<float> { typedef float4 T; static constexpr int N = 4; };
+template <> struct Vec16<double> { typedef double2 T; static constexpr int N = 2; };
+
+template <typename S, int T, int P, int D>
+struct Cfg {
+    static constexpr int X = 1 << T;          // trajectories per node
+    static constexpr int NC = X * X;          // columns per message row
+    static constexpr int K = D - 2;           // neighbours in the register table
+    static constexpr int BASE = K + 1;
+    static constexpr int NS = ipow(BASE, T);  // table size
+    static constexpr int NT = 64 / D;         // nodes per tile
+    static constexpr int NL = NT * D;         // active lanes (messages) per tile
+    static constexpr int NVALID = X / 2;      // valid x_a per attr value
+    static constexpr int NW = NVALID < 4 ? NVALID : 4;
+    static constexpr int XPW = NVALID / NW;   // valid x_a per wave
+    static constexpr int STRIDE = NC + 1;     // padded LDS row stride (elements)
+    static constexpr size_t LDS = (size_t)NL * STRIDE * sizeof(S) + (size_t)NL * 2 * sizeof(S) +
+                                  (size_t)NW * 64 * sizeof(S);
+};
+
+// Compile-time index tables of one (T, P, D, XA) instance.
+template <int T, int P, int D, int XA>
+struct Tabs {
+    static constexpr int X = 1 << T, K = D - 2, BASE = K + 1, NS = ipow(BASE, T);
+    struct Data {
+        int xo[X];               // table offset of a neighbour trajectory
+        int maxd[NS];            // largest digit of a table index
+        int dg[T][NS];           // digit t of a table index
+        int dir[T];              // +1: suffix sums in dim t, -1: prefix sums
+        int cn[X][X];            // corner(x, xb) or -1
+    };
+    static constexpr Data make() {
+        Data d{};
+        for (int x = 0; x < X; ++x) d.xo[x] = xoff(x, T, BASE);
+        for (int i = 0; i < NS; ++i) {
+            d.maxd[i] = maxdigit(i, T, BASE);
+            for (int t = 0; t < T; ++t) d.dg[t][i] = digit(i, t, T, BASE);
+        }
+        for (int t = 0; t < T; ++t) d.dir[t] = cond_s(XA, t, T, P);
+        for (int x = 0; x < X; ++x)
+            for (int xb = 0; xb < X; ++xb) d.cn[x][xb] = corner(XA, x, xb, T, P, D);
+        return d;
+    }
+    static constexpr Data v = make();
+};
+
+// out[XB] for one compile-time x_a; returns the partial row sum.
+template <typename S, int T, int P, int D, int XA>
+__device__ __forceinline__ S xa_messages(const S* __restrict__ rows, const S* __restrict__ bias, int a_local, int m,
+                                         S w, S (&out)[1 << T]) {
+    using C = Cfg<S, T, P, D>;
+    using TB = Tabs<T, P, D, XA>;
+    constexpr int X = C::X, K = C::K, BASE = C::BASE, NS = C::NS;
+    // M_j(x) for the d-1 incoming neighbours other than the receiver (slot m)
+    S M[D - 1][X];
+#pragma unroll
+    for (int j = 0; j < D - 1; ++j) {
+        const int slot = a_local * D + (j < m ? j : j + 1);
+        const S bp = bias[2 * slot], bm = bias[2 * slot + 1];
+        const S* r = rows + slot * C::STRIDE + XA;
+#pragma unroll
+        for (int x = 0; x < X; ++x) M[j][x] = (x < X / 2 ? bp : bm) * r[x * X];
+    }
+    // count table of the first K neighbours
+    S tab[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) tab[i] = S(0);
+    if constexpr (K == 0) {
+        tab[0] = S(1);
+    } else {
+#pragma unroll
+        for (int x = 0; x < X; ++x) tab[TB::v.xo[x]] = M[0][x];
+#pragma unroll
+        for (int j = 1; j < K; ++j) {
+            S nxt[NS];
+#pragma unroll
+            for (int i = 0; i < NS; ++i) nxt[i] = S(0);
+#pragma unroll
+            for (int i = 0; i < NS; ++i) {
+                if (TB::v.maxd[i] <= j) {   // table holds j neighbours: digits <= j
+#pragma unroll
+                    for (int x = 0; x < X; ++x) nxt[i + TB::v.xo[x]] += tab[i] * M[j][x];
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < NS; ++i) tab[i] = nxt[i];
+        }
+    }
+    // directional cumulative sums: suffix in dims whose target spin is +1, prefix otherwise
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const int wt = ipow(BASE, T - 1 - t);
+        if (TB::v.dir[t] > 0) {
+#pragma unroll
+            for (int i = NS - 1; i >= 0; --i)
+                if (TB::v.dg[t][i] < K) tab[i] += tab[i + wt];
+        } else {
+#pragma unroll
+            for (int i = 0; i < NS; ++i)
+                if (TB::v.dg[t][i] > 0) tab[i] += tab[i - wt];
+        }
+    }
+    // fold in the last neighbour
+    S rs = S(0);
+#pragma unroll
+    for (int xb = 0; xb < X; ++xb) {
+        S acc = S(0);
+#pragma unroll
+        for (int x = 0; x < X; ++x) {
+            const int cn = TB::v.cn[x][xb];
+            if (cn >= 0) acc += M[D - 2][x] * tab[cn];
+        }
+        acc *= w;
+        out[xb] = acc;
+        rs += acc;
+    }
+    return rs;
+}
+
+template <typename S, int T, int P, int D>
+__global__ void __launch_bounds__((64 * Cfg<S, T, P, D>::NW))
+k_hpr_update(const S* __restrict__ chi_in, S* __restrict__ chi_out, const S* __restrict__ biases,
+             const int32_t* __restrict__ nbr, const int32_t* __restrict__ in_row, const int32_t* __restrict__ out_row,
+             int64_t n, int attr_plus, S w_plus, S w_minus, S damp) {
+    using C = Cfg<S, T, P, D>;
+    constexpr int X = C::X, NC = C::NC, NT = C::NT, NL = C::NL, NW = C::NW, XPW = C::XPW;
+    extern __shared__ __align__(16) unsigned char smem[];
+    S* rows = reinterpret_cast<S*>(smem);
+    S* bias = rows + NL * C::STRIDE;
+    S* red = bias + NL * 2;
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const int64_t a0 = (int64_t)blockIdx.x * NT;
+    const int nt = (int)((n - a0) < NT ? (n - a0) : NT);   // nodes in this tile
+    const int nl = nt * D;
+    // ---- stage the incoming rows of the tile's nodes and their sources' biases
+    {
+        using V = typename Vec16<S>::T;
+        constexpr int VN = Vec16<S>::N;
+        constexpr int VPR = NC / VN;                 // 16-B vectors per row
+        for (int q = tid; q < nl * VPR; q += 64 * NW) {
+            const int slot = q / VPR, v = q % VPR;
+            const int64_t r = in_row[a0 * D + slot];
+            const V x = reinterpret_cast<const V*>(chi_in + r * NC)[v];
+            const S* xs = reinterpret_cast<const S*>(&x);
+#pragma unroll
+            for (int k = 0; k < VN; ++k) rows[slot * C::STRIDE + v * VN + k] = xs[k];
+        }
+        for (int q = tid; q < nl; q += 64 * NW) {
+            const int64_t k = nbr[a0 * D + q];
+            bias[2 * q] = biases[2 * k];
+            bias[2 * q + 1] = biases[2 * k + 1];
+        }
+    }
+    __syncthreads();
+    const bool active = lane < nl;
+    const int a_local = lane / D, m = lane % D;
+    S out[XPW][X];
+    S rs = S(0);
+    if (active) {
+        static_for<0, XPW>([&](auto ii) {
+            constexpr int i = decltype(ii)::value;
+            // the x_a pair 2q, 2q+1 differ only in x_a[T-1]; attr picks the valid one
+            static_for<0, NW>([&](auto ww) {
+                constexpr int wv = decltype(ww)::value;
+                constexpr int q = wv * XPW + i;
+                if (wave == wv) {
+                    constexpr int XP = 2 * q, XM = 2 * q + 1;      // x_a[T-1] = +1 / -1
+                    const S wgt0 = (XP < X / 2) ? w_plus : w_minus;
+                    if (attr_plus) rs += xa_messages<S, T, P, D, XP>(rows, bias, a_local, m, wgt0, out[i]);
+                    else rs += xa_messages<S, T, P, D, XM>(rows, bias, a_local, m, wgt0, out[i]);
+                }
+            });
+        });
+    }
+    red[wave * 64 + lane] = rs;
+    __syncthreads();
+    if (!active) return;
+    S tot = S(0);
+#pragma unroll
+    for (int w = 0; w < NW; ++w) tot += red[w * 64 + lane];
+    // chi <- damp * chi_new / rowsum + (1 - damp) * chi_old   (code/HPR_pytorch_RRG.py:215)
+    const S inv = S(1) / tot;
+    const S keep = S(1) - damp;
+    const int64_t orow = out_row[(a0 + a_local) * D + m];
+    const S* old = chi_in + orow * NC;
+    S* dst = chi_out + orow * NC;
+#pragma unroll
+    for (int i = 0; i < XPW; ++i) {
+        const int q = wave * XPW + i;
+        const int cv = (attr_plus ? 2 * q : 2 * q + 1) * X;     // valid block
+        const int ci = (attr_plus ? 2 * q + 1 : 2 * q) * X;     // x_a[T-1] != attr: chi_new = 0
+#pragma unroll
+        for (int xb = 0; xb < X; ++xb) {
+            dst[cv + xb] = damp * (out[i][xb] * inv) + keep * old[cv + xb];
+            dst[ci + xb] = keep * old[ci + xb];
+        }
+    }
+}
+
+// ---- marginals (code/HPR_pytorch_RRG.py:147-167) ---------------------------
+// One group of LPE lanes per undirected edge r: Z sums of chi^{u->v}(x_u,x_v) chi^{v->u}(x_v,x_u)
+// by x_u[0] (row r) and by x_v[0] (row r+E), clamped at eps, normalised.
+template <typename S, int T>
+__global__ void __launch_bounds__(256) k_hpr_edge_z(const S* __restrict__ chi, int64_t E, S eps,
+                                                     S* __restrict__ zp, S* __restrict__ zm) {
+    constexpr int X = 1 << T, NC = X * X;
+    constexpr int LPE = NC < 64 ? NC : 64;
+    constexpr int EPW = 64 / LPE;
+    const int lane = threadIdx.x & 63;
+    const int g = lane / LPE, l = lane % LPE;
+    const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * 256) >> 6;
+    for (int64_t base = wave * EPW; base < E; base += nwaves * EPW) {
+        const int64_t r = base + g;
+        S fp = 0, fm = 0, bp = 0, bm = 0;
+        if (r < E) {
+            const S* f = chi + r * NC;
+            const S* b = chi + (r + E) * NC;
+            for (int j = l; j < NC; j += LPE) {
+                const int xa = j / X, xb = j % X;
+                const S z = f[j] * b[xb * X + xa];
+                if (xa < X / 2) fp += z; else fm += z;
+                if (xb < X / 2) bp += z; else bm += z;
+            }
+        }
+#pragma unroll
+        for (int off = LPE / 2; off > 0; off >>= 1) {
+            fp += __shfl_xor(fp, off, 64);
+            fm += __shfl_xor(fm, off, 64);
+            bp += __shfl_xor(bp, off, 64);
+            bm += __shfl_xor(bm, off, 64);
+        }
+        if (l == 0 && r < E) {
+            fp = fp > eps ? fp : eps; fm = fm > eps ? fm : eps;
+            bp = bp > eps ? bp : eps; bm = bm > eps ? bm : eps;
+            const S sf = fp + fm, sb = bp + bm;
+            zp[r] = fp / sf; zm[r] = fm / sf;
+            zp[r + E] = bp / sb; zm[r + E] = bm / sb;
+        }
+    }
+}
+
+template <typename S>
+__global__ void __launch_bounds__(256) k_hpr_node_marg(const S* __restrict__ zp, const S* __restrict__ zm,
+                                                        const int32_t* __restrict__ out_row, int64_t n, int d,
+                                                        S* __restrict__ marg) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    S p = 1, q = 1;
+    for (int m = 0; m < d; ++m) {
+        const int64_t r = out_row[i * d + m];
+        p *= zp[r];
+        q *= zm[r];
+    }
+    const S s = p + q;
+    marg[2 * i] = p / s;
+    marg[2 * i + 1] = q / s;
+}
+
+// new_biases_i (code/HPR_pytorch_RRG.py:137-145) with caller-supplied uniforms
+template <typename S>
+__global__ void __launch_bounds__(256) k_hpr_new_biases(S* __restrict__ biases, const S* __restrict__ marg,
+                                                         const double* __restrict__ u, double thresh, S pie,
+                                                         int64_t n, int32_t* __restrict__ s) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    S b0 = biases[2 * i], b1 = biases[2 * i + 1];
+    if (u[i] < thresh) {
+        const bool minus = marg[2 * i + 1] >= marg[2 * i];
+        b0 = minus ? pie : S(1) - pie;
+        b1 = minus ? S(1) - pie : pie;
+        biases[2 * i] = b0;
+        biases[2 * i + 1] = b1;
+    }
+    if (s) s[i] = b0 > b1 ? 1 : -1;
+}
+
+// ---- dispatch --------------------------------------------------------------
+template <typename S, int T, int P, int D>
+static int launch_update(const void* chi_in, void* chi_out, const void* biases, const int32_t* nbr,
+                         const int32_t* in_row, const int32_t* out_row, int64_t n, int attr_plus, double w_plus,
+                         double w_minus, double damp, hipStream_t st) {
+    using C = Cfg<S, T, P, D>;
+    if constexpr (C::NS > 128 || C::LDS > 160 * 1024) {
+        return MJX_ERANGE;
+    } else {
+        const int64_t tiles = (n + C::NT - 1) / C::NT;
+        if (tiles > INT32_MAX) return MJX_ERANGE;
+        auto kern = k_hpr_update<S, T, P, D>;
+        static bool attr_set = false;   // per instantiation: opt in to > 64 KiB dynamic LDS once
+        if (!attr_set) {
+            MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS),
+                    "hpr set lds");
+            attr_set = true;
+        }
+        kern<<<(unsigned)tiles, 64 * C::NW, C::LDS, st>>>((const S*)chi_in, (S*)chi_out, (const S*)biases, nbr,
+                                                          in_row, out_row, n, attr_plus, (S)w_plus, (S)w_minus,
+                                                          (S)damp);
+        MJX_LAUNCH_CHECK("k_hpr_update");
+        return MJX_OK;
+    }
+}
+
+template <typename S, int T, int P>
+static int dispatch_d(int d, const void* ci, void* co, const void* b, const int32_t* nb, const int32_t* ir,
+                      const int32_t* orr, int64_t n, int ap, double wp, double wm, double dp, hipStream_t st) {
+    switch (d) {
+        case 2: return launch_update<S, T, P, 2>(ci, co, b, nb, ir, orr, n, ap, wp, wm, dp, st);
+        case 3: return launch_update<S, T, P, 3>(ci, co, b, nb, ir, orr, n, ap, wp, wm, dp, st);
+        case 4: return launch_update<S, T, P, 4>(ci, co, b, nb, ir, orr, n, ap, wp, wm, dp, st);
+        case 5: return launch_update<S, T, P, 5>(ci, co, b, nb, ir, orr, n, ap, wp, wm, dp, st);
+        case 6: return launch_update<S, T, P, 6>(ci, co, b, nb, ir, orr, n, ap, wp, wm, dp, st);
+        default: return MJX_ERANGE;
+    }
+}
+
+template <typename S>
+static int dispatch_tp(int p, int c, int d, const void* ci, void* co, const void* b, const int32_t* nb,
+                       const int32_t* ir, const int32_t* orr, int64_t n, int ap, double wp, double wm, double dp,
+                       hipStream_t st) {
+    const int T = p + c;
+#define MJX_TP(TT, PP) \
+    if (T == TT && p == PP) return dispatch_d<S, TT, PP>(d, ci, co, b, nb, ir, orr, n, ap, wp, wm, dp, st);
+    MJX_TP(2, 1) MJX_TP(3, 1) MJX_TP(3, 2) MJX_TP(4, 1) MJX_TP(4, 2) MJX_TP(4, 3)
+#undef MJX_TP
+    return MJX_ERANGE;
+}
+
+// per-dtype instantiation units (mjx_hpr_f32.hip, mjx_hpr_f64.hip)
+int update_f32(const void* ci, void* co, const void* b, const int32_t* nb, const int32_t* ir, const int32_t* orr,
+               int64_t n, int d, int p, int c, int ap, double wp, double wm, double dp, hipStream_t st);
+int update_f64(const void* ci, void* co, const void* b, const int32_t* nb, const int32_t* ir, const int32_t* orr,
+               int64_t n, int d, int p, int c, int ap, double wp, double wm, double dp, hipStream_t st);
+
+}  // namespace hpr
+}  // namespace mjx

@@ -1,0 +1,248 @@
+"""History-passing reinforcement (HPR) on random regular graphs, backed by HIP
+kernels (code/HPR_pytorch_RRG.py).
+
+Reference-shaped entry points (same names, argument meaning and layouts):
+
+  HPr_dp(chi_mat, biases_i, plan, p, c, attr_value, lmbd_in, damppar)
+                                  code/HPR_pytorch_RRG.py:183-218 (+ new_biases_chi :128-133)
+  marginals_comp(chi_mat, plan, p, c, epsilon=1e-15)
+                                  code/HPR_pytorch_RRG.py:147-167
+  new_biases_i(biases_i, pie, gamma, marginals, t, u=None)
+                                  code/HPR_pytorch_RRG.py:137-145
+  hpr_run(d, n, p, c, ...)        the experiment loop code/HPR_pytorch_RRG.py:224-377
+
+``chi_mat`` is the reference's (2E, 4^(p+c)) message matrix in its own row and
+column order (row r < E: G.edges[r] = (u, v) as u->v, row r+E: v->u); it is
+kept on the device.  ``plan`` (``HPRPlan``) replaces the reference's auxiliary
+index arrays (edge_dict, N_edg_pos_chi_mat, N_edges_pos, N_nodes, pos_biases,
+pairs, pji): they are all functions of the edge list and neighbour order.
+
+Precision: ``dtype=torch.float32`` is the fast path (north star: fp32 edge
+messages, 1e-5 row-normalised tolerance per step); ``torch.float64`` runs the
+same kernels in the reference's default dtype (code/HPR_pytorch_RRG.py:11).
+"""
+import math
+
+import numpy as np
+import torch
+
+from . import _device, _lib
+from .dynamics import pack, rollout
+from .graph import Graph
+
+_DT = {torch.float32: _lib.MJX_F32, torch.float64: _lib.MJX_F64}
+
+
+def _code(dtype):
+    try:
+        return _DT[dtype]
+    except KeyError:
+        raise _lib.MjxError(f"HPR messages must be float32 or float64, got {dtype}") from None
+
+
+class HPRPlan:
+    """Device-resident index plan of a d-regular graph for the HPR kernels.
+
+    edges: (E, 2) list(G.edges) — fixes the message row order.
+    nbrs:  (n, d) neighbours of each node in G.neighbors order (the reference's
+           N_nodes, code/HPR_pytorch_RRG.py:110-118); optional, any order gives
+           the same messages up to floating-point summation order.
+    """
+
+    def __init__(self, edges, n, d, nbrs=None):
+        e = np.asarray(edges, dtype=np.int64).reshape(-1, 2)
+        n, d = int(n), int(d)
+        E = e.shape[0]
+        if 2 * E != n * d:
+            raise ValueError(f"{E} edges is not a {d}-regular graph on {n} nodes")
+        u, v = e[:, 0], e[:, 1]
+        if nbrs is None:
+            src = np.concatenate([u, v])
+            dst = np.concatenate([v, u])
+            order = np.lexsort((dst, src))
+            nbrs = dst[order].reshape(n, d)
+            if not np.array_equal(src[order], np.repeat(np.arange(n), d)):
+                raise ValueError("graph is not d-regular")
+        nbrs = np.asarray(nbrs, dtype=np.int64).reshape(n, d)
+        # row of the directed message x -> y: r for (u_r, v_r), r + E for (v_r, u_r)
+        keys = np.concatenate([u * n + v, v * n + u])
+        rows = np.concatenate([np.arange(E), np.arange(E) + E])
+        srt = np.argsort(keys, kind="stable")
+        keys, rows = keys[srt], rows[srt]
+
+        def row_of(x, y):
+            k = x * n + y
+            pos = np.searchsorted(keys, k)
+            if np.any(pos >= keys.size) or np.any(keys[np.minimum(pos, keys.size - 1)] != k):
+                raise ValueError("neighbour array inconsistent with the edge list")
+            return rows[pos]
+
+        a = np.repeat(np.arange(n, dtype=np.int64), d)
+        k = nbrs.reshape(-1)
+        self.n, self.d, self.E = n, d, E
+        self.edges = e
+        self.nbrs_host = nbrs
+        self.out_row_host = row_of(a, k).reshape(n, d)      # N_edges_pos (:110-118)
+        self.in_row_host = row_of(k, a).reshape(n, d)
+        dev = _device.require_gpu()
+        self.nbr = torch.from_numpy(nbrs.astype(np.int32).reshape(-1)).to(dev)
+        self.in_row = torch.from_numpy(self.in_row_host.astype(np.int32).reshape(-1)).to(dev)
+        self.out_row = torch.from_numpy(self.out_row_host.astype(np.int32).reshape(-1)).to(dev)
+        self._graph = None
+
+    @classmethod
+    def from_networkx(cls, G):
+        n = G.number_of_nodes()
+        d = max(deg for _, deg in G.degree())
+        nbrs = np.array([list(G.neighbors(i)) for i in range(n)], dtype=np.int64)
+        return cls(np.array(list(G.edges), dtype=np.int64), n, d, nbrs)
+
+    @property
+    def graph(self):
+        """ELL graph for the majority-dynamics check (the reference's N_nodes)."""
+        if self._graph is None:
+            self._graph = Graph.ell(self.nbr.view(self.n, self.d))
+        return self._graph
+
+    def num_combs(self, p, c):
+        return 4 ** (int(p) + int(c))
+
+
+def _weights(lmbd_in, n):
+    # torch.exp(-lmbd_in*xi[0]/n) with xi[0] = +1 / -1 (code/HPR_pytorch_RRG.py:39)
+    return math.exp(-lmbd_in * 1 / n), math.exp(-lmbd_in * -1 / n)
+
+
+def HPr_dp(chi_mat, biases_i, plan, p, c, attr_value, lmbd_in, damppar, out=None):
+    """One HPR message update; returns the new (2E, 4^T) message matrix."""
+    chi = _device.to_device(chi_mat)
+    dt = chi.dtype
+    nc = plan.num_combs(p, c)
+    if chi.shape != (2 * plan.E, nc):
+        raise ValueError(f"chi_mat must be ({2 * plan.E}, {nc}), got {tuple(chi.shape)}")
+    b = _device.to_device(biases_i, dtype=dt)
+    out = torch.empty_like(chi) if out is None else out
+    wp, wm = _weights(lmbd_in, plan.n)
+    _lib.call("mjx_hpr_update", _code(dt), _device.ptr(chi), _device.ptr(out), _device.ptr(b),
+              _device.ptr(plan.nbr), _device.ptr(plan.in_row), _device.ptr(plan.out_row), plan.n, plan.d,
+              int(p), int(c), int(attr_value), wp, wm, float(damppar), _device.stream_handle())
+    return out
+
+
+def marginals_comp(chi_mat, plan, p, c, epsilon=1e-15, zwork=None, out=None):
+    """(n, 2) node marginals, column 0 = spin +1."""
+    chi = _device.to_device(chi_mat)
+    dt = chi.dtype
+    zwork = torch.empty(4 * plan.E, dtype=dt, device=chi.device) if zwork is None else zwork
+    out = torch.empty((plan.n, 2), dtype=dt, device=chi.device) if out is None else out
+    _lib.call("mjx_hpr_marginals", _code(dt), _device.ptr(chi), _device.ptr(plan.out_row), plan.n, plan.d,
+              int(p), int(c), float(epsilon), _device.ptr(zwork), _device.ptr(out), _device.stream_handle())
+    return out
+
+
+def new_biases_i(biases_i, pie, gamma, marginals, t, u=None, generator=None, s_out=None):
+    """Bias refresh (updates ``biases_i`` in place, like the reference) and the
+    new trial configuration s (int32 +-1).  ``u``: the n uniforms the reference
+    draws with torch.rand(n) on the CPU generator; drawn that way if None."""
+    b = biases_i
+    if not (isinstance(b, torch.Tensor) and b.is_cuda):
+        raise _lib.MjxError("biases_i must be a device tensor (it is updated in place)")
+    n = b.shape[0]
+    if u is None:
+        u = torch.rand(n, dtype=torch.float64, generator=generator)
+    u = _device.to_device(u, dtype=torch.float64)
+    s = torch.empty(n, dtype=torch.int32, device=b.device) if s_out is None else s_out
+    thresh = 1 - (1 + t) ** (-gamma)                       # code/HPR_pytorch_RRG.py:142
+    _lib.call("mjx_hpr_new_biases", _code(b.dtype), _device.ptr(b), _device.ptr(marginals), _device.ptr(u),
+              float(thresh), float(pie), n, _device.ptr(s), _device.stream_handle())
+    return b, s
+
+
+class HPRState:
+    """Device buffers of one HPR run; ``step`` is one iteration of the main loop
+    (code/HPR_pytorch_RRG.py:345-356) and returns sum(s_endstate(s))."""
+
+    def __init__(self, plan, p, c, chi0, biases0, dtype=torch.float32, damppar=0.4, attr_value=1,
+                 lmbd_in=None, pie=0.3, gamma=0.1):
+        self.plan, self.p, self.c = plan, int(p), int(c)
+        self.dtype = dtype
+        self.damppar, self.attr_value = float(damppar), int(attr_value)
+        self.lmbd_in = 25 * plan.n if lmbd_in is None else lmbd_in
+        self.pie, self.gamma = float(pie), float(gamma)
+        self.chi = _device.to_device(chi0, dtype=dtype)
+        self.chi_b = torch.empty_like(self.chi)
+        self.biases = _device.to_device(biases0, dtype=dtype).clone()
+        dev = self.chi.device
+        self.zwork = torch.empty(4 * plan.E, dtype=dtype, device=dev)
+        self.marg = torch.empty((plan.n, 2), dtype=dtype, device=dev)
+        self.s = torch.empty(plan.n, dtype=torch.int32, device=dev)
+        self.cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.t = 0
+
+    def s_from_biases(self):
+        """s = 2*(b0 > b1) - 1 (code/HPR_pytorch_RRG.py:337-338): the bias kernel
+        with no node selected for refresh (threshold below every uniform)."""
+        u = torch.zeros(self.plan.n, dtype=torch.float64, device=self.s.device)
+        _lib.call("mjx_hpr_new_biases", _code(self.dtype), _device.ptr(self.biases), _device.ptr(self.marg),
+                  _device.ptr(u), -1.0, self.pie, self.plan.n, _device.ptr(self.s), _device.stream_handle())
+        return self.s
+
+    def sum_end(self, s=None):
+        """sum(s_endstate(N_nodes, s, p, c)) via the majority rollout kernel."""
+        s = self.s if s is None else s
+        bits = pack(s)
+        self.cnt.zero_()
+        rollout(self.plan.graph, bits, self.p + self.c - 1, counts=self.cnt)
+        return 2 * int(self.cnt.item()) - self.plan.n
+
+    def step(self, u=None, generator=None):
+        HPr_dp(self.chi, self.biases, self.plan, self.p, self.c, self.attr_value, self.lmbd_in, self.damppar,
+               out=self.chi_b)
+        self.chi, self.chi_b = self.chi_b, self.chi
+        marginals_comp(self.chi, self.plan, self.p, self.c, zwork=self.zwork, out=self.marg)
+        new_biases_i(self.biases, self.pie, self.gamma, self.marg, self.t, u=u, generator=generator, s_out=self.s)
+        self.t += 1
+        return self.sum_end()
+
+
+def hpr_run(d, n, p, c, damppar=0.4, attr_value=1, lmbd_in=None, pie=0.3, gamma=0.1, TT=10000, edges=None,
+            nbrs=None, seed=0, dtype=torch.float32, chi0=None, biases0=None, generator=None):
+    """The HPR experiment of code/HPR_pytorch_RRG.py:224-377 for one graph.
+
+    Randomness follows the reference: with ``generator`` a torch CPU generator
+    (default: seeded with ``seed``), chi0 = rand(2E, 4^T) row-normalised,
+    biases0 = rand(n, 2) row-normalised (:329-335) and one rand(n) per
+    iteration (:142), all float64 like the reference's default dtype.
+    Returns the np.savez keys of :377 (mag_reached, conf, num_steps, graphs).
+    """
+    from .graph import random_regular_edges
+    if edges is None:
+        edges = random_regular_edges(d, n, seed=seed)
+    plan = HPRPlan(edges, n, d, nbrs)
+    if generator is None:
+        generator = torch.Generator().manual_seed(int(seed))
+    nc = 4 ** (p + c)
+    if chi0 is None:
+        chi0 = torch.rand((2 * plan.E, nc), dtype=torch.float64, generator=generator)
+        chi0 = chi0 / torch.sum(chi0, axis=1, keepdims=True)
+    if biases0 is None:
+        biases0 = torch.rand((n, 2), dtype=torch.float64, generator=generator)
+        biases0 = biases0 / torch.sum(biases0, axis=1, keepdims=True)
+    st = HPRState(plan, p, c, chi0, biases0, dtype=dtype, damppar=damppar, attr_value=attr_value,
+                  lmbd_in=lmbd_in, pie=pie, gamma=gamma)
+    st.s_from_biases()
+    total = st.sum_end()
+    m_final = total / n
+    while m_final < 1:                                     # code/HPR_pytorch_RRG.py:344-356
+        total = st.step(generator=generator)
+        if st.t > TT:
+            m_final = 2
+        else:
+            m_final = total / n
+    s = st.s.cpu().numpy()
+    return {
+        "mag_reached": np.array([np.sum(s) / n]),
+        "num_steps": np.array([float(st.t)]),
+        "conf": s[None, :].astype(np.float64),
+        "graphs": plan.nbrs_host[None, :, :].astype(np.float64),
+    }

@@ -8,7 +8,7 @@ AST-extracted and exec'd with the module globals they read injected
 parameter constants.  Only data (inputs and the reference's outputs) is
 written; no reference source is copied.
 
-Usage:  python tests/golden/make_golden.py [dyn] [er] [sa] [sa_full]
+Usage:  python tests/golden/make_golden.py [dyn] [er] [sa] [sa_full] [hpr] [hpr_full]
 """
 import ast
 import json
@@ -221,9 +221,150 @@ def gen_sa_full():
     np.savez_compressed(os.path.join(OUT, "sa_fullscript.npz"), **out)
 
 
+# ---------------------------------------------------------------------------
+# HPR (code/HPR_pytorch_RRG.py): one HPr_dp step, marginals_comp, new_biases_i,
+# a short chain of full loop iterations, and a whole-script run.
+# ---------------------------------------------------------------------------
+HPR_CASES = [
+    # (name, d, n, p, c, graph seed, torch seed, chain iterations)
+    ("hpr_d4_n64_p1c1", 4, 64, 1, 1, 21, 1, 4),
+    ("hpr_d4_n64_p2c2", 4, 64, 2, 2, 22, 2, 2),
+    ("hpr_d3_n50_p2c1", 3, 50, 2, 1, 23, 3, 3),
+    ("hpr_d4_n40_p1c2", 4, 40, 1, 2, 24, 4, 2),
+    ("hpr_d5_n40_p1c1", 5, 40, 1, 1, 25, 5, 2),
+    ("hpr_d3_n40_p3c1", 3, 40, 3, 1, 26, 6, 2),
+]
+
+
+def hpr_env(G, n, d, p, c):
+    """Globals the reference's HPR functions read (code/HPR_pytorch_RRG.py:224-304)."""
+    import itertools
+    import torch
+    T = p + c
+    num_edg = int(n * d / 2)
+    num_combs = 2 ** (2 * (p + c))
+    x = torch.tensor([1, 0], dtype=torch.int)
+    xi_comb = torch.cartesian_prod(*x.repeat(T, 1))
+    edge_dict = {}
+    N_nodes_order = np.zeros(2 * num_edg)
+    for idx, edge in enumerate(G.edges):
+        edge_dict[edge] = idx * num_combs
+        edge_dict[edge[::-1]] = (idx + num_edg) * num_combs
+        N_nodes_order[idx] = edge[0]
+        N_nodes_order[idx + num_edg] = edge[1]
+    env = dict(n=n, d=d, T=T, num_edg=num_edg, num_combs=num_combs, xi_comb=xi_comb,
+               device=torch.device("cpu"), edge_dict=edge_dict)
+    ref = load_ref(HPR_PATH, **env)
+    xi_comb_cpu = np.array(list(itertools.product([1, -1], repeat=p + c)))
+    pairs = np.zeros(num_combs)
+    pji = np.zeros(num_combs)
+    pls = mns = 0
+    for idx, xixj in enumerate(itertools.product(xi_comb_cpu, repeat=2)):
+        pairs[idx] = ref["order"](xixj[1], xixj[0], p, c)
+        if xixj[1][0] == 1:
+            pji[pls] = idx
+            pls += 1
+        else:
+            pji[mns + int(num_combs / 2)] = idx
+            mns += 1
+    N_edg_pos_chi_mat = ref["neib_edg_pos_chi_mat"](G)
+    N_edges_pos, N_nodes = ref["neighb_edges_pos_AND_nodes"](G)
+    pos_biases = ref["positions_biases"](N_nodes_order, n, p, c, num_edg)
+    rho = torch.zeros((2 ** T, T)).int()
+    for idx, xi in enumerate(xi_comb):
+        rho[idx] = xi
+    aux = dict(pairs=torch.tensor(pairs).int(), pji=torch.tensor(pji).int(),
+               N_edg_pos_chi_mat=torch.tensor(N_edg_pos_chi_mat).int(), N_edges_pos=torch.tensor(N_edges_pos).int(),
+               N_nodes=torch.tensor(N_nodes).int(), pos_biases=torch.tensor(pos_biases).int(), rho_D11=rho)
+    return ref, env, aux
+
+
+def gen_hpr():
+    import networkx as nx
+    import torch
+    torch.set_default_dtype(torch.float64)     # code/HPR_pytorch_RRG.py:11
+    damppar, attr_value, pie, gamma = 0.4, 1, 0.3, 0.1
+    for (name, d, n, p, c, gseed, tseed, chain) in HPR_CASES:
+        t0 = time.time()
+        lmbd_in = 25 * n
+        random.seed(gseed)
+        G = nx.random_regular_graph(d, n)
+        ref, env, aux = hpr_env(G, n, d, p, c)
+        torch.manual_seed(tseed)
+        chi_mat = ref["mes_init_mat"](env["num_edg"], p, c)
+        chi_col = chi_mat.reshape(-1)
+        biases_i = torch.rand((n, 2))
+        biases_i = biases_i / torch.sum(biases_i, axis=1, keepdims=True)
+        out = {"edges": np.array(list(G.edges), dtype=np.int64), "n": np.array(n), "d": np.array(d),
+               "p": np.array(p), "c": np.array(c), "damppar": np.array(damppar), "attr_value": np.array(attr_value),
+               "lmbd_in": np.array(lmbd_in), "pie": np.array(pie), "gamma": np.array(gamma),
+               "N_nodes": aux["N_nodes"].numpy(), "N_edges_pos": aux["N_edges_pos"].numpy(),
+               "N_edg_pos_chi_mat": aux["N_edg_pos_chi_mat"].numpy(),
+               "chi0": chi_mat.numpy().copy(), "biases0": biases_i.numpy().copy()}
+        for k in range(chain):
+            biases_chi = ref["new_biases_chi"](biases_i, aux["pos_biases"])
+            rho_D1 = aux["rho_D11"].detach().clone()
+            chi_col, chi_mat = ref["HPr_dp"](chi_mat, chi_col, biases_chi, rho_D1, aux["N_edg_pos_chi_mat"], d, p, c,
+                                              attr_value, lmbd_in, damppar)
+            marg = ref["marginals_comp"](chi_mat, aux["pairs"], aux["pji"], aux["N_edges_pos"],
+                                         epsilon=torch.tensor(1e-15))
+            st = torch.get_rng_state()
+            u = torch.rand(n)
+            torch.set_rng_state(st)
+            biases_i, s = ref["new_biases_i"](biases_i, pie, gamma, marg, k)
+            s_end = ref["s_endstate"](aux["N_nodes"], s, p, c)
+            out[f"it{k}_chi"] = chi_mat.numpy().copy()
+            out[f"it{k}_marg"] = marg.numpy().copy()
+            out[f"it{k}_u"] = u.numpy().copy()
+            out[f"it{k}_biases"] = biases_i.numpy().copy()
+            out[f"it{k}_s"] = s.numpy().copy()
+            out[f"it{k}_m_end"] = np.array(float(ref["m"](s_end)))
+        out["chain"] = np.array(chain)
+        np.savez_compressed(os.path.join(OUT, name + ".npz"), **out)
+        print(f"{name}: {chain} iterations ({time.time() - t0:.1f}s)")
+
+
+def gen_hpr_full():
+    """Whole-script runs of code/HPR_pytorch_RRG.py on the CPU (constants
+    substituted, device forced to the CPU, seeds fixed, np.savez redirected)."""
+    import tempfile
+    with open(HPR_PATH) as f:
+        src = f.read()
+    out = {}
+    for (n, d, p, c, TT, gseed, tseed) in ((40, 4, 1, 1, 300, 31, 7), (30, 3, 2, 1, 300, 32, 8)):
+        tmp = tempfile.mktemp(suffix=".npz")
+        s = src
+        for old, new in (("n=10000", f"n={n}"), ("d=4", f"d={d}"), ("p=1", f"p={p}"), ("c=1", f"c={c}"),
+                         ("TT=10000", f"TT={TT}"),
+                         ("device = torch.device('cuda' if torch.cuda.is_available() else 'cpu')",
+                          "device = torch.device('cpu')"),
+                         (".to(device='cuda')", ".to(device=device)"),
+                         ('np.savez("hpr_d4_p1.npz"', f'np.savez("{tmp}"'),
+                         ("for kkk in range(n_rep):", f"random.seed({gseed}); torch.manual_seed({tseed})\nfor kkk in range(n_rep):")):
+            assert old in s, old
+            s = s.replace(old, new, 1)
+        g = {"__name__": "ref_hpr_full"}
+        t0 = time.time()
+        exec(compile(s, HPR_PATH, "exec"), g)
+        z = np.load(tmp)
+        key = f"n{n}_d{d}_p{p}c{c}"
+        for k in z.files:
+            if k != "time":
+                out[f"{key}_{k}"] = z[k]
+        import networkx as nx
+        random.seed(gseed)
+        G = nx.random_regular_graph(d, n)
+        out[f"{key}_edges"] = np.array(list(G.edges), dtype=np.int64)
+        out[f"{key}_params"] = np.array([n, d, p, c, TT, tseed])
+        os.unlink(tmp)
+        print("hpr full script", key, "steps", z["num_steps"], "m", z["mag_reached"], f"({time.time() - t0:.1f}s)")
+    np.savez_compressed(os.path.join(OUT, "hpr_fullscript.npz"), **out)
+
+
 if __name__ == "__main__":
     if not os.path.isdir(REF):
         sys.exit(f"reference not found at {REF}: fixtures can only be generated in the build container")
     what = sys.argv[1:] or ["dyn", "er", "sa", "sa_full"]
     for w in what:
-        {"dyn": gen_dyn, "er": gen_er, "sa": gen_sa, "sa_full": gen_sa_full}[w]()
+        {"dyn": gen_dyn, "er": gen_er, "sa": gen_sa, "sa_full": gen_sa_full, "hpr": gen_hpr,
+         "hpr_full": gen_hpr_full}[w]()
