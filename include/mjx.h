@@ -137,6 +137,22 @@ int mjx_sa_steps(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R,
                  double par_a, double par_b, double a_cap, double b_cap, int64_t t_cap,
                  void* stream);
 
+/* Light-cone SA: the same proposals, accept decisions and
+ * outputs as mjx_sa_steps, but each proposal is evaluated only inside the ball
+ * of radius p+c-1 around the flipped node, from cached rollout levels.
+ * levels: host array of T = p+c-1 device pointers, levels[t-1] = onestep^t(s)
+ * (n*W words each), kept consistent by the kernel as flips are accepted.
+ * mjx_sa_lightcone_prepare fills them from s (call after mjx_sa_init).
+ * Supported: 1 <= T <= 6, d <= 16 and mjx_sa_lightcone_lds(d,p,c) <= 150 KiB
+ * (bytes of LDS per 64 replicas; -1 if unsupported). */
+int64_t mjx_sa_lightcone_lds(int d, int p, int c);
+int mjx_sa_lightcone_prepare(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R,
+                             const uint64_t* s, uint64_t* const* levels, void* stream);
+int mjx_sa_lightcone_steps(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R,
+                           uint64_t* s, uint64_t* const* levels, mjx_sa_state* st, int64_t nsteps,
+                           double par_a, double par_b, double a_cap, double b_cap, int64_t t_cap,
+                           void* stream);
+
 /* ---- history-passing reinforcement on d-regular graphs ------------------ */
 /*
  * Message arrays use the reference's layout (code/HPR_pytorch_RRG.py:277-285, 46-61):

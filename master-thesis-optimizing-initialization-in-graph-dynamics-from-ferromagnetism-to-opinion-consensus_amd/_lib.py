@@ -35,12 +35,17 @@ SIGNATURES = {
                     c_vp, c_vp, c_vp, c_vp, c_vp],
     "mjx_sa_steps": [c_vp, c_i64, c_int, c_int, c_int, c_i64, c_vp, c_vp, c_vp, c_vp,
                      c_i64, c_dbl, c_dbl, c_dbl, c_dbl, c_i64, c_vp],
+    "mjx_sa_lightcone_lds": [c_int, c_int, c_int],
+    "mjx_sa_lightcone_prepare": [c_vp, c_i64, c_int, c_int, c_int, c_i64, c_vp, c_vp, c_vp],
+    "mjx_sa_lightcone_steps": [c_vp, c_i64, c_int, c_int, c_int, c_i64, c_vp, c_vp, c_vp,
+                               c_i64, c_dbl, c_dbl, c_dbl, c_dbl, c_i64, c_vp],
     "mjx_hpr_update": [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_int,
                        c_dbl, c_dbl, c_dbl, c_vp],
     "mjx_hpr_marginals": [c_int, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_dbl, c_vp, c_vp, c_vp],
     "mjx_hpr_new_biases": [c_int, c_vp, c_vp, c_vp, c_dbl, c_dbl, c_i64, c_vp, c_vp],
 }
-_RESTYPES = {"mjx_strerror": ctypes.c_char_p, "mjx_last_hip_error": ctypes.c_char_p}
+_RESTYPES = {"mjx_strerror": ctypes.c_char_p, "mjx_last_hip_error": ctypes.c_char_p,
+             "mjx_sa_lightcone_lds": c_i64}
 
 MJX_I8, MJX_I32, MJX_I64 = 1, 4, 8
 MJX_F32, MJX_F64 = 104, 108

@@ -78,7 +78,7 @@ constexpr int corner(int XA, int x, int XB, int T, int P, int D) {
     for (int t = 0; t < T; ++t) {
         const int s = cond_s(XA, t, T, P), prev = cond_prev(XA, t, T);
         const int b = bit01(x, t, T), y = spin(XB, t, T);
-        int dg;
+        int dg = 0;
         if (s > 0) {   // sigma > 0, or sigma == 0 and prev == +1
             const int thr = prev > 0 ? 0 : 1;
             int lo = ceil_div2(D - 1 - y + thr) - b;

@@ -265,6 +265,220 @@ __global__ void __launch_bounds__(kBlock) k_sa_accept(int64_t n, int64_t R, int6
     if (st.tr_dE) st.tr_dE[step * R + r] = dE;
 }
 
+
+// ---------------------------------------------------------------------------
+// Light-cone SA.  sum(s_endstate(s with s_i flipped)) -
+// sum(s_endstate(s)) is evaluated exactly from cached levels
+// s_0 = s, s_t = onestep^t(s_0) (t = 1..T, T = p+c-1): a flip at i can change
+// s_t only inside the radius-t ball around i, and only nodes whose level-(t-1)
+// inputs changed need re-evaluation.  Per level the changed nodes are kept in a
+// per-lane list (LDS, [slot][lane]), candidates are the changed nodes of the
+// previous level and their neighbours.  The accept sequence is bit-identical
+// to the full rollout (same integer sum, same float64 delta_H).
+//
+// One wave = the 64 replicas of one replica-packed word column, so no other
+// wave ever touches these words; words are read with agent-scope (L1
+// bypassing) loads because the wave's own accepted flips are atomics.
+// ---------------------------------------------------------------------------
+constexpr int LC_MAXT = 6;
+constexpr int LC_MAXD = 16;
+
+struct LcLevels {
+    u64* s[LC_MAXT + 1];     // s[0] = current configuration, s[t] = onestep^t(s[0])
+    int off[LC_MAXT + 2];    // list slot offset of level t; off[T+1] = candidate list
+};
+
+__device__ __forceinline__ u64 ld_word(const u64* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int D>
+__device__ __forceinline__ int lc_nbrs(const int32_t* __restrict__ adj, int d, int32_t v, int32_t* k) {
+    if constexpr (D > 0) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) k[j] = adj[(int64_t)v * D + j];
+        return D;
+    } else {
+        for (int j = 0; j < d; ++j) k[j] = adj[(int64_t)v * d + j];
+        return d;
+    }
+}
+
+// value (0/1) of node k at level t-1 as seen by the proposal: the list entry
+// if k changed at that level, else the cached word bit
+__device__ __forceinline__ uint32_t lc_val(const uint32_t* prev, int np, int32_t k, const u64* lvl, int64_t W,
+                                           int64_t col, u64 bit) {
+    for (int q = 0; q < np; ++q) {
+        const uint32_t e = prev[q * 64];
+        if ((int32_t)(e & 0x7fffffffu) == k) return e >> 31;
+    }
+    return (ld_word(lvl + (int64_t)k * W + col) & bit) ? 1u : 0u;
+}
+
+__device__ __forceinline__ void lc_add_unique(uint32_t* U, int& nu, int32_t v) {
+    for (int q = 0; q < nu; ++q)
+        if ((int32_t)U[q * 64] == v) return;
+    U[nu * 64] = (uint32_t)v;
+    ++nu;
+}
+
+// Returns sum(s_end(flipped)) - sum(s_end); fills the per-level change lists
+// (cnt[t] entries at lists + off[t]*64) and the old spin of i.
+template <int D>
+__device__ int64_t lc_delta(const int32_t* __restrict__ adj, int d, int64_t W, int64_t col, u64 bit, int T,
+                            const LcLevels& L, uint32_t* lists, int32_t i, int* cnt, int* old_i) {
+    const u64 w0 = ld_word(L.s[0] + (int64_t)i * W + col);
+    *old_i = (w0 & bit) ? 1 : 0;
+    lists[L.off[0] * 64] = (uint32_t)i | ((w0 & bit) ? 0u : 0x80000000u);
+    cnt[0] = 1;
+    int t = 1;
+    for (; t <= T; ++t) {
+        const uint32_t* prev = lists + L.off[t - 1] * 64;
+        uint32_t* U = lists + L.off[T + 1] * 64;
+        uint32_t* cur = lists + L.off[t] * 64;
+        const int np = cnt[t - 1];
+        int nu = 0;
+        for (int q = 0; q < np; ++q) {
+            const int32_t v = (int32_t)(prev[q * 64] & 0x7fffffffu);
+            int32_t k[D > 0 ? D : LC_MAXD];
+            const int dd = lc_nbrs<D>(adj, d, v, k);
+            lc_add_unique(U, nu, v);
+            for (int j = 0; j < dd; ++j) lc_add_unique(U, nu, k[j]);
+        }
+        int nc = 0;
+        for (int q = 0; q < nu; ++q) {
+            const int32_t j = (int32_t)U[q * 64];
+            int32_t k[D > 0 ? D : LC_MAXD];
+            const int dd = lc_nbrs<D>(adj, d, j, k);
+            int ones = 0;
+            for (int m = 0; m < dd; ++m) ones += (int)lc_val(prev, np, k[m], L.s[t - 1], W, col, bit);
+            const uint32_t own = lc_val(prev, np, j, L.s[t - 1], W, col, bit);
+            // always-stay majority (code/SA_RRG.py:19-20)
+            const uint32_t nb = (2 * ones > dd) ? 1u : ((2 * ones < dd) ? 0u : own);
+            const uint32_t ob = (ld_word(L.s[t] + (int64_t)j * W + col) & bit) ? 1u : 0u;
+            if (nb != ob) {
+                cur[nc * 64] = (uint32_t)j | (nb << 31);
+                ++nc;
+            }
+        }
+        cnt[t] = nc;
+        if (nc == 0) break;          // nothing propagates further
+    }
+    for (int u = t + 1; u <= T; ++u) cnt[u] = 0;
+    if (t <= T) return 0;
+    int64_t ds = 0;
+    const uint32_t* last = lists + L.off[T] * 64;
+    for (int q = 0; q < cnt[T]; ++q) ds += (last[q * 64] >> 31) ? 2 : -2;
+    return ds;
+}
+
+template <int D>
+__global__ void __launch_bounds__(64) k_sa_lightcone(const int32_t* __restrict__ adj, int d, int64_t n, int64_t R,
+                                                     int64_t W, LcLevels L, int T, mjx_sa_state st, int64_t nsteps,
+                                                     double par_a, double par_b, double a_cap, double b_cap,
+                                                     int64_t t_cap) {
+    extern __shared__ uint32_t lc_lists[];
+    __shared__ uint32_t twist_buf[MT_N];
+    const int lane = threadIdx.x;
+    const int64_t col = blockIdx.x;
+    const int64_t r = col * 64 + lane;
+    const bool live = r < R;
+    const u64 bit = 1ull << lane;
+    uint32_t* lists = lc_lists + lane;
+    WaveMT g{st.mt, twist_buf, r, live ? st.mt_idx[r] : MT_N, lane};
+    double a = live ? st.a[r] : 0.0, b = live ? st.b[r] : 0.0;
+    int64_t t = live ? st.t[r] : 0, sum_end = live ? st.sum_end[r] : 0;
+    int done = live ? st.done[r] : 1;
+    int ties = 0;
+    const uint64_t rng = (uint64_t)(n - 1);
+    uint32_t mask = (uint32_t)rng;
+    mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+    for (int64_t step = 0; step < nsteps; ++step) {
+        const bool active = live && done == 0;
+        // randint(low=0, high=n) (code/SA_RRG.py:73): numpy legacy masked rejection
+        bool pending = active && rng > 0;
+        uint32_t i = 0;
+        while (__ballot(pending)) {
+            const uint32_t y = g.draw(pending);
+            if (pending) {
+                const uint32_t v = y & mask;
+                if (v <= (uint32_t)rng) { i = v; pending = false; }
+            }
+        }
+        // rand() (code/SA_RRG.py:76)
+        const uint32_t w1 = g.draw(active);
+        const uint32_t w2 = g.draw(active);
+        if (active) {
+            const double u = mt_double(w1, w2);
+            int cnt[LC_MAXT + 1];
+            int old_i;
+            const int64_t ds = lc_delta<D>(adj, d, W, col, bit, T, L, lists, (int32_t)i, cnt, &old_i);
+            const int64_t sum_new = sum_end + ds;
+            // delta_H (code/SA_RRG.py:37), same operation order, no contraction
+            const double si = old_i ? 1.0 : -1.0;
+            const double t1 = (-2.0 * a) * si;
+            const double t2 = b * (double)(sum_end - sum_new);
+            const double dE = (t1 + t2) / (double)n;
+            const double e = exp(-dE);
+            const double prob = (e < 1.0) ? e : 1.0;                 // (code/SA_RRG.py:75)
+            const bool acc = u < prob;                               // (code/SA_RRG.py:76)
+            if (e < 1.0 && fabs(u - e) <= 4.0 * (nextafter(e, 2.0) - e)) ++ties;
+            if (acc) {                                               // (code/SA_RRG.py:77)
+                for (int lv = 0; lv <= T; ++lv) {
+                    const uint32_t* lst = lists + L.off[lv] * 64;
+                    for (int q = 0; q < cnt[lv]; ++q) {
+                        const int64_t j = (int64_t)(lst[q * 64] & 0x7fffffffu);
+                        atomicXor((unsigned long long*)(L.s[lv] + j * W + col), (unsigned long long)bit);
+                    }
+                }
+                sum_end = sum_new;
+            }
+            if (a < a_cap) a = par_a * a;                            // (code/SA_RRG.py:80-81)
+            if (b < b_cap) b = par_b * b;
+            t += 1;                                                  // (code/SA_RRG.py:82)
+            if (t > t_cap) done = 2;                                 // (code/SA_RRG.py:84)
+            else if (sum_end == n) done = 1;                         // m(s_endstate(s)) == 1
+            if (st.tr_i) st.tr_i[step * R + r] = (int32_t)i;
+            if (st.tr_acc) st.tr_acc[step * R + r] = acc ? 1 : 0;
+            if (st.tr_sum) st.tr_sum[step * R + r] = sum_end;
+            if (st.tr_dE) st.tr_dE[step * R + r] = dE;
+        } else if (live) {
+            if (st.tr_i) st.tr_i[step * R + r] = -1;
+            if (st.tr_acc) st.tr_acc[step * R + r] = -1;
+            if (st.tr_sum) st.tr_sum[step * R + r] = sum_end;
+            if (st.tr_dE) st.tr_dE[step * R + r] = 0.0;
+        }
+        // this wave's flips must land before its next reads of the same words
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (live) {
+        st.mt_idx[r] = g.idx;
+        st.a[r] = a;
+        st.b[r] = b;
+        st.t[r] = t;
+        st.sum_end[r] = sum_end;
+        st.done[r] = done;
+        if (st.tr_tie) st.tr_tie[r] += ties;
+    }
+}
+
+// list slots per lane: levels 0..T (ball bounds) + candidate list
+static int lc_slots(int d, int T, int* off) {
+    int64_t total = 0, ball = 1, shell = 1;
+    for (int t = 0; t <= T; ++t) {
+        if (t > 0) {
+            shell = (t == 1) ? d : shell * (d - 1);
+            ball += shell;
+        }
+        off[t] = (int)total;
+        total += ball;
+        if (total > (1 << 20)) return -1;
+    }
+    off[T + 1] = (int)total;
+    total += ball;                    // candidates of the last level
+    return (int)total;
+}
+
 }  // namespace mjx
 
 using namespace mjx;
@@ -314,4 +528,65 @@ extern "C" int mjx_sa_steps(const int32_t* adj, int64_t n, int d, int p, int c, 
         MJX_LAUNCH_CHECK("k_sa_accept");
     }
     return MJX_OK;
+}
+
+
+extern "C" int64_t mjx_sa_lightcone_lds(int d, int p, int c) {
+    const int T = p + c - 1;
+    if (d < 1 || d > LC_MAXD || T < 1 || T > LC_MAXT) return -1;
+    int off[LC_MAXT + 2];
+    const int slots = lc_slots(d, T, off);
+    if (slots < 0) return -1;
+    return (int64_t)slots * 64 * 4;
+}
+
+extern "C" int mjx_sa_lightcone_prepare(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R,
+                                        const uint64_t* s, uint64_t* const* levels, void* stream) {
+    const int T = p + c - 1;
+    if (!adj || !s || !levels || n < 2 || R < 1 || d < 1 || T < 1 || T > LC_MAXT) return MJX_EINVAL;
+    const int64_t W = (R + 63) / 64;
+    const uint64_t* src = s;
+    for (int t = 0; t < T; ++t) {
+        if (!levels[t]) return MJX_EINVAL;
+        int rc = mjx_rollout_ell_rp(adj, n, d, W, src, levels[t], nullptr, 1, nullptr, stream);
+        if (rc) return rc;
+        src = levels[t];
+    }
+    return MJX_OK;
+}
+
+extern "C" int mjx_sa_lightcone_steps(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R, uint64_t* s,
+                                      uint64_t* const* levels, mjx_sa_state* stp, int64_t nsteps, double par_a,
+                                      double par_b, double a_cap, double b_cap, int64_t t_cap, void* stream) {
+    const int T = p + c - 1;
+    if (!stp || !adj || !s || !levels || n < 2 || R < 1 || d < 1 || d > LC_MAXD || nsteps < 0) return MJX_EINVAL;
+    if (T < 1 || T > LC_MAXT) return MJX_ERANGE;
+    if (n > (int64_t)INT32_MAX) return MJX_ERANGE;
+    LcLevels L;
+    const int slots = lc_slots(d, T, L.off);
+    const size_t lds = (size_t)slots * 64 * 4;
+    if (slots < 0 || lds > 150 * 1024) return MJX_ERANGE;
+    L.s[0] = (u64*)s;
+    for (int t = 1; t <= T; ++t) {
+        if (!levels[t - 1]) return MJX_EINVAL;
+        L.s[t] = (u64*)levels[t - 1];
+    }
+    for (int t = T + 1; t <= LC_MAXT; ++t) L.s[t] = nullptr;
+    if (nsteps == 0) return MJX_OK;
+    const int64_t W = (R + 63) / 64;
+    hipStream_t hs = as_stream(stream);
+    const mjx_sa_state st = *stp;
+    auto launch = [&](auto kern) -> int {
+        MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+                "lightcone lds");
+        kern<<<(unsigned)W, 64, lds, hs>>>(adj, d, n, R, W, L, T, st, nsteps, par_a, par_b, a_cap, b_cap, t_cap);
+        MJX_LAUNCH_CHECK("k_sa_lightcone");
+        return MJX_OK;
+    };
+    switch (d) {
+        case 3: return launch(k_sa_lightcone<3>);
+        case 4: return launch(k_sa_lightcone<4>);
+        case 6: return launch(k_sa_lightcone<6>);
+        default: return launch(k_sa_lightcone<0>);
+    }
 }

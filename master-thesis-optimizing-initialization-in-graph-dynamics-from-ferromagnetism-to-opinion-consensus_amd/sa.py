@@ -14,10 +14,17 @@ its N_stat replicas back to back on one global numpy stream and a fresh graph
 each; here each replica owns a seed, which is what makes them independent and
 parallel.)
 
-Per step the device does: draw (i, u) and flip s[i] for every running replica
-(k_sa_propose), roll out the flipped configuration with the fused per-replica
-+1 count (mjx_rollout_ell_rp), then the Metropolis test, annealing schedule
-and consensus check (k_sa_accept), un-flipping rejected proposals.
+Two evaluation modes give bit-identical trajectories:
+
+* ``"lightcone"`` (default where it fits): one persistent kernel runs many
+  steps; each proposal's sum(s_endstate) change is computed only inside the
+  radius-(p+c-1) ball around the flipped node from cached rollout levels
+  (mjx_sa_lightcone_steps) — O(ball) instead of O(N).
+* ``"rollout"``: per step the device draws (i, u) and flips s[i] for every
+  running replica (k_sa_propose), rolls out the flipped configuration with the
+  fused per-replica +1 count (mjx_rollout_ell_rp), then does the Metropolis
+  test, annealing schedule and consensus check (k_sa_accept), un-flipping
+  rejected proposals.
 """
 import numpy as np
 import torch
@@ -39,7 +46,7 @@ def schedule_constants(n):
 class SAReplicas:
     """R bit-packed SA replicas on one random regular graph (device resident)."""
 
-    def __init__(self, N, p, c, seeds, par_a=PAR_A, par_b=PAR_B, a0=None, b0=None):
+    def __init__(self, N, p, c, seeds, par_a=PAR_A, par_b=PAR_B, a0=None, b0=None, mode="auto"):
         self.graph = as_graph(N)
         if self.graph.kind != "ell":
             raise ValueError("SA runs on random regular graphs (ELL adjacency), code/SA_RRG.py:59-61")
@@ -85,6 +92,21 @@ class SAReplicas:
                   _device.ptr(self.seeds), self.a0, self.b0, _device.ptr(self.s), _device.ptr(self.tmp1),
                   _device.ptr(self.tmp2) if T >= 2 else None, _lib.ctypes.byref(self._state),
                   _device.stream_handle())
+        lds = _lib.load().mjx_sa_lightcone_lds(self.graph.d, self.p, self.c)
+        fits = T >= 1 and 0 < lds <= 150 * 1024
+        if mode == "auto":
+            mode = "lightcone" if fits else "rollout"
+        if mode == "lightcone" and not fits:
+            raise ValueError(f"light-cone SA unsupported for d={self.graph.d}, p+c-1={T}")
+        if mode not in ("lightcone", "rollout"):
+            raise ValueError(f"unknown SA mode {mode!r}")
+        self.mode = mode
+        if mode == "lightcone":
+            # levels s_1..s_T = onestep^t(s); the rollout ping-pong buffers are reused
+            self.levels = [self.tmp1, self.tmp2][:T] + [torch.empty_like(self.s) for _ in range(T - 2)]
+            self._lvl = (_lib.ctypes.c_void_p * T)(*[t.data_ptr() for t in self.levels])
+            _lib.call("mjx_sa_lightcone_prepare", _device.ptr(self.graph.adj), n, self.graph.d, self.p, self.c, R,
+                      _device.ptr(self.s), self._lvl, _device.stream_handle())
 
     # -- stepping -----------------------------------------------------------
     def steps(self, k, trace=False):
@@ -107,10 +129,15 @@ class SAReplicas:
         else:
             st.tr_i = st.tr_acc = st.tr_sum = st.tr_dE = None
         T = self.p + self.c - 1
-        _lib.call("mjx_sa_steps", _device.ptr(self.graph.adj), self.n, self.graph.d, self.p, self.c, self.R,
-                  _device.ptr(self.s), _device.ptr(self.tmp1), _device.ptr(self.tmp2) if T >= 2 else None,
-                  _lib.ctypes.byref(st), k, self.par_a, self.par_b, self.a_cap, self.b_cap,
-                  int(self.t_cap), _device.stream_handle())
+        if self.mode == "lightcone":
+            _lib.call("mjx_sa_lightcone_steps", _device.ptr(self.graph.adj), self.n, self.graph.d, self.p, self.c,
+                      self.R, _device.ptr(self.s), self._lvl, _lib.ctypes.byref(st), k, self.par_a, self.par_b,
+                      self.a_cap, self.b_cap, int(self.t_cap), _device.stream_handle())
+        else:
+            _lib.call("mjx_sa_steps", _device.ptr(self.graph.adj), self.n, self.graph.d, self.p, self.c, self.R,
+                      _device.ptr(self.s), _device.ptr(self.tmp1), _device.ptr(self.tmp2) if T >= 2 else None,
+                      _lib.ctypes.byref(st), k, self.par_a, self.par_b, self.a_cap, self.b_cap,
+                      int(self.t_cap), _device.stream_handle())
         st.tr_i = st.tr_acc = st.tr_sum = st.tr_dE = None
         return tr
 

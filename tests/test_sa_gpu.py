@@ -33,13 +33,15 @@ def test_sa_init_draws_reference_s0(mjx_mod):
         assert np.array_equal(conf[r], 2 * rs.binomial(n=1, p=0.5, size=[n]) - 1)
 
 
+@pytest.mark.parametrize("mode", ["lightcone", "rollout"])
 @pytest.mark.parametrize("name", ["sa_d4_n200_p3c1.npz", "sa_d3_n300_p2c1.npz", "sa_d4_n200_p1c1.npz",
                                   "sa_d4_n1000_p2c2.npz"])
-def test_sa_trace_bit_exact(mjx_mod, name):
+def test_sa_trace_bit_exact(mjx_mod, name, mode):
     z = load_golden(name)
     N, p, c = z["N"], int(z["p"]), int(z["c"])
     seeds = [int(s) for s in z["seeds"]]
-    sa = mjx_mod.SAReplicas(N, p, c, seeds)
+    sa = mjx_mod.SAReplicas(N, p, c, seeds, mode=mode)
+    assert sa.mode == mode
     lens = [len(z[f"seed{sd}_i"]) for sd in seeds]
     steps = max(lens)
     done_at = 0
@@ -73,6 +75,24 @@ def test_sa_trace_bit_exact(mjx_mod, name):
     assert int(res["near_ties"].sum()) == 0
 
 
+def test_sa_lightcone_levels_stay_consistent(mjx_mod):
+    """After many accepted flips the cached levels the light-cone kernel keeps
+    up to date must equal fresh rollouts of the current configuration."""
+    n, d, p, c = 2000, 4, 2, 2
+    adj = mjx_mod.random_regular_graph(d, n, seed=9)
+    sa = mjx_mod.SAReplicas(adj, p, c, list(range(130)), mode="lightcone")
+    sa.steps(3000)
+    W = sa.W
+    g = mjx_mod.Graph.ell(adj)
+    cur = sa.s
+    for lvl in sa.levels:
+        cur = mjx_mod.rollout(g, cur, 1, words=W)
+        assert torch.equal(cur, lvl)
+    cnt = torch.zeros(64 * W, dtype=torch.int64, device="cuda")
+    mjx_mod.rollout(g, sa.s, p + c - 1, words=W, counts=cnt)
+    assert torch.equal(2 * cnt[:sa.R] - n, sa.sum_end)
+
+
 def test_sa_run_matches_full_reference_script(mjx_mod):
     full = load_golden("sa_fullscript.npz")
     N = full["n200_d4_p3_graphs"][0]
@@ -83,13 +103,14 @@ def test_sa_run_matches_full_reference_script(mjx_mod):
     assert np.array_equal(res["graphs"][0], N)
 
 
-def test_sa_many_replicas_vs_oracle(mjx_mod):
+@pytest.mark.parametrize("mode", ["lightcone", "rollout"])
+def test_sa_many_replicas_vs_oracle(mjx_mod, mode):
     """R = 200 replicas (ragged: 4 words, 56 padding bits) on a fresh graph,
-    3000 steps, every replica's accept sequence against the oracle."""
+    600 steps, sampled replicas' accept sequences against the oracle."""
     n, d, p, c = 500, 3, 2, 1
     adj = mjx_mod.random_regular_graph(d, n, seed=42)
     seeds = list(range(200))
-    sa = mjx_mod.SAReplicas(adj, p, c, seeds)
+    sa = mjx_mod.SAReplicas(adj, p, c, seeds, mode=mode)
     tr = {k: v.cpu().numpy() for k, v in sa.steps(600, trace=True).items()}
     for r in (0, 1, 63, 64, 127, 199):
         o = orc.sa_loop(adj, p, c, seeds[r], max_steps=600, trace=True)["trace"]
