@@ -48,7 +48,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--sa-steps", type=int, default=20)
+    ap.add_argument("--sa-steps", type=int, default=2000)
+    ap.add_argument("--sa-rollout-steps", type=int, default=10)
     ap.add_argument("--no-sa", action="store_true")
     return ap.parse_args()
 
@@ -97,6 +98,60 @@ def cpu_baseline(adj, T, seconds):
 
 
 # ---------------------------------------------------------------------------
+def _timed(fn, dist, dev):
+    """Run fn between barrier+synchronize brackets; max wall time over ranks."""
+    import torch
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    fn()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if dist:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    return el
+
+
+def bench_sa(args, rank, world, dist, dev):
+    """configs[1]: SA on a d=3 RRG, N=1e6, p=2, c=1, 4096 bit-packed replicas per
+    GPU (code/SA_RRG.py:63-88, bit-exact replay of numpy's seeded stream).
+    Light-cone mode (default) and the full-rollout mode are both timed."""
+    import torch
+    import mjx
+    sa_n, sa_d, sa_p, sa_c, sa_R = 1_000_000, 3, 2, 1, 4096
+    sa_adj = mjx.random_regular_graph(sa_d, sa_n, seed=args.seed + 7 + 1000 * rank)
+    seeds = np.arange(sa_R, dtype=np.int64) + rank * sa_R
+    out = {"config": "configs[1]: d=3 RRG N=1e6 p=2 c=1, 4096 bit-packed SA replicas per GPU "
+                     "(numpy MT19937 replay, bit-exact accept sequences)"}
+    for mode, steps in (("lightcone", args.sa_steps), ("rollout", args.sa_rollout_steps)):
+        if steps <= 0:
+            continue
+        torch.cuda.synchronize()
+        t_init = time.perf_counter()
+        sa = mjx.SAReplicas(sa_adj, sa_p, sa_c, seeds, mode=mode)
+        sa.steps(2)
+        torch.cuda.synchronize()
+        t_init = time.perf_counter() - t_init
+        el = _timed(lambda: sa.steps(steps), dist, dev)
+        props = world * sa_R * steps / el
+        out[mode] = {
+            "proposals_per_s": props,
+            "sweeps_per_s": props / sa_n,
+            "ms_per_step": 1e3 * el / steps,
+            "reference_equivalent_node_updates_per_s": props * 3 * (sa_p + sa_c - 1) * sa_n,
+            "init_s": t_init,
+            "steps": steps,
+        }
+        del sa
+    return out
+
+
 def rocprof_traffic(kernel_prefix="k_sweep_ell_rp"):
     """HBM bytes per launch from a committed rocprofv3 PMC summary, if any
     (profiles/pmc_traffic.json, written by tools/pmc_traffic.py)."""
@@ -188,38 +243,7 @@ def main():
 
     sa_res = None
     if not args.no_sa and args.sa_steps > 0:
-        sa_n, sa_d, sa_p, sa_c, sa_R = 1_000_000, 3, 2, 1, 4096
-        sa_adj = mjx.random_regular_graph(sa_d, sa_n, seed=args.seed + 7 + 1000 * rank)
-        seeds = np.arange(sa_R, dtype=np.int64) + rank * sa_R
-        t_init = time.perf_counter()
-        sa = mjx.SAReplicas(sa_adj, sa_p, sa_c, seeds)
-        sa.steps(2)
-        torch.cuda.synchronize()
-        t_init = time.perf_counter() - t_init
-        if dist:
-            dist.barrier()
-        torch.cuda.synchronize()
-        ts = time.perf_counter()
-        sa.steps(args.sa_steps)
-        torch.cuda.synchronize()
-        if dist:
-            dist.barrier()
-        torch.cuda.synchronize()
-        sa_el = time.perf_counter() - ts
-        if dist:
-            tt = torch.tensor([sa_el], dtype=torch.float64, device=dev)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            sa_el = float(tt.item())
-        props = world * sa_R * args.sa_steps / sa_el
-        sa_res = {
-            "config": "configs[1]: d=3 RRG N=1e6 p=2 c=1, 4096 bit-packed replicas per GPU, full rollout per proposal",
-            "proposals_per_s": props,
-            "sweeps_per_s": props / sa_n,
-            "ms_per_step": 1e3 * sa_el / args.sa_steps,
-            "reference_equivalent_node_updates_per_s": props * 3 * (sa_p + sa_c - 1) * sa_n,
-            "init_s": t_init,
-            "steps": args.sa_steps,
-        }
+        sa_res = bench_sa(args, rank, world, dist, dev)
 
     if rank == 0:
         line = {

@@ -8,7 +8,7 @@ AST-extracted and exec'd with the module globals they read injected
 parameter constants.  Only data (inputs and the reference's outputs) is
 written; no reference source is copied.
 
-Usage:  python tests/golden/make_golden.py [dyn] [er] [sa] [sa_full] [hpr] [hpr_full]
+Usage:  python tests/golden/make_golden.py [dyn] [er] [sa] [sa_full] [hpr] [hpr_full] [bdcm]
 """
 import ast
 import json
@@ -361,10 +361,95 @@ def gen_hpr_full():
     np.savez_compressed(os.path.join(OUT, "hpr_fullscript.npz"), **out)
 
 
+# ---------------------------------------------------------------------------
+# BDCM on Erdos-Renyi graphs (code/ER_BDCM_entropy.ipynb): the notebook's own
+# graph builder, one BDCM_ER sweep with its observables, and the whole
+# lambda procedure (iteration counts parsed from its printed output).
+# ---------------------------------------------------------------------------
+BDCM_CASES = [
+    # (name, n, mean degree, p, c, graph seed, numpy seed, lambdas)
+    ("bdcm_er_n300_deg2_p1c1", 300, 2.0, 1, 1, 41, 1, (0.0, 0.5, 1.0)),
+    ("bdcm_er_n300_deg5_p1c1", 300, 5.0, 1, 1, 42, 2, (0.0, 0.5)),
+    ("bdcm_er_n150_deg3_p2c1", 150, 3.0, 2, 1, 43, 3, (0.0, 0.4)),
+    ("bdcm_er_n120_deg3_p1c2", 120, 3.0, 1, 2, 44, 4, (0.3,)),
+]
+
+
+def gen_bdcm():
+    import contextlib
+    import io
+    import itertools
+    import re
+    attr_value, damppar, eps, epsilon, T_max = 1, 0.1, 1e-6, 0, 1300
+    for (name, n, deg, p, c, gseed, nseed, lambdas) in BDCM_CASES:
+        t0 = time.time()
+        T = p + c
+        nb = load_nb(T=T, p=p, c=c, n=n, attr_value=attr_value, eps=eps, damppar=damppar, epsilon=epsilon)
+        random.seed(gseed)
+        res = nb["GENERAL_ERgraph_and_auxialiaryarrays_generation"](n, deg / (n - 1), p, c, T, attr_value)
+        (avg_deg, n_core, n_iso, num_edg, adj_matrix, degrees_all, degrees_nodes, N_nodes, A, Ai,
+         N_edges_pos_dm1, N_edges_pos_full, N_edges_pos_full_marginals, N_nodes_pos, edges_with_d_positions,
+         nodes_with_d_positions, degrees_edges, edges) = res
+        nb.update(num_edg=num_edg, degrees_all=degrees_all, degrees_nodes=degrees_nodes, A=A, Ai=Ai,
+                  N_edges_pos_dm1=N_edges_pos_dm1, N_edges_pos_full=N_edges_pos_full,
+                  edges_with_d_positions=edges_with_d_positions, nodes_with_d_positions=nodes_with_d_positions,
+                  degrees_edges=degrees_edges, edges=edges, N_G_without_isolated=n_core, number_iso=n_iso)
+        row_ptr = np.zeros(n_core + 1, np.int64)
+        cols = []
+        for i in range(n_core):
+            row_ptr[i + 1] = row_ptr[i] + len(N_nodes[i])
+            cols.extend(N_nodes[i])
+        np.random.seed(nseed)
+        chi = np.random.random([2 * num_edg] + [2] * T + [2] * T)
+        chi = nb["normalize"](chi)
+        flat = lambda x: np.asarray(x).reshape(2 * num_edg, -1).copy()
+        out = {"edges": np.asarray(edges[:num_edg], np.int64), "row_ptr": row_ptr, "col": np.asarray(cols, np.int64),
+               "n": np.array(n), "n_iso": np.array(n_iso), "p": np.array(p), "c": np.array(c),
+               "attr_value": np.array(attr_value), "damppar": np.array(damppar), "eps": np.array(eps),
+               "epsilon": np.array(float(epsilon)), "T_max": np.array(T_max), "lambdas": np.array(lambdas, float),
+               "chi0": flat(chi)}
+        # one sweep at the last lambda: leaf reset exactly as nb:404-417, then BDCM_ER (nb:425)
+        lm = float(lambdas[-1])
+        ch = chi.copy()
+        if degrees_edges[0] == 0:
+            aux = np.zeros_like(ch[edges_with_d_positions[0]])
+            zero_sum = np.zeros(T)
+            for xi in itertools.product([1, 0], repeat=T):
+                if xi[-1] == attr_value:
+                    for xj in itertools.product([1, 0], repeat=T):
+                        aux[tuple([slice(None)] + list(xi) + list(xj))] = nb["A_i_sums"](
+                            2 * np.array(xi) - 1, 2 * np.array(xj) - 1, zero_sum, p, c, attr_value, lm)
+            ch[edges_with_d_positions[0]] = nb["normalize"](aux)
+        out["sweep_lmbd"] = np.array(lm)
+        out["sweep_leaf"] = flat(ch)
+        ch = nb["BDCM_ER"](ch, degrees_edges, edges_with_d_positions, N_edges_pos_dm1, A, p, c, attr_value, lm,
+                           damppar, epsilon)
+        out["sweep_chi"] = flat(ch)
+        out["sweep_zi"] = nb["Zi_ER"](ch, degrees_nodes, nodes_with_d_positions, N_edges_pos_full, Ai, p, c, n_core,
+                                      attr_value, lm)
+        out["sweep_zij"] = nb["Zij"](ch, num_edg, epsilon)
+        out["sweep_phi"] = np.array(nb["phi_BP_GENERAL_ER"](ch, num_edg, degrees_nodes, nodes_with_d_positions,
+                                                            N_edges_pos_full, Ai, n_core, n, p, c, attr_value, lm,
+                                                            epsilon, n_iso))
+        out["sweep_m_init"] = np.array(nb["avg_m_init_GENERAL_ER"](ch, num_edg, degrees_all, edges, n, epsilon, n_iso))
+        # the whole procedure (mutates its chi argument in place: it ends holding the last fixed point)
+        run = chi.copy()
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            m_init, ent1, ent, counts = nb["BDCM_entropy_procedure_GENERAL_ER"](run, np.array(lambdas, float), T_max,
+                                                                               0, 1e9, time.time())
+        iters = [int(x) for x in re.findall(r"t=\s*(\d+)", buf.getvalue())]
+        out.update(m_init=np.asarray(m_init), ent1=np.asarray(ent1), ent=np.asarray(ent), counts=np.array(counts),
+                   iters=np.array(iters, np.int64), chi_final=flat(run))
+        np.savez_compressed(os.path.join(OUT, name + ".npz"), **out)
+        print(f"{name}: n_core={n_core} iso={n_iso} E={num_edg} classes={list(degrees_edges)} iters={iters} "
+              f"m_init={np.round(m_init, 5)} ent1={np.round(ent1, 5)} ({time.time() - t0:.1f}s)")
+
+
 if __name__ == "__main__":
     if not os.path.isdir(REF):
         sys.exit(f"reference not found at {REF}: fixtures can only be generated in the build container")
     what = sys.argv[1:] or ["dyn", "er", "sa", "sa_full"]
     for w in what:
         {"dyn": gen_dyn, "er": gen_er, "sa": gen_sa, "sa_full": gen_sa_full, "hpr": gen_hpr,
-         "hpr_full": gen_hpr_full}[w]()
+         "hpr_full": gen_hpr_full, "bdcm": gen_bdcm}[w]()
