@@ -16,6 +16,8 @@
  *   onestep_majority (ER)        nb:113-117,  s_endstate (ER) nb:120-123
  *   m(s)                         code/SA_RRG.py:39-40, code/HPR_pytorch_RRG.py:179-180, nb:125-126
  *   E_delta + SA loop body       code/SA_RRG.py:32-37, 63-88
+ *   HPr_dp, marginals_comp, new_biases_i   code/HPR_pytorch_RRG.py:137-218
+ *   BDCM_ER, Zi_ER, Zij, phi/m_init sums   nb:133-276, 372-392
  *
  * Spin layouts in HBM (bit = 1 means spin +1, bit = 0 means spin -1):
  *
@@ -184,6 +186,38 @@ int mjx_hpr_marginals(int dtype, const void* chi, const int32_t* out_row, int64_
  * place and writes s[n] = +-1 (int32, nullable). */
 int mjx_hpr_new_biases(int dtype, void* biases, const void* marg, const double* u, double thresh,
                        double pie, int64_t n, int32_t* s, void* stream);
+
+/* ---- BDCM on Erdos-Renyi graphs (code/ER_BDCM_entropy.ipynb), float64 ---- */
+/*
+ * chi[2E][4^T] in the notebook's layout (nb:150-154, 303-314): row r < E is
+ * G.edges[r] = (i, j) as the message i -> j, row r + E is j -> i; column of
+ * (x_i, x_j) = idx(x_i)*2^T + idx(x_j), idx(x) = sum_t [x_t = +1] 2^(T-1-t).
+ * T = p + c <= 4.  An "edge class" is the set of messages a -> b with
+ * deg(a) - 1 = D (nb:312-318): rows[m] are their chi rows, inc[m*D + k] the
+ * rows of the D incoming messages k -> a (the notebook's N_edges_pos_dm1).
+ * mjx_bdcm_lds_bytes(D, p, c) must be <= 160 KiB (else MJX_ERANGE).
+ */
+int64_t mjx_bdcm_lds_bytes(int D, int p, int c);
+/* One class of BDCM_ER (nb:150-196): new rows = damp*normalize(max(chi2, eps))
+ * + (1-damp)*old, written to upd[m*4^T] and then committed into chi (the class
+ * reads chi before any of its own rows change: Jacobi within a class,
+ * Gauss-Seidel across classes when called in ascending D).  damp >= 1 assigns
+ * normalize(chi2): with D = 0 that is the leaf reset of nb:404-417.
+ * delta_bits (nullable): atomic max of |new - old| as IEEE bits (a NaN wins). */
+int mjx_bdcm_update_class(double* chi, const int32_t* rows, const int32_t* inc, int64_t m, int D, int p, int c,
+                          int attr_value, double lmbd, double damp, double eps, double* upd,
+                          unsigned long long* delta_bits, void* stream);
+/* Zi_ER for the m nodes of degree D (nb:211-276): zi[nodes[k]] = max(Zi, eps);
+ * inc[k*D + j] = row of the message from the j-th neighbour into the node. */
+int mjx_bdcm_node_z(const double* chi, const int32_t* nodes, const int32_t* inc, int64_t m, int D, int p, int c,
+                    int attr_value, double lmbd, double eps, double* zi, void* stream);
+/* Zij (nb:200-209) and the per-edge term of avg_m_init (nb:379-392);
+ * edges[2E] = G.edges (u, v) pairs, deg[n] node degrees; m_term nullable. */
+int mjx_bdcm_edge_obs(const double* chi, const int32_t* edges, const int32_t* deg, int64_t E, int p, int c,
+                      int attr_value, double eps, double* zij, double* m_term, void* stream);
+/* out[0] = sum_i x[i] (take_log: sum_i log x[i]), deterministic order;
+ * work: 256 doubles of device scratch. */
+int mjx_sum_f64(const double* x, int64_t n, int take_log, double* work, double* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -12,6 +12,8 @@ from .graph import (Graph, neighbours, csr_from_networkx, random_regular_graph, 
 from .dynamics import onestep_majority, s_endstate, m, pack, unpack, rollout, popcount, as_graph
 from .sa import SAReplicas, E_delta, sa_run, schedule_constants
 from .hpr import HPRPlan, HPRState, HPr_dp, marginals_comp, new_biases_i, hpr_run
+from .bdcm import (BDCMPlan, bdcm_er_plan, BDCM_ER, bdcm_leaf_reset, Zij, Zi_ER, phi_BP_GENERAL_ER,
+                   avg_m_init_GENERAL_ER, BDCM_entropy_procedure_GENERAL_ER, bdcm_er_run)
 
 __all__ = [
     "MjxError", "lib_path", "Graph", "neighbours", "csr_from_networkx", "random_regular_graph",
@@ -19,6 +21,8 @@ __all__ = [
     "onestep_majority", "s_endstate", "m", "pack", "unpack", "rollout", "popcount", "as_graph",
     "SAReplicas", "E_delta", "sa_run", "schedule_constants",
     "HPRPlan", "HPRState", "HPr_dp", "marginals_comp", "new_biases_i", "hpr_run",
+    "BDCMPlan", "bdcm_er_plan", "BDCM_ER", "bdcm_leaf_reset", "Zij", "Zi_ER", "phi_BP_GENERAL_ER",
+    "avg_m_init_GENERAL_ER", "BDCM_entropy_procedure_GENERAL_ER", "bdcm_er_run",
 ]
 
 

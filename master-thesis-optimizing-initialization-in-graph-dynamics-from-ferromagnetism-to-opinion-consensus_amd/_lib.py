@@ -43,9 +43,15 @@ SIGNATURES = {
                        c_dbl, c_dbl, c_dbl, c_vp],
     "mjx_hpr_marginals": [c_int, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_dbl, c_vp, c_vp, c_vp],
     "mjx_hpr_new_biases": [c_int, c_vp, c_vp, c_vp, c_dbl, c_dbl, c_i64, c_vp, c_vp],
+    "mjx_bdcm_lds_bytes": [c_int, c_int, c_int],
+    "mjx_bdcm_update_class": [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_int, c_dbl, c_dbl, c_dbl, c_vp,
+                              c_vp, c_vp],
+    "mjx_bdcm_node_z": [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_int, c_dbl, c_dbl, c_vp, c_vp],
+    "mjx_bdcm_edge_obs": [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_dbl, c_vp, c_vp, c_vp],
+    "mjx_sum_f64": [c_vp, c_i64, c_int, c_vp, c_vp, c_vp],
 }
 _RESTYPES = {"mjx_strerror": ctypes.c_char_p, "mjx_last_hip_error": ctypes.c_char_p,
-             "mjx_sa_lightcone_lds": c_i64}
+             "mjx_sa_lightcone_lds": c_i64, "mjx_bdcm_lds_bytes": c_i64}
 
 MJX_I8, MJX_I32, MJX_I64 = 1, 4, 8
 MJX_F32, MJX_F64 = 104, 108

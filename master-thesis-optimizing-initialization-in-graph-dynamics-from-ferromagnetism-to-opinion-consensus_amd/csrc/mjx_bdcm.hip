@@ -1,0 +1,417 @@
+// Backtracking dynamical cavity method (BDCM) on Erdos-Renyi graphs: the
+// per-degree-class edge-message update, leaf messages, node and edge partition
+// functions and the free-entropy observables of code/ER_BDCM_entropy.ipynb
+// ("nb:L" = raw JSON line L of the notebook).  float64, like the reference.
+//
+// Message layout (the reference's, so chi arrays are drop-in): chi[2E][2^T][2^T],
+// row r < E = list(G.edges)[r] = (i, j) as the message i -> j, row r + E = j -> i
+// (nb:303-314); trajectory index bit (T-1-t) = 1 means spin +1 at time t
+// (the ndarray axes are indexed by itertools.product([1, 0]) values, nb:150-154).
+//
+// BDCM_ER for the message a -> b of edge class D = deg(a) - 1 (nb:312-318):
+//   LL(x_a, rho) = sum over x_k1..x_kD ending in the attractor of prod_m chi^{k_m->a}(x_km, x_a),
+//                  rho_t = number of +1 among x_k1[t]..x_kD[t]                  (nb:150-184)
+//   chi2(x_a, x_b) = exp(-lmbd (2 x_a[0] - 1)) sum_rho A(x_a, x_b, rho) LL(x_a, rho)   (nb:186-191)
+//   chi <- damp * normalize(max(chi2, eps)) + (1 - damp) * chi                  (nb:194-196)
+// A is the majority / always-stay trajectory indicator (nb:66-111).  For a fixed
+// x_a every time step restricts rho_t to a one-sided interval (a lower bound when
+// the spin it must produce is +1, an upper bound when it is -1), so the sum over
+// the box is one entry of the directional cumulative sums of LL: the contraction
+// over (D+1)^T count vectors becomes one lookup per (x_a, x_b).  The node factor
+// of Zi_ER (nb:211-276) is the same box with no receiver term.
+//
+// Kernel geometry: one wave per message (or node).  The DP table of every valid
+// x_a lives in LDS and is convolved in place one neighbour at a time (top-down
+// chunks, read-then-write), then turned into directional cumulative sums.
+#include "mjx_common.h"
+#include <math.h>
+
+#pragma clang fp contract(off)
+
+namespace mjx {
+namespace bdcm {
+
+constexpr int kMaxT = 4;
+constexpr size_t kMaxLds = 160 * 1024;
+
+struct Geo {
+    int T, P, D, X, XV, B, S, ab;     // ab: trajectory index bit of the attractor spin at t = T-1
+    int pw[kMaxT];                    // B^(T-1-t)
+};
+
+__host__ __device__ inline int bspin(int x, int t, int T) { return ((x >> (T - 1 - t)) & 1) ? 1 : -1; }
+__host__ __device__ inline int fdiv2(int a) { return a >= 0 ? a / 2 : -((-a + 1) / 2); }
+__host__ __device__ inline int cdiv2(int a) { return -fdiv2(-a); }
+
+static bool make_geo(int D, int p, int c, int attr_value, Geo* g) {
+    const int T = p + c;
+    if (p < 0 || c < 1 || T > kMaxT || D < 0 || D > 255) return false;
+    if (attr_value != 1 && attr_value != -1) return false;
+    g->T = T;
+    g->P = p;
+    g->D = D;
+    g->X = 1 << T;
+    g->XV = g->X / 2;
+    g->B = D + 1;
+    int64_t S = 1;
+    for (int t = T - 1; t >= 0; --t) {
+        g->pw[t] = (int)S;
+        S *= g->B;
+        if (S > (1 << 22)) return false;
+    }
+    for (int t = T; t < kMaxT; ++t) g->pw[t] = 0;
+    g->S = (int)S;
+    g->ab = attr_value > 0 ? 1 : 0;
+    return true;
+}
+
+static size_t lds_bytes(const Geo& g) {
+    return ((size_t)g.XV * g.S + (size_t)g.D * g.XV * g.XV) * sizeof(double);
+}
+
+// the spin the condition on rho_t must produce, and the spin a tie keeps
+// (traj_condition for t < T-1, atr_condition for t = T-1; nb:66-83)
+__device__ inline int cond_dir(const Geo& g, int xa, int t) {
+    return (t < g.T - 1) ? bspin(xa, t + 1, g.T) : bspin(xa, g.P, g.T);
+}
+__device__ inline int cond_prev(const Geo& g, int xa, int t) {
+    return (t < g.T - 1) ? bspin(xa, t, g.T) : bspin(xa, g.T - 1, g.T);
+}
+
+// table index of the corner of the rho box allowed for (x_a, receiver), -1 when
+// the box is empty.  sigma_t = 2 rho_t - D + y_t with y = spin of x_b (edge
+// factor) or 0 (node factor, A_i_sums2).
+__device__ inline int corner(const Geo& g, int xa, int xb, bool node) {
+    int idx = 0;
+    for (int t = 0; t < g.T; ++t) {
+        const int s = cond_dir(g, xa, t), prev = cond_prev(g, xa, t);
+        const int y = node ? 0 : bspin(xb, t, g.T);
+        int dg;
+        if (s > 0) {            // sigma > 0, or sigma == 0 and prev == +1
+            const int lo = cdiv2(g.D - y + (prev > 0 ? 0 : 1));
+            if (lo > g.D) return -1;
+            dg = lo < 0 ? 0 : lo;
+        } else {                // sigma < 0, or sigma == 0 and prev == -1
+            const int hi = fdiv2(g.D - y + (prev < 0 ? 0 : -1));
+            if (hi < 0) return -1;
+            dg = hi > g.D ? g.D : hi;
+        }
+        idx += dg * g.pw[t];
+    }
+    return idx;
+}
+
+__device__ inline int traj_off(const Geo& g, int x) {
+    int o = 0;
+    for (int t = 0; t < g.T; ++t)
+        if (bspin(x, t, g.T) > 0) o += g.pw[t];
+    return o;
+}
+
+__device__ inline double wave_sum(double v) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// LL of item e for every valid x_a into tab[XV][S], then directional cumulative
+// sums.  inc[e*D + m] = row of the m-th incoming message k_m -> a.
+__device__ void build_table(const Geo& g, const double* __restrict__ chi, const int32_t* __restrict__ inc, int64_t e,
+                            double* tab, double* M, int lane) {
+    const int X = g.X, NC = X * X, XV = g.XV, S = g.S, D = g.D, ab = g.ab, T = g.T;
+    // M[m][a][k] = chi^{k_m -> a}(x_k, x_a), valid x_a = 2a+ab, x_k = 2k+ab
+    for (int q = lane; q < D * XV * XV; q += 64) {
+        const int m = q / (XV * XV), r = q % (XV * XV), a = r / XV, k = r % XV;
+        const int64_t row = inc[e * D + m];
+        M[q] = chi[row * NC + (2 * k + ab) * X + (2 * a + ab)];
+    }
+    for (int q = lane; q < XV * S; q += 64) tab[q] = 0.0;
+    __syncthreads();
+    if (D == 0) {
+        if (lane < XV) tab[lane * S] = 1.0;
+    } else {
+        for (int q = lane; q < XV * XV; q += 64) {
+            const int a = q / XV, k = q % XV;
+            tab[a * S + traj_off(g, 2 * k + ab)] = M[q];
+        }
+    }
+    __syncthreads();
+    const int tot = XV * S;
+    for (int m = 1; m < D; ++m) {
+        const double* Mm = M + m * XV * XV;
+        // in place, top-down: an entry only reads entries at or below itself
+        for (int base = ((tot - 1) / 64) * 64; base >= 0; base -= 64) {
+            const int q = base + lane;
+            double acc = 0.0;
+            if (q < tot) {
+                const int a = q / S, i = q % S;
+                int dg[kMaxT];
+                int rem = i;
+                for (int t = 0; t < T; ++t) {
+                    dg[t] = rem / g.pw[t];
+                    rem -= dg[t] * g.pw[t];
+                }
+                for (int k = XV - 1; k >= 0; --k) {
+                    const int xk = 2 * k + ab;
+                    int src = i;
+                    bool ok = true;
+                    for (int t = 0; t < T; ++t)
+                        if (bspin(xk, t, T) > 0) {
+                            ok = ok && dg[t] > 0;
+                            src -= g.pw[t];
+                        }
+                    if (ok) acc += tab[a * S + src] * Mm[a * XV + k];
+                }
+            }
+            __syncthreads();
+            if (q < tot) tab[q] = acc;
+            __syncthreads();
+        }
+    }
+    // suffix sums along t where the condition needs +1, prefix sums where it needs -1
+    const int lines = XV * (S / g.B);
+    for (int t = 0; t < T; ++t) {
+        const int step = g.pw[t], span = step * g.B;
+        for (int L = lane; L < lines; L += 64) {
+            const int a = L / (S / g.B), r = L % (S / g.B);
+            double* p = tab + a * S + (r / step) * span + (r % step);
+            double run = 0.0;
+            if (cond_dir(g, 2 * a + ab, t) > 0) {
+                for (int j = D; j >= 0; --j) {
+                    run += p[j * step];
+                    p[j * step] = run;
+                }
+            } else {
+                for (int j = 0; j <= D; ++j) {
+                    run += p[j * step];
+                    p[j * step] = run;
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// BDCM_ER for one edge class (nb:150-196), new rows into upd[m][NC].
+// damp >= 1 assigns normalize(chi2) (the leaf reset of nb:404-417 is class D = 0).
+__global__ void __launch_bounds__(64) k_bdcm_edge(const double* __restrict__ chi, const int32_t* __restrict__ rows,
+                                                  const int32_t* __restrict__ inc, Geo g, double w_plus,
+                                                  double w_minus, double eps, double damp, double* __restrict__ upd) {
+    extern __shared__ __align__(16) double sm[];
+    double* tab = sm;
+    double* M = sm + (size_t)g.XV * g.S;
+    const int lane = threadIdx.x;
+    const int64_t e = blockIdx.x;
+    build_table(g, chi, inc, e, tab, M, lane);
+    const int X = g.X, NC = X * X;
+    double v[4];
+    double rs = 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int col = lane + 64 * j;
+        double x = 0.0;
+        if (col < NC) {
+            const int xa = col / X, xb = col % X;
+            if ((xa & 1) == g.ab) {
+                const int cn = corner(g, xa, xb, false);
+                if (cn >= 0) x = (bspin(xa, 0, g.T) > 0 ? w_plus : w_minus) * tab[(xa >> 1) * g.S + cn];
+            }
+            x = (x < eps) ? eps : x;           // np.maximum(chi2, epsilon); a NaN stays NaN
+            rs += x;
+        }
+        v[j] = x;
+    }
+    rs = wave_sum(rs);
+    const int64_t row = rows[e];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int col = lane + 64 * j;
+        if (col < NC) {
+            const double nv = v[j] / rs;       // normalize (nb:128-130), no epsilon
+            upd[e * NC + col] = (damp >= 1.0) ? nv : damp * nv + (1.0 - damp) * chi[row * NC + col];
+        }
+    }
+}
+
+// scatter the class's new rows into chi; max |new - old| as double bits
+__global__ void __launch_bounds__(256) k_bdcm_commit(double* __restrict__ chi, const int32_t* __restrict__ rows,
+                                                     int64_t m, int NC, const double* __restrict__ upd,
+                                                     unsigned long long* __restrict__ delta_bits) {
+    unsigned long long mx = 0;
+    const int64_t total = m * NC;
+    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < total; q += (int64_t)gridDim.x * 256) {
+        const int64_t e = q / NC;
+        const int col = (int)(q % NC);
+        double* p = chi + (int64_t)rows[e] * NC + col;
+        const double nv = upd[q];
+        // |d| >= 0 orders like its bit pattern; a NaN (0x7ff8...) beats every number
+        const unsigned long long b = (unsigned long long)__double_as_longlong(fabs(nv - *p));
+        mx = b > mx ? b : mx;
+        *p = nv;
+    }
+    if (delta_bits) {
+        for (int off = 32; off > 0; off >>= 1) {
+            const unsigned long long o = __shfl_xor(mx, off, 64);
+            mx = o > mx ? o : mx;
+        }
+        if ((threadIdx.x & 63) == 0 && mx) atomicMax(delta_bits, mx);
+    }
+}
+
+// Zi_ER for one node-degree class (nb:211-276): zi[node] = max(sum_xa w Ai LL, eps)
+__global__ void __launch_bounds__(64) k_bdcm_node(const double* __restrict__ chi, const int32_t* __restrict__ nodes,
+                                                  const int32_t* __restrict__ inc, Geo g, double w_plus,
+                                                  double w_minus, double eps, double* __restrict__ zi) {
+    extern __shared__ __align__(16) double sm[];
+    double* tab = sm;
+    double* M = sm + (size_t)g.XV * g.S;
+    const int lane = threadIdx.x;
+    const int64_t e = blockIdx.x;
+    build_table(g, chi, inc, e, tab, M, lane);
+    double z = 0.0;
+    if (lane < g.XV) {
+        const int xa = 2 * lane + g.ab;
+        const int cn = corner(g, xa, 0, true);
+        if (cn >= 0) z = (bspin(xa, 0, g.T) > 0 ? w_plus : w_minus) * tab[lane * g.S + cn];
+    }
+    z = wave_sum(z);
+    if (lane == 0) zi[nodes[e]] = (z < eps) ? eps : z;
+}
+
+// Zij (nb:200-209) and the per-edge m_init term (nb:379-392)
+__global__ void __launch_bounds__(256) k_bdcm_edge_obs(const double* __restrict__ chi, const int32_t* __restrict__ edges,
+                                                       const int32_t* __restrict__ deg, int64_t E, int T, int ab,
+                                                       double eps, double* __restrict__ zij,
+                                                       double* __restrict__ mterm) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= E) return;
+    const int X = 1 << T, NC = X * X, XV = X / 2;
+    const double du = (double)deg[edges[2 * e]], dv = (double)deg[edges[2 * e + 1]];
+    const double* f = chi + e * NC;
+    const double* b = chi + (e + E) * NC;
+    double z = 0.0, mt = 0.0;
+    for (int a = XV - 1; a >= 0; --a) {
+        const int xa = 2 * a + ab;
+        const double sa = (double)bspin(xa, 0, T);
+        for (int c = XV - 1; c >= 0; --c) {
+            const int xb = 2 * c + ab;
+            const double pr = f[xa * X + xb] * b[xb * X + xa];
+            z += pr;
+            mt += (sa / du + (double)bspin(xb, 0, T) / dv) * pr;
+        }
+    }
+    z = (z < eps) ? eps : z;
+    zij[e] = z;
+    if (mterm) mterm[e] = mt / z;
+}
+
+// deterministic two-level sum (of logs): fixed grid, fixed tree
+constexpr int kSumBlocks = 256;
+
+__device__ inline double block_sum256(double s, double* red) {
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    return red[0];
+}
+
+__global__ void __launch_bounds__(256) k_sum_partial(const double* __restrict__ x, int64_t n, int take_log,
+                                                     double* __restrict__ part) {
+    __shared__ double red[256];
+    double s = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+        s += take_log ? log(x[i]) : x[i];
+    const double t = block_sum256(s, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = t;
+}
+
+__global__ void __launch_bounds__(256) k_sum_final(const double* __restrict__ part, int np, double* __restrict__ out) {
+    __shared__ double red[256];
+    double s = 0.0;
+    for (int i = threadIdx.x; i < np; i += 256) s += part[i];
+    const double t = block_sum256(s, red);
+    if (threadIdx.x == 0) out[0] = t;
+}
+
+template <typename K>
+static int set_lds(K kern, size_t lds) {
+    if (lds > 64 * 1024) {
+        MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+                "bdcm set lds");
+    }
+    return MJX_OK;
+}
+
+}  // namespace bdcm
+}  // namespace mjx
+
+using namespace mjx;
+using namespace mjx::bdcm;
+
+extern "C" int64_t mjx_bdcm_lds_bytes(int D, int p, int c) {
+    Geo g;
+    if (!make_geo(D, p, c, 1, &g)) return -1;
+    return (int64_t)lds_bytes(g);
+}
+
+extern "C" int mjx_bdcm_update_class(double* chi, const int32_t* rows, const int32_t* inc, int64_t m, int D, int p,
+                                     int c, int attr_value, double lmbd, double damp, double eps, double* upd,
+                                     unsigned long long* delta_bits, void* stream) {
+    if (m < 0 || !chi) return MJX_EINVAL;
+    if (m == 0) return MJX_OK;
+    if (!rows || !upd || (D > 0 && !inc) || !(damp > 0.0)) return MJX_EINVAL;
+    Geo g;
+    if (!make_geo(D, p, c, attr_value, &g)) return MJX_ERANGE;
+    const size_t lds = lds_bytes(g);
+    if (lds > kMaxLds || m > (int64_t)INT32_MAX) return MJX_ERANGE;
+    hipStream_t st = as_stream(stream);
+    int rc = set_lds(k_bdcm_edge, lds);
+    if (rc) return rc;
+    // exp(-lmbd*(2 x_a[0] - 1)) for x_a[0] = +1 / -1 (nb:191)
+    k_bdcm_edge<<<(unsigned)m, 64, lds, st>>>(chi, rows, inc, g, exp(-lmbd), exp(lmbd), eps, damp, upd);
+    MJX_LAUNCH_CHECK("k_bdcm_edge");
+    const int NC = g.X * g.X;
+    k_bdcm_commit<<<grid_for(m * NC), 256, 0, st>>>(chi, rows, m, NC, upd, delta_bits);
+    MJX_LAUNCH_CHECK("k_bdcm_commit");
+    return MJX_OK;
+}
+
+extern "C" int mjx_bdcm_node_z(const double* chi, const int32_t* nodes, const int32_t* inc, int64_t m, int D, int p,
+                               int c, int attr_value, double lmbd, double eps, double* zi, void* stream) {
+    if (m < 0 || !chi || !zi) return MJX_EINVAL;
+    if (m == 0) return MJX_OK;
+    if (!nodes || (D > 0 && !inc)) return MJX_EINVAL;
+    Geo g;
+    if (!make_geo(D, p, c, attr_value, &g)) return MJX_ERANGE;
+    const size_t lds = lds_bytes(g);
+    if (lds > kMaxLds || m > (int64_t)INT32_MAX) return MJX_ERANGE;
+    hipStream_t st = as_stream(stream);
+    int rc = set_lds(k_bdcm_node, lds);
+    if (rc) return rc;
+    k_bdcm_node<<<(unsigned)m, 64, lds, st>>>(chi, nodes, inc, g, exp(-lmbd), exp(lmbd), eps, zi);
+    MJX_LAUNCH_CHECK("k_bdcm_node");
+    return MJX_OK;
+}
+
+extern "C" int mjx_bdcm_edge_obs(const double* chi, const int32_t* edges, const int32_t* deg, int64_t E, int p, int c,
+                                 int attr_value, double eps, double* zij, double* m_term, void* stream) {
+    if (E < 0 || p < 0 || c < 1 || p + c > kMaxT || (attr_value != 1 && attr_value != -1)) return MJX_EINVAL;
+    if (E == 0) return MJX_OK;
+    if (!chi || !edges || !deg || !zij) return MJX_EINVAL;
+    k_bdcm_edge_obs<<<(unsigned)((E + 255) / 256), 256, 0, as_stream(stream)>>>(
+        chi, edges, deg, E, p + c, attr_value > 0 ? 1 : 0, eps, zij, m_term);
+    MJX_LAUNCH_CHECK("k_bdcm_edge_obs");
+    return MJX_OK;
+}
+
+extern "C" int mjx_sum_f64(const double* x, int64_t n, int take_log, double* work, double* out, void* stream) {
+    if (n < 0 || !work || !out || (n > 0 && !x)) return MJX_EINVAL;
+    hipStream_t st = as_stream(stream);
+    k_sum_partial<<<kSumBlocks, 256, 0, st>>>(x, n, take_log, work);
+    MJX_LAUNCH_CHECK("k_sum_partial");
+    k_sum_final<<<1, 256, 0, st>>>(work, kSumBlocks, out);
+    MJX_LAUNCH_CHECK("k_sum_final");
+    return MJX_OK;
+}
