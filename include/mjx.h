@@ -187,6 +187,35 @@ int mjx_hpr_marginals(int dtype, const void* chi, const int32_t* out_row, int64_
 int mjx_hpr_new_biases(int dtype, void* biases, const void* marg, const double* u, double thresh,
                        double pie, int64_t n, int32_t* s, void* stream);
 
+/* ---- one giant graph partitioned by node range -- */
+/* One synchronous sweep of the rows [row_lo, row_hi) of a node-packed state.
+ * adj holds those rows only: adj[(v - row_lo)*d + k].  s_in / s_out are the
+ * full ceil(n/64)-word states (s_in read anywhere, s_out written only in words
+ * [row_lo/64, ceil(row_hi/64))).  row_lo must be a multiple of 64 and row_hi a
+ * multiple of 64 or n.  counts (nullable): +1 spins among the written nodes,
+ * added.  Replaces onestep_majority (code/SA_RRG.py:18-20) on one rank's rows. */
+int mjx_sweep_ell_np_range(const int32_t* adj, int64_t n, int d, int64_t row_lo, int64_t row_hi,
+                           const uint64_t* s_in, uint64_t* s_out, unsigned long long* counts, void* stream);
+
+/* ---- device graph generation ----------------------- */
+/* Random simple d-regular graph (configuration model through a keyed
+ * pseudorandom stub permutation, then deterministic double-edge switches that
+ * remove self-loops and multi-edges), replacing nx.random_regular_graph
+ * (code/SA_RRG.py:59) with distributional parity.  Writes the ELL rows
+ * [row_lo, row_hi) into adj[(row_hi-row_lo)*d]; every rank that calls it with
+ * the same (n, d, seed) gets rows of the same graph.  work: device scratch of
+ * work_words >= 3 uint64 (defect list; 1 + 2*65536 is ample).  This is a setup
+ * call: it synchronises `stream` to run the repair on the host.  n_switches
+ * (host, nullable) receives the number of switches made.  d <= 16. */
+int mjx_rrg_generate(int64_t n, int d, uint64_t seed, int64_t row_lo, int64_t row_hi, int32_t* adj,
+                     uint64_t* work, int64_t work_words, int64_t* n_switches, void* stream);
+/* Host-only: partner stub of `stub` in the unrepaired pairing (-1 on bad input). */
+int64_t mjx_rrg_partner_host(int64_t n, int d, uint64_t seed, int64_t stub);
+/* Checks a full ELL adjacency: counts[0] += self-loops, counts[1] += entries
+ * repeated in their row, counts[2] += entries whose reverse multiplicity
+ * differs or that are out of range. */
+int mjx_graph_check_ell(const int32_t* adj, int64_t n, int d, unsigned long long* counts, void* stream);
+
 /* ---- BDCM on Erdos-Renyi graphs (code/ER_BDCM_entropy.ipynb), float64 ---- */
 /*
  * chi[2E][4^T] in the notebook's layout (nb:150-154, 303-314): row r < E is

@@ -23,6 +23,7 @@ UNITS = [
     ("mjx_hpr_f32.hip", []),
     ("mjx_hpr_f64.hip", []),
     ("mjx_bdcm.hip", ["-ffp-contract=off"]),
+    ("mjx_graph.hip", []),
 ]
 
 

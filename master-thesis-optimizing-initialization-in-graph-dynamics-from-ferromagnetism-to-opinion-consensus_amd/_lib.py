@@ -15,6 +15,7 @@ c_i64 = ctypes.c_int64
 c_int = ctypes.c_int
 c_dbl = ctypes.c_double
 c_vp = ctypes.c_void_p
+c_u64 = ctypes.c_uint64
 
 # name -> argtypes (restype is c_int unless listed in _RESTYPES)
 SIGNATURES = {
@@ -43,6 +44,10 @@ SIGNATURES = {
                        c_dbl, c_dbl, c_dbl, c_vp],
     "mjx_hpr_marginals": [c_int, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_dbl, c_vp, c_vp, c_vp],
     "mjx_hpr_new_biases": [c_int, c_vp, c_vp, c_vp, c_dbl, c_dbl, c_i64, c_vp, c_vp],
+    "mjx_sweep_ell_np_range": [c_vp, c_i64, c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp],
+    "mjx_rrg_generate": [c_i64, c_int, c_u64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp],
+    "mjx_rrg_partner_host": [c_i64, c_int, c_u64, c_i64],
+    "mjx_graph_check_ell": [c_vp, c_i64, c_int, c_vp, c_vp],
     "mjx_bdcm_lds_bytes": [c_int, c_int, c_int],
     "mjx_bdcm_update_class": [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_int, c_dbl, c_dbl, c_dbl, c_vp,
                               c_vp, c_vp],
@@ -51,7 +56,8 @@ SIGNATURES = {
     "mjx_sum_f64": [c_vp, c_i64, c_int, c_vp, c_vp, c_vp],
 }
 _RESTYPES = {"mjx_strerror": ctypes.c_char_p, "mjx_last_hip_error": ctypes.c_char_p,
-             "mjx_sa_lightcone_lds": c_i64, "mjx_bdcm_lds_bytes": c_i64}
+             "mjx_sa_lightcone_lds": c_i64, "mjx_bdcm_lds_bytes": c_i64,
+             "mjx_rrg_partner_host": c_i64}
 
 MJX_I8, MJX_I32, MJX_I64 = 1, 4, 8
 MJX_F32, MJX_F64 = 104, 108

@@ -131,7 +131,8 @@ struct VertCounter {
 
 // ---------------------------------------------------------------------------
 // node-packed (one replica) ELL sweep: a wave owns 64 consecutive nodes = one
-// output word; each lane gathers its node's d neighbour bits.
+// output word; each lane gathers its node's d neighbour bits.  Rows [v0, v1)
+// are updated (v0 a multiple of 64); adj holds those rows only.
 // ---------------------------------------------------------------------------
 template <int D>
 __device__ __forceinline__ void load_adj(const int32_t* __restrict__ adj, int64_t v, int32_t* k) {
@@ -151,22 +152,34 @@ __device__ __forceinline__ void load_adj(const int32_t* __restrict__ adj, int64_
     }
 }
 
+__device__ __forceinline__ void block_count(unsigned long long ones, unsigned long long* counts) {
+    __shared__ unsigned long long red[kBlock / 64];
+    const int lane = threadIdx.x & 63;
+    if (lane == 0) red[threadIdx.x >> 6] = ones;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long tot = 0;
+        for (int i = 0; i < kBlock / 64; ++i) tot += red[i];
+        if (tot) atomicAdd(counts, tot);
+    }
+}
+
 template <int D>
-__global__ void __launch_bounds__(kBlock) k_sweep_ell_np(const int32_t* __restrict__ adj, int64_t n,
+__global__ void __launch_bounds__(kBlock) k_sweep_ell_np(const int32_t* __restrict__ adj, int64_t v0, int64_t v1,
                                                          const uint32_t* __restrict__ s_in32,
                                                          u64* __restrict__ s_out,
                                                          unsigned long long* __restrict__ counts) {
     const int lane = threadIdx.x & 63;
-    const int64_t nwords = (n + 63) >> 6;
+    const int64_t w0 = v0 >> 6, w1 = (v1 + 63) >> 6;
     const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
     unsigned long long ones = 0;
-    for (int64_t w = wave; w < nwords; w += nwaves) {
+    for (int64_t w = w0 + wave; w < w1; w += nwaves) {
         const int64_t v = (w << 6) + lane;
         bool nb = false;
-        if (v < n) {
+        if (v < v1) {
             int32_t k[D];
-            load_adj<D>(adj, v, k);
+            load_adj<D>(adj, v - v0, k);
             int cnt = 0;
 #pragma unroll
             for (int j = 0; j < D; ++j) cnt += (s_in32[k[j] >> 5] >> (k[j] & 31)) & 1u;
@@ -179,35 +192,26 @@ __global__ void __launch_bounds__(kBlock) k_sweep_ell_np(const int32_t* __restri
             ones += __popcll(word);
         }
     }
-    if (counts) {
-        __shared__ unsigned long long red[kBlock / 64];
-        if (lane == 0) red[threadIdx.x >> 6] = ones;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned long long tot = 0;
-            for (int i = 0; i < kBlock / 64; ++i) tot += red[i];
-            if (tot) atomicAdd(counts, tot);
-        }
-    }
+    if (counts) block_count(ones, counts);
 }
 
 // runtime-degree node-packed ELL sweep (degrees other than the specialised ones)
-__global__ void __launch_bounds__(kBlock) k_sweep_ell_np_dyn(const int32_t* __restrict__ adj, int64_t n, int d,
-                                                             const uint32_t* __restrict__ s_in32,
+__global__ void __launch_bounds__(kBlock) k_sweep_ell_np_dyn(const int32_t* __restrict__ adj, int64_t v0, int64_t v1,
+                                                             int d, const uint32_t* __restrict__ s_in32,
                                                              u64* __restrict__ s_out,
                                                              unsigned long long* __restrict__ counts) {
     const int lane = threadIdx.x & 63;
-    const int64_t nwords = (n + 63) >> 6;
+    const int64_t w0 = v0 >> 6, w1 = (v1 + 63) >> 6;
     const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
     unsigned long long ones = 0;
-    for (int64_t w = wave; w < nwords; w += nwaves) {
+    for (int64_t w = w0 + wave; w < w1; w += nwaves) {
         const int64_t v = (w << 6) + lane;
         bool nb = false;
-        if (v < n) {
+        if (v < v1) {
             int cnt = 0;
             for (int j = 0; j < d; ++j) {
-                int32_t k = adj[v * d + j];
+                int32_t k = adj[(v - v0) * d + j];
                 cnt += (s_in32[k >> 5] >> (k & 31)) & 1u;
             }
             const int own = (s_in32[v >> 5] >> (v & 31)) & 1u;
@@ -219,16 +223,7 @@ __global__ void __launch_bounds__(kBlock) k_sweep_ell_np_dyn(const int32_t* __re
             ones += __popcll(word);
         }
     }
-    if (counts) {
-        __shared__ unsigned long long red[kBlock / 64];
-        if (lane == 0) red[threadIdx.x >> 6] = ones;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned long long tot = 0;
-            for (int i = 0; i < kBlock / 64; ++i) tot += red[i];
-            if (tot) atomicAdd(counts, tot);
-        }
-    }
+    if (counts) block_count(ones, counts);
 }
 
 // node-packed CSR sweep (nb:113-117: sign(2S+s), same as always-stay)
@@ -566,16 +561,16 @@ extern "C" int mjx_unpack_rp(const uint64_t* bits, int64_t n, int64_t R, void* s
 
 // ---- sweep launchers -------------------------------------------------------
 
-static int launch_sweep_ell_np(const int32_t* adj, int64_t n, int d, const u64* in, u64* out,
+static int launch_sweep_ell_np(const int32_t* adj, int64_t v0, int64_t v1, int d, const u64* in, u64* out,
                                unsigned long long* counts, hipStream_t st) {
-    const int64_t nwords = (n + 63) / 64;
+    const int64_t nwords = ((v1 + 63) >> 6) - (v0 >> 6);
     const int grid = grid_for(nwords * 64);
     const uint32_t* in32 = reinterpret_cast<const uint32_t*>(in);
     switch (d) {
-        case 3: k_sweep_ell_np<3><<<grid, kBlock, 0, st>>>(adj, n, in32, out, counts); break;
-        case 4: k_sweep_ell_np<4><<<grid, kBlock, 0, st>>>(adj, n, in32, out, counts); break;
-        case 6: k_sweep_ell_np<6><<<grid, kBlock, 0, st>>>(adj, n, in32, out, counts); break;
-        default: k_sweep_ell_np_dyn<<<grid, kBlock, 0, st>>>(adj, n, d, in32, out, counts); break;
+        case 3: k_sweep_ell_np<3><<<grid, kBlock, 0, st>>>(adj, v0, v1, in32, out, counts); break;
+        case 4: k_sweep_ell_np<4><<<grid, kBlock, 0, st>>>(adj, v0, v1, in32, out, counts); break;
+        case 6: k_sweep_ell_np<6><<<grid, kBlock, 0, st>>>(adj, v0, v1, in32, out, counts); break;
+        default: k_sweep_ell_np_dyn<<<grid, kBlock, 0, st>>>(adj, v0, v1, d, in32, out, counts); break;
     }
     MJX_LAUNCH_CHECK("sweep_ell_np");
     return MJX_OK;
@@ -699,7 +694,7 @@ extern "C" int mjx_rollout_ell_np(const int32_t* adj, int64_t n, int d, const ui
     hipStream_t st = as_stream(stream);
     const size_t bytes = (size_t)((n + 63) / 64) * 8;
     auto sweep = [&](const u64* a, u64* b, unsigned long long* c) {
-        return launch_sweep_ell_np(adj, n, d, a, b, c, st);
+        return launch_sweep_ell_np(adj, 0, n, d, a, b, c, st);
     };
     if (steps < 0) return MJX_EINVAL;
     if (steps == 0) {
@@ -707,6 +702,17 @@ extern "C" int mjx_rollout_ell_np(const int32_t* adj, int64_t n, int d, const ui
         return counts ? mjx_popcount_np(s_out, n, counts, stream) : MJX_OK;
     }
     return run_rollout(steps, (const u64*)s_in, (u64*)s_out, (u64*)tmp, counts, sweep);
+}
+
+extern "C" int mjx_sweep_ell_np_range(const int32_t* adj, int64_t n, int d, int64_t row_lo, int64_t row_hi,
+                                      const uint64_t* s_in, uint64_t* s_out, unsigned long long* counts,
+                                      void* stream) {
+    if (n < 1 || d < 0 || d > 255 || row_lo < 0 || row_hi > n || row_lo > row_hi || (row_lo & 63)) return MJX_EINVAL;
+    if ((row_hi & 63) && row_hi != n) return MJX_EINVAL;
+    if (!s_in || !s_out || (row_hi > row_lo && d > 0 && !adj) || overlaps(s_in, s_out)) return MJX_EINVAL;
+    if (n > (int64_t)INT32_MAX) return MJX_ERANGE;
+    if (row_hi == row_lo) return MJX_OK;
+    return launch_sweep_ell_np(adj, row_lo, row_hi, d, (const u64*)s_in, (u64*)s_out, counts, as_stream(stream));
 }
 
 extern "C" int mjx_rollout_ell_rp(const int32_t* adj, int64_t n, int d, int64_t words, const uint64_t* s_in,
