@@ -8,7 +8,9 @@ through the C ABI in include/mjx.h.  There is no CPU fallback.
 from . import _lib
 from ._lib import MjxError, lib_path
 from .graph import (Graph, neighbours, csr_from_networkx, random_regular_graph, random_regular_edges,
-                    erdos_renyi, erdos_renyi_edges, csr_from_edges, remove_isolated)
+                    erdos_renyi, erdos_renyi_edges, csr_from_edges, remove_isolated,
+                    random_regular_rows_device, random_regular_graph_device, check_ell)
+from .partition import NodeRange, ShardedRRG, pack_host, unpack_host
 from .dynamics import onestep_majority, s_endstate, m, pack, unpack, rollout, popcount, as_graph
 from .sa import SAReplicas, E_delta, sa_run, schedule_constants
 from .hpr import HPRPlan, HPRState, HPr_dp, marginals_comp, new_biases_i, hpr_run

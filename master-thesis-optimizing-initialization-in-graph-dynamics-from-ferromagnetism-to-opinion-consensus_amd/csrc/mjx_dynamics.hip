@@ -707,11 +707,11 @@ extern "C" int mjx_rollout_ell_np(const int32_t* adj, int64_t n, int d, const ui
 extern "C" int mjx_sweep_ell_np_range(const int32_t* adj, int64_t n, int d, int64_t row_lo, int64_t row_hi,
                                       const uint64_t* s_in, uint64_t* s_out, unsigned long long* counts,
                                       void* stream) {
-    if (n < 1 || d < 0 || d > 255 || row_lo < 0 || row_hi > n || row_lo > row_hi || (row_lo & 63)) return MJX_EINVAL;
-    if ((row_hi & 63) && row_hi != n) return MJX_EINVAL;
+    if (n < 1 || d < 0 || d > 255 || row_lo < 0 || row_hi > n || row_lo > row_hi) return MJX_EINVAL;
+    if (row_hi == row_lo) return MJX_OK;                       // a rank without rows
+    if ((row_lo & 63) || ((row_hi & 63) && row_hi != n)) return MJX_EINVAL;
     if (!s_in || !s_out || (row_hi > row_lo && d > 0 && !adj) || overlaps(s_in, s_out)) return MJX_EINVAL;
     if (n > (int64_t)INT32_MAX) return MJX_ERANGE;
-    if (row_hi == row_lo) return MJX_OK;
     return launch_sweep_ell_np(adj, row_lo, row_hi, d, (const u64*)s_in, (u64*)s_out, counts, as_stream(stream));
 }
 

@@ -190,6 +190,49 @@ def erdos_renyi(n, p, seed=None, drop_isolated=False):
 
 
 # ---------------------------------------------------------------------------
+# device generation (libmjx, mjx_rrg_generate)
+# ---------------------------------------------------------------------------
+_RRG_WORK_WORDS = 1 + 2 * 65536
+
+
+def random_regular_rows_device(d, n, seed=0, row_lo=0, row_hi=None):
+    """ELL rows [row_lo, row_hi) of a random simple d-regular graph generated on
+    the device (int32 tensor of shape (row_hi-row_lo, d)).  Every call with the
+    same (d, n, seed) describes the same graph, so ranks of a node-range
+    partition each generate only their own rows."""
+    from . import _lib
+    import ctypes
+    if (n * d) % 2:
+        raise ValueError("n * d must be even")  # networkx raises NetworkXError here
+    if not 0 < d < n:
+        raise ValueError("the 0 < d < n inequality must be satisfied")
+    row_hi = n if row_hi is None else int(row_hi)
+    dev = _device.require_gpu()
+    adj = torch.empty((row_hi - row_lo, d), dtype=torch.int32, device=dev)
+    work = torch.empty(_RRG_WORK_WORDS, dtype=torch.int64, device=dev)
+    nsw = ctypes.c_int64(0)
+    _lib.call("mjx_rrg_generate", int(n), int(d), int(seed) & 0xFFFFFFFFFFFFFFFF, int(row_lo), row_hi,
+              _device.ptr(adj) if adj.numel() else None, _device.ptr(work), work.numel(), ctypes.byref(nsw),
+              _device.stream_handle())
+    return adj
+
+
+def random_regular_graph_device(d, n, seed=0):
+    """Device-resident ELL ``Graph`` of a random simple d-regular graph (for
+    sizes networkx cannot reach, e.g. N = 1e9 at d = 6: 24 GB of int32)."""
+    return Graph.ell(random_regular_rows_device(d, n, seed))
+
+
+def check_ell(graph):
+    """(self-loops, repeated entries, asymmetric entries) of a device ELL graph."""
+    from . import _lib
+    counts = torch.zeros(3, dtype=torch.int64, device=graph.adj.device)
+    _lib.call("mjx_graph_check_ell", _device.ptr(graph.adj), graph.n, graph.d, _device.ptr(counts),
+              _device.stream_handle())
+    return tuple(int(x) for x in counts.cpu())
+
+
+# ---------------------------------------------------------------------------
 # device-resident graph
 # ---------------------------------------------------------------------------
 class Graph:
