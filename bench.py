@@ -51,6 +51,10 @@ def parse():
     ap.add_argument("--sa-steps", type=int, default=2000)
     ap.add_argument("--sa-rollout-steps", type=int, default=10)
     ap.add_argument("--no-sa", action="store_true")
+    ap.add_argument("--giant-n", type=int, default=1_000_000_000)
+    ap.add_argument("--giant-d", type=int, default=6)
+    ap.add_argument("--giant-sweeps", type=int, default=10)
+    ap.add_argument("--no-giant", action="store_true")
     return ap.parse_args()
 
 
@@ -152,6 +156,47 @@ def bench_sa(args, rank, world, dist, dev):
     return out
 
 
+def bench_giant(args, rank, world, dist, dev):
+    """configs[4]: ONE d=6 RRG with N=1e9 nodes, partitioned by node range over
+    the ranks (strong scaling); each rank generates its own rows on its GPU and
+    every sweep ends with an in-place RCCL all-gather of the packed state."""
+    import torch
+    import mjx
+    n, d, K = args.giant_n, args.giant_d, args.giant_sweeps
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    sh = mjx.ShardedRRG(d, n, seed=args.seed + 12345)
+    torch.cuda.synchronize()
+    gen_s = time.perf_counter() - t0
+    gen = torch.Generator(device=dev).manual_seed(args.seed + 99)     # same replicated state on every rank
+    sh.buf[sh.cur].copy_(torch.randint(-2 ** 62, 2 ** 62, sh.buf[sh.cur].shape, dtype=torch.int64, device=dev,
+                                       generator=gen))
+    sh.rollout(2)                                                    # warm-up
+    stream = torch.cuda.current_stream()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+    def run():
+        ev0.record(stream)
+        for _ in range(K):
+            sh.sweep()
+        ev1.record(stream)
+
+    el = _timed(run, dist, dev)
+    ev_ms = ev0.elapsed_time(ev1)
+    per_update_bytes = 4 * d + (d + 2) / 8.0          # SURVEY 8d: 4 d/R + (d+2)/8 at R = 1
+    return {
+        "config": f"configs[4]: one d={d} RRG N={n} partitioned by node range over {world} GPU(s), "
+                  "per-sweep in-place RCCL all-gather of the node-packed state",
+        "scaling": "strong", "ranks": world, "n": n, "d": d, "sweeps": K,
+        "gen_s": gen_s,
+        "ms_per_sweep": 1e3 * el / K,
+        "node_updates_per_s": n * K / el,
+        "algorithmic_GBps": n * K * per_update_bytes / el / 1e9,
+        "stream_ms_per_sweep": ev_ms / K,
+        "rows_per_rank": sh.range.hi - sh.range.lo,
+    }
+
+
 def rocprof_traffic(kernel_prefix="k_sweep_ell_rp"):
     """HBM bytes per launch from a committed rocprofv3 PMC summary, if any
     (profiles/pmc_traffic.json, written by tools/pmc_traffic.py)."""
@@ -245,6 +290,12 @@ def main():
     if not args.no_sa and args.sa_steps > 0:
         sa_res = bench_sa(args, rank, world, dist, dev)
 
+    giant = None
+    if not args.no_giant and args.giant_n > 0:
+        del s0, out, tmp, counts, chk, o2
+        torch.cuda.empty_cache()
+        giant = bench_giant(args, rank, world, dist, dev)
+
     if rank == 0:
         line = {
             "metric": "node-updates/s, d=4 RRG majority rollout (s_endstate + m of bit-packed replicas)",
@@ -278,6 +329,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "sa": sa_res,
+            "giant": giant,
         }
         print(json.dumps(line), flush=True)
     if dist:

@@ -83,6 +83,14 @@ int mjx_rollout_ell_np(const int32_t* adj, int64_t n, int d,
 int mjx_rollout_ell_rp(const int32_t* adj, int64_t n, int d, int64_t words,
                        const uint64_t* s_in, uint64_t* s_out, uint64_t* tmp,
                        int steps, unsigned long long* counts, void* stream);
+/* The replica-packed rollout run slice by slice: slice q of S covers word units
+ * [q*U/S, (q+1)*U/S) of every node (U = words/2 16-byte units, or words if
+ * odd); replicas never interact, so the result is identical for every S.
+ * slices = 0 picks S from the state size (mjx_rollout_ell_rp uses that).
+ * S must divide U (MJX_EINVAL otherwise). */
+int mjx_rollout_ell_rp_sliced(const int32_t* adj, int64_t n, int d, int64_t words,
+                              const uint64_t* s_in, uint64_t* s_out, uint64_t* tmp,
+                              int steps, int slices, unsigned long long* counts, void* stream);
 int mjx_rollout_csr_np(const int64_t* row_ptr, const int32_t* col, int64_t n,
                        const uint64_t* s_in, uint64_t* s_out, uint64_t* tmp,
                        int steps, unsigned long long* counts, void* stream);

@@ -297,26 +297,36 @@ __device__ __forceinline__ void stv(u64* __restrict__ p, const u64* x) {
     }
 }
 
+// A launch covers the units [unit0, unit0 + Us) of every node (a "slice" of
+// the replicas); LDS counters are indexed relative to the slice.
 template <int VW>
 __device__ __forceinline__ void flush_to(VertCounter<VW>& vc, int use_lds, unsigned* lds,
-                                         unsigned long long* counts, int64_t unit) {
-    if (use_lds) vc.flush(lds + unit * VW * 64);
+                                         unsigned long long* counts, int64_t unit, int64_t unit0) {
+    if (use_lds) vc.flush(lds + (unit - unit0) * VW * 64);
     else vc.flush(counts + unit * VW * 64);
+}
+
+template <int VW>
+__device__ __forceinline__ void lds_count_init(unsigned* lds, int64_t Us, bool use_lds) {
+    if (use_lds) {
+        for (int64_t r = threadIdx.x; r < Us * VW * 64; r += kBlock) lds[r] = 0;
+        __syncthreads();
+    }
 }
 
 // Shared epilogue for the fused per-replica counts.
 template <int VW, bool COUNT>
-__device__ __forceinline__ void count_epilogue(VertCounter<VW>& vc, bool active, int64_t unit, int64_t W,
-                                               unsigned* lds, bool use_lds,
+__device__ __forceinline__ void count_epilogue(VertCounter<VW>& vc, bool active, int64_t unit, int64_t unit0,
+                                               int64_t Us, unsigned* lds, bool use_lds,
                                                unsigned long long* __restrict__ counts) {
     if constexpr (COUNT) {
-        const int64_t R = W * 64;
         if (use_lds) {
-            if (active && vc.added) vc.flush(lds + unit * VW * 64);
+            if (active && vc.added) vc.flush(lds + (unit - unit0) * VW * 64);
             __syncthreads();  // every thread of the block reaches this (no early return)
-            for (int64_t r = threadIdx.x; r < R; r += kBlock) {
+            const int64_t r0 = unit0 * VW * 64;
+            for (int64_t r = threadIdx.x; r < Us * VW * 64; r += kBlock) {
                 unsigned x = lds[r];
-                if (x) atomicAdd(&counts[r], (unsigned long long)x);
+                if (x) atomicAdd(&counts[r0 + r], (unsigned long long)x);
             }
         } else {
             if (active && vc.added) vc.flush(counts + unit * VW * 64);
@@ -327,20 +337,17 @@ __device__ __forceinline__ void count_epilogue(VertCounter<VW>& vc, bool active,
 template <int D, int VW, bool COUNT>
 __global__ void __launch_bounds__(kBlock) k_sweep_ell_rp(const int32_t* __restrict__ adj, int64_t n, int64_t W,
                                                          const u64* __restrict__ s_in, u64* __restrict__ s_out,
-                                                         unsigned long long* __restrict__ counts, int use_lds) {
+                                                         unsigned long long* __restrict__ counts, int use_lds,
+                                                         int64_t unit0, int64_t Us) {
     extern __shared__ unsigned lds_cnt[];
-    const int64_t U = W / VW;
     const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    const int64_t slots = ((int64_t)gridDim.x * kBlock) / U;
-    const int64_t unit = t % U, slot = t / U;
+    const int64_t slots = ((int64_t)gridDim.x * kBlock) / Us;
+    const int64_t unit = unit0 + t % Us, slot = t / Us;
     const bool active = slot < slots;
     VertCounter<VW> vc;
     if constexpr (COUNT) {
         vc.reset();
-        if (use_lds) {
-            for (int64_t r = threadIdx.x; r < W * 64; r += kBlock) lds_cnt[r] = 0;
-            __syncthreads();
-        }
+        lds_count_init<VW>(lds_cnt, Us, use_lds);
     }
     if (active) {
         for (int64_t v = slot; v < n; v += slots) {
@@ -360,11 +367,11 @@ __global__ void __launch_bounds__(kBlock) k_sweep_ell_rp(const int32_t* __restri
             stv<VW>(s_out + v * W + unit * VW, out);
             if constexpr (COUNT) {
                 vc.add(out);
-                if (vc.added == (1 << KC) - 1) flush_to<VW>(vc, use_lds, lds_cnt, counts, unit);
+                if (vc.added == (1 << KC) - 1) flush_to<VW>(vc, use_lds, lds_cnt, counts, unit, unit0);
             }
         }
     }
-    count_epilogue<VW, COUNT>(vc, active, unit, W, lds_cnt, use_lds, counts);
+    count_epilogue<VW, COUNT>(vc, active, unit, unit0, Us, lds_cnt, use_lds, counts);
 }
 
 // runtime degree (ELL rows of length d) and CSR rows; KB counter planes
@@ -373,20 +380,17 @@ __global__ void __launch_bounds__(kBlock) k_sweep_gen_rp(const int32_t* __restri
                                                          const int64_t* __restrict__ row_ptr,
                                                          const int32_t* __restrict__ col, int64_t n, int64_t W,
                                                          const u64* __restrict__ s_in, u64* __restrict__ s_out,
-                                                         unsigned long long* __restrict__ counts, int use_lds) {
+                                                         unsigned long long* __restrict__ counts, int use_lds,
+                                                         int64_t unit0, int64_t Us) {
     extern __shared__ unsigned lds_cnt[];
-    const int64_t U = W / VW;
     const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    const int64_t slots = ((int64_t)gridDim.x * kBlock) / U;
-    const int64_t unit = t % U, slot = t / U;
+    const int64_t slots = ((int64_t)gridDim.x * kBlock) / Us;
+    const int64_t unit = unit0 + t % Us, slot = t / Us;
     const bool active = slot < slots;
     VertCounter<VW> vc;
     if constexpr (COUNT) {
         vc.reset();
-        if (use_lds) {
-            for (int64_t r = threadIdx.x; r < W * 64; r += kBlock) lds_cnt[r] = 0;
-            __syncthreads();
-        }
+        lds_count_init<VW>(lds_cnt, Us, use_lds);
     }
     if (active) {
         for (int64_t v = slot; v < n; v += slots) {
@@ -414,11 +418,11 @@ __global__ void __launch_bounds__(kBlock) k_sweep_gen_rp(const int32_t* __restri
             stv<VW>(s_out + v * W + unit * VW, out);
             if constexpr (COUNT) {
                 vc.add(out);
-                if (vc.added == (1 << KC) - 1) flush_to<VW>(vc, use_lds, lds_cnt, counts, unit);
+                if (vc.added == (1 << KC) - 1) flush_to<VW>(vc, use_lds, lds_cnt, counts, unit, unit0);
             }
         }
     }
-    count_epilogue<VW, COUNT>(vc, active, unit, W, lds_cnt, use_lds, counts);
+    count_epilogue<VW, COUNT>(vc, active, unit, unit0, Us, lds_cnt, use_lds, counts);
 }
 
 }  // namespace mjx
@@ -454,19 +458,16 @@ __global__ void __launch_bounds__(kBlock) k_popcount_rp(const u64* __restrict__ 
     const bool active = slot < slots;
     VertCounter<VW> vc;
     vc.reset();
-    if (use_lds) {
-        for (int64_t r = threadIdx.x; r < W * 64; r += kBlock) lds_cnt[r] = 0;
-        __syncthreads();
-    }
+    lds_count_init<VW>(lds_cnt, U, use_lds);
     if (active) {
         for (int64_t v = slot; v < n; v += slots) {
             u64 x[VW];
             ldv<VW>(bits + v * W + unit * VW, x);
             vc.add(x);
-            if (vc.added == (1 << KC) - 1) flush_to<VW>(vc, use_lds, lds_cnt, counts, unit);
+            if (vc.added == (1 << KC) - 1) flush_to<VW>(vc, use_lds, lds_cnt, counts, unit, 0);
         }
     }
-    count_epilogue<VW, true>(vc, active, unit, W, lds_cnt, use_lds, counts);
+    count_epilogue<VW, true>(vc, active, unit, 0, U, lds_cnt, use_lds, counts);
 }
 
 }  // namespace mjx
@@ -587,58 +588,74 @@ static int launch_sweep_csr_np(const int64_t* rp, const int32_t* col, int64_t n,
 
 template <int VW, bool COUNT>
 static void launch_ell_rp_vw(const int32_t* adj, int64_t n, int d, int64_t W, const u64* in, u64* out,
-                             unsigned long long* counts, int grid, size_t lds, int use_lds, hipStream_t st) {
+                             unsigned long long* counts, int grid, size_t lds, int use_lds, int64_t unit0,
+                             int64_t Us, hipStream_t st) {
     switch (d) {
-        case 3: k_sweep_ell_rp<3, VW, COUNT><<<grid, kBlock, lds, st>>>(adj, n, W, in, out, counts, use_lds); break;
-        case 4: k_sweep_ell_rp<4, VW, COUNT><<<grid, kBlock, lds, st>>>(adj, n, W, in, out, counts, use_lds); break;
-        case 6: k_sweep_ell_rp<6, VW, COUNT><<<grid, kBlock, lds, st>>>(adj, n, W, in, out, counts, use_lds); break;
+        case 3: k_sweep_ell_rp<3, VW, COUNT><<<grid, kBlock, lds, st>>>(adj, n, W, in, out, counts, use_lds, unit0, Us); break;
+        case 4: k_sweep_ell_rp<4, VW, COUNT><<<grid, kBlock, lds, st>>>(adj, n, W, in, out, counts, use_lds, unit0, Us); break;
+        case 6: k_sweep_ell_rp<6, VW, COUNT><<<grid, kBlock, lds, st>>>(adj, n, W, in, out, counts, use_lds, unit0, Us); break;
         default:
             k_sweep_gen_rp<VW, COUNT, false><<<grid, kBlock, lds, st>>>(adj, d, nullptr, nullptr, n, W, in, out,
-                                                                       counts, use_lds);
+                                                                       counts, use_lds, unit0, Us);
             break;
     }
 }
 
-static int rp_geometry(int64_t n, int64_t W, int* grid, int* vw, int* use_lds, size_t* lds) {
+// Geometry of one launch over Us units (of VW words) of every node.
+static int rp_geometry(int64_t n, int64_t W, int64_t Us, int* grid, int* vw, int* use_lds, size_t* lds) {
     *vw = (W % 2 == 0) ? 2 : 1;
-    const int64_t U = W / *vw;
-    *grid = grid_for(n * U);
+    *grid = grid_for(n * Us);
     const int64_t threads = (int64_t)(*grid) * kBlock;
-    if (threads / U < 1) return MJX_ERANGE;
-    *use_lds = (W * 64 <= kMaxLdsReplicas) ? 1 : 0;
-    *lds = *use_lds ? (size_t)(W * 64 * sizeof(unsigned)) : 0;
+    if (threads / Us < 1) return MJX_ERANGE;
+    *use_lds = (Us * (*vw) * 64 <= kMaxLdsReplicas) ? 1 : 0;
+    *lds = *use_lds ? (size_t)(Us * (*vw) * 64 * sizeof(unsigned)) : 0;
     return MJX_OK;
 }
 
+// Replica slices of a replica-packed rollout: slice q covers units
+// [q*U/S, (q+1)*U/S).  Replicas never interact, so a rollout can run slice by
+// slice; a slice's state (n * W/S words) is small enough to stay in the 256 MB
+// Infinity Cache between the sweeps that re-read it.
+static int64_t units_of(int64_t W) { return (W % 2 == 0) ? W / 2 : W; }
+
+static int auto_slices(int64_t n, int64_t W) {
+    const int64_t U = units_of(W);
+    const int64_t vwb = (W % 2 == 0) ? 16 : 8;
+    int S = 1;
+    // slice footprint <= 64 MiB and >= 128 B of every node row
+    while (S < U && U % (2 * S) == 0 && n * (U / S) * vwb > (64ll << 20) && (U / (2 * S)) * vwb >= 128) S *= 2;
+    return S;
+}
+
 static int launch_sweep_ell_rp(const int32_t* adj, int64_t n, int d, int64_t W, const u64* in, u64* out,
-                               unsigned long long* counts, hipStream_t st) {
+                               unsigned long long* counts, int64_t unit0, int64_t Us, hipStream_t st) {
     int grid, vw, use_lds; size_t lds;
-    int rc = rp_geometry(n, W, &grid, &vw, &use_lds, &lds);
+    int rc = rp_geometry(n, W, Us, &grid, &vw, &use_lds, &lds);
     if (rc) return rc;
     if (!counts) { lds = 0; use_lds = 0; }
     if (vw == 2) {
-        if (counts) launch_ell_rp_vw<2, true>(adj, n, d, W, in, out, counts, grid, lds, use_lds, st);
-        else launch_ell_rp_vw<2, false>(adj, n, d, W, in, out, counts, grid, lds, use_lds, st);
+        if (counts) launch_ell_rp_vw<2, true>(adj, n, d, W, in, out, counts, grid, lds, use_lds, unit0, Us, st);
+        else launch_ell_rp_vw<2, false>(adj, n, d, W, in, out, counts, grid, lds, use_lds, unit0, Us, st);
     } else {
-        if (counts) launch_ell_rp_vw<1, true>(adj, n, d, W, in, out, counts, grid, lds, use_lds, st);
-        else launch_ell_rp_vw<1, false>(adj, n, d, W, in, out, counts, grid, lds, use_lds, st);
+        if (counts) launch_ell_rp_vw<1, true>(adj, n, d, W, in, out, counts, grid, lds, use_lds, unit0, Us, st);
+        else launch_ell_rp_vw<1, false>(adj, n, d, W, in, out, counts, grid, lds, use_lds, unit0, Us, st);
     }
     MJX_LAUNCH_CHECK("sweep_ell_rp");
     return MJX_OK;
 }
 
 static int launch_sweep_csr_rp(const int64_t* rp, const int32_t* col, int64_t n, int64_t W, const u64* in,
-                               u64* out, unsigned long long* counts, hipStream_t st) {
+                               u64* out, unsigned long long* counts, int64_t unit0, int64_t Us, hipStream_t st) {
     int grid, vw, use_lds; size_t lds;
-    int rc = rp_geometry(n, W, &grid, &vw, &use_lds, &lds);
+    int rc = rp_geometry(n, W, Us, &grid, &vw, &use_lds, &lds);
     if (rc) return rc;
     if (!counts) { lds = 0; use_lds = 0; }
     if (vw == 2) {
-        if (counts) k_sweep_gen_rp<2, true, true><<<grid, kBlock, lds, st>>>(nullptr, 0, rp, col, n, W, in, out, counts, use_lds);
-        else k_sweep_gen_rp<2, false, true><<<grid, kBlock, lds, st>>>(nullptr, 0, rp, col, n, W, in, out, counts, use_lds);
+        if (counts) k_sweep_gen_rp<2, true, true><<<grid, kBlock, lds, st>>>(nullptr, 0, rp, col, n, W, in, out, counts, use_lds, unit0, Us);
+        else k_sweep_gen_rp<2, false, true><<<grid, kBlock, lds, st>>>(nullptr, 0, rp, col, n, W, in, out, counts, use_lds, unit0, Us);
     } else {
-        if (counts) k_sweep_gen_rp<1, true, true><<<grid, kBlock, lds, st>>>(nullptr, 0, rp, col, n, W, in, out, counts, use_lds);
-        else k_sweep_gen_rp<1, false, true><<<grid, kBlock, lds, st>>>(nullptr, 0, rp, col, n, W, in, out, counts, use_lds);
+        if (counts) k_sweep_gen_rp<1, true, true><<<grid, kBlock, lds, st>>>(nullptr, 0, rp, col, n, W, in, out, counts, use_lds, unit0, Us);
+        else k_sweep_gen_rp<1, false, true><<<grid, kBlock, lds, st>>>(nullptr, 0, rp, col, n, W, in, out, counts, use_lds, unit0, Us);
     }
     MJX_LAUNCH_CHECK("sweep_csr_rp");
     return MJX_OK;
@@ -674,7 +691,7 @@ extern "C" int mjx_popcount_rp(const uint64_t* bits, int64_t n, int64_t words, u
     if (n < 0 || words < 1 || !counts || (n > 0 && !bits)) return MJX_EINVAL;
     if (n == 0) return MJX_OK;
     int grid, vw, use_lds; size_t lds;
-    int rc = rp_geometry(n, words, &grid, &vw, &use_lds, &lds);
+    int rc = rp_geometry(n, words, units_of(words), &grid, &vw, &use_lds, &lds);
     if (rc) return rc;
     hipStream_t st = as_stream(stream);
     if (vw == 2) k_popcount_rp<2><<<grid, kBlock, lds, st>>>((const u64*)bits, n, words, counts, use_lds);
@@ -715,10 +732,11 @@ extern "C" int mjx_sweep_ell_np_range(const int32_t* adj, int64_t n, int d, int6
     return launch_sweep_ell_np(adj, row_lo, row_hi, d, (const u64*)s_in, (u64*)s_out, counts, as_stream(stream));
 }
 
-extern "C" int mjx_rollout_ell_rp(const int32_t* adj, int64_t n, int d, int64_t words, const uint64_t* s_in,
-                                  uint64_t* s_out, uint64_t* tmp, int steps, unsigned long long* counts,
-                                  void* stream) {
-    if (n < 0 || d < 0 || d > 255 || words < 1 || (n > 0 && (!s_in || !s_out || (!adj && d > 0)))) return MJX_EINVAL;
+extern "C" int mjx_rollout_ell_rp_sliced(const int32_t* adj, int64_t n, int d, int64_t words, const uint64_t* s_in,
+                                         uint64_t* s_out, uint64_t* tmp, int steps, int slices,
+                                         unsigned long long* counts, void* stream) {
+    if (n < 0 || d < 0 || d > 255 || words < 1 || slices < 0 || (n > 0 && (!s_in || !s_out || (!adj && d > 0))))
+        return MJX_EINVAL;
     if (n > (int64_t)INT32_MAX) return MJX_ERANGE;
     if (overlaps(s_in, s_out) || overlaps(s_in, tmp) || overlaps(s_out, tmp)) return MJX_EINVAL;
     if (n == 0) return MJX_OK;
@@ -729,10 +747,24 @@ extern "C" int mjx_rollout_ell_rp(const int32_t* adj, int64_t n, int d, int64_t 
         MJX_HIP(hipMemcpyAsync(s_out, s_in, bytes, hipMemcpyDeviceToDevice, st), "rollout copy");
         return counts ? mjx_popcount_rp(s_out, n, words, counts, stream) : MJX_OK;
     }
-    auto sweep = [&](const u64* a, u64* b, unsigned long long* c) {
-        return launch_sweep_ell_rp(adj, n, d, words, a, b, c, st);
-    };
-    return run_rollout(steps, (const u64*)s_in, (u64*)s_out, (u64*)tmp, counts, sweep);
+    const int64_t U = units_of(words);
+    const int S = slices ? slices : auto_slices(n, words);
+    if (S < 1 || U % S) return MJX_EINVAL;
+    const int64_t Us = U / S;
+    for (int q = 0; q < S; ++q) {
+        auto sweep = [&](const u64* a, u64* b, unsigned long long* c) {
+            return launch_sweep_ell_rp(adj, n, d, words, a, b, c, q * Us, Us, st);
+        };
+        int rc = run_rollout(steps, (const u64*)s_in, (u64*)s_out, (u64*)tmp, counts, sweep);
+        if (rc) return rc;
+    }
+    return MJX_OK;
+}
+
+extern "C" int mjx_rollout_ell_rp(const int32_t* adj, int64_t n, int d, int64_t words, const uint64_t* s_in,
+                                  uint64_t* s_out, uint64_t* tmp, int steps, unsigned long long* counts,
+                                  void* stream) {
+    return mjx_rollout_ell_rp_sliced(adj, n, d, words, s_in, s_out, tmp, steps, 0, counts, stream);
 }
 
 extern "C" int mjx_rollout_csr_np(const int64_t* row_ptr, const int32_t* col, int64_t n, const uint64_t* s_in,
@@ -769,8 +801,15 @@ extern "C" int mjx_rollout_csr_rp(const int64_t* row_ptr, const int32_t* col, in
         MJX_HIP(hipMemcpyAsync(s_out, s_in, bytes, hipMemcpyDeviceToDevice, st), "rollout copy");
         return counts ? mjx_popcount_rp(s_out, n, words, counts, stream) : MJX_OK;
     }
-    auto sweep = [&](const u64* a, u64* b, unsigned long long* c) {
-        return launch_sweep_csr_rp(row_ptr, col, n, words, a, b, c, st);
-    };
-    return run_rollout(steps, (const u64*)s_in, (u64*)s_out, (u64*)tmp, counts, sweep);
+    const int64_t U = units_of(words);
+    const int S = auto_slices(n, words);
+    const int64_t Us = U / S;
+    for (int q = 0; q < S; ++q) {
+        auto sweep = [&](const u64* a, u64* b, unsigned long long* c) {
+            return launch_sweep_csr_rp(row_ptr, col, n, words, a, b, c, q * Us, Us, st);
+        };
+        int rc = run_rollout(steps, (const u64*)s_in, (u64*)s_out, (u64*)tmp, counts, sweep);
+        if (rc) return rc;
+    }
+    return MJX_OK;
 }

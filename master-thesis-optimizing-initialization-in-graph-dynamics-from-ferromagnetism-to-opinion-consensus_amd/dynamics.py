@@ -54,12 +54,14 @@ def unpack(bits, n, R=None, dtype=torch.int64):
     return s
 
 
-def rollout(graph, bits, steps, words=None, out=None, tmp=None, counts=None):
+def rollout(graph, bits, steps, words=None, out=None, tmp=None, counts=None, slices=None):
     """Apply ``steps`` synchronous majority sweeps to packed spins.
 
     words=None: node-packed single replica; else replica-packed with ``words``
     64-bit words per node.  ``counts`` (uint64 tensor viewed as int64, length
     R or 1) receives, added, the number of +1 spins of the result.
+    ``slices`` (ELL, replica-packed only): run the replicas in that many
+    slices (mjx_rollout_ell_rp_sliced); None = the library's automatic choice.
     """
     st = _device.stream_handle()
     out = torch.empty_like(bits) if out is None else out
@@ -72,8 +74,8 @@ def rollout(graph, bits, steps, words=None, out=None, tmp=None, counts=None):
             _lib.call("mjx_rollout_ell_np", _device.ptr(graph.adj), graph.n, graph.d, _device.ptr(bits),
                       _device.ptr(out), tptr, int(steps), cptr, st)
         else:
-            _lib.call("mjx_rollout_ell_rp", _device.ptr(graph.adj), graph.n, graph.d, int(words),
-                      _device.ptr(bits), _device.ptr(out), tptr, int(steps), cptr, st)
+            _lib.call("mjx_rollout_ell_rp_sliced", _device.ptr(graph.adj), graph.n, graph.d, int(words),
+                      _device.ptr(bits), _device.ptr(out), tptr, int(steps), int(slices or 0), cptr, st)
     else:
         if words is None:
             _lib.call("mjx_rollout_csr_np", _device.ptr(graph.row_ptr), _device.ptr(graph.col), graph.n,
