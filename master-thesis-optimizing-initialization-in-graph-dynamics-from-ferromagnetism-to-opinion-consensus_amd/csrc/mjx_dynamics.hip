@@ -306,16 +306,16 @@ __device__ __forceinline__ void flush_to(VertCounter<VW>& vc, int use_lds, unsig
     else vc.flush(counts + unit * VW * 64);
 }
 
-template <int VW>
+template <int VW, int BS = kBlock>
 __device__ __forceinline__ void lds_count_init(unsigned* lds, int64_t Us, bool use_lds) {
     if (use_lds) {
-        for (int64_t r = threadIdx.x; r < Us * VW * 64; r += kBlock) lds[r] = 0;
+        for (int64_t r = threadIdx.x; r < Us * VW * 64; r += BS) lds[r] = 0;
         __syncthreads();
     }
 }
 
 // Shared epilogue for the fused per-replica counts.
-template <int VW, bool COUNT>
+template <int VW, bool COUNT, int BS = kBlock>
 __device__ __forceinline__ void count_epilogue(VertCounter<VW>& vc, bool active, int64_t unit, int64_t unit0,
                                                int64_t Us, unsigned* lds, bool use_lds,
                                                unsigned long long* __restrict__ counts) {
@@ -324,7 +324,7 @@ __device__ __forceinline__ void count_epilogue(VertCounter<VW>& vc, bool active,
             if (active && vc.added) vc.flush(lds + (unit - unit0) * VW * 64);
             __syncthreads();  // every thread of the block reaches this (no early return)
             const int64_t r0 = unit0 * VW * 64;
-            for (int64_t r = threadIdx.x; r < Us * VW * 64; r += kBlock) {
+            for (int64_t r = threadIdx.x; r < Us * VW * 64; r += BS) {
                 unsigned x = lds[r];
                 if (x) atomicAdd(&counts[r0 + r], (unsigned long long)x);
             }
@@ -334,20 +334,22 @@ __device__ __forceinline__ void count_epilogue(VertCounter<VW>& vc, bool active,
     }
 }
 
-template <int D, int VW, bool COUNT>
-__global__ void __launch_bounds__(kBlock) k_sweep_ell_rp(const int32_t* __restrict__ adj, int64_t n, int64_t W,
-                                                         const u64* __restrict__ s_in, u64* __restrict__ s_out,
-                                                         unsigned long long* __restrict__ counts, int use_lds,
-                                                         int64_t unit0, int64_t Us) {
+// BS: block size; the counting sweep runs 1024-thread blocks so that 4x fewer
+// blocks each add their per-replica counts to global memory once.
+template <int D, int VW, bool COUNT, int BS = kBlock>
+__global__ void __launch_bounds__(BS) k_sweep_ell_rp(const int32_t* __restrict__ adj, int64_t n, int64_t W,
+                                                     const u64* __restrict__ s_in, u64* __restrict__ s_out,
+                                                     unsigned long long* __restrict__ counts, int use_lds,
+                                                     int64_t unit0, int64_t Us) {
     extern __shared__ unsigned lds_cnt[];
-    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    const int64_t slots = ((int64_t)gridDim.x * kBlock) / Us;
+    const int64_t t = (int64_t)blockIdx.x * BS + threadIdx.x;
+    const int64_t slots = ((int64_t)gridDim.x * BS) / Us;
     const int64_t unit = unit0 + t % Us, slot = t / Us;
     const bool active = slot < slots;
     VertCounter<VW> vc;
     if constexpr (COUNT) {
         vc.reset();
-        lds_count_init<VW>(lds_cnt, Us, use_lds);
+        lds_count_init<VW, BS>(lds_cnt, Us, use_lds);
     }
     if (active) {
         for (int64_t v = slot; v < n; v += slots) {
@@ -371,7 +373,7 @@ __global__ void __launch_bounds__(kBlock) k_sweep_ell_rp(const int32_t* __restri
             }
         }
     }
-    count_epilogue<VW, COUNT>(vc, active, unit, unit0, Us, lds_cnt, use_lds, counts);
+    count_epilogue<VW, COUNT, BS>(vc, active, unit, unit0, Us, lds_cnt, use_lds, counts);
 }
 
 // runtime degree (ELL rows of length d) and CSR rows; KB counter planes
@@ -586,14 +588,18 @@ static int launch_sweep_csr_np(const int64_t* rp, const int32_t* col, int64_t n,
     return MJX_OK;
 }
 
+constexpr int kCountBlock = 1024;
+
 template <int VW, bool COUNT>
 static void launch_ell_rp_vw(const int32_t* adj, int64_t n, int d, int64_t W, const u64* in, u64* out,
                              unsigned long long* counts, int grid, size_t lds, int use_lds, int64_t unit0,
                              int64_t Us, hipStream_t st) {
+    constexpr int BS = COUNT ? kCountBlock : kBlock;
+    const int g = COUNT ? (grid + kCountBlock / kBlock - 1) / (kCountBlock / kBlock) : grid;
     switch (d) {
-        case 3: k_sweep_ell_rp<3, VW, COUNT><<<grid, kBlock, lds, st>>>(adj, n, W, in, out, counts, use_lds, unit0, Us); break;
-        case 4: k_sweep_ell_rp<4, VW, COUNT><<<grid, kBlock, lds, st>>>(adj, n, W, in, out, counts, use_lds, unit0, Us); break;
-        case 6: k_sweep_ell_rp<6, VW, COUNT><<<grid, kBlock, lds, st>>>(adj, n, W, in, out, counts, use_lds, unit0, Us); break;
+        case 3: k_sweep_ell_rp<3, VW, COUNT, BS><<<g, BS, lds, st>>>(adj, n, W, in, out, counts, use_lds, unit0, Us); break;
+        case 4: k_sweep_ell_rp<4, VW, COUNT, BS><<<g, BS, lds, st>>>(adj, n, W, in, out, counts, use_lds, unit0, Us); break;
+        case 6: k_sweep_ell_rp<6, VW, COUNT, BS><<<g, BS, lds, st>>>(adj, n, W, in, out, counts, use_lds, unit0, Us); break;
         default:
             k_sweep_gen_rp<VW, COUNT, false><<<grid, kBlock, lds, st>>>(adj, d, nullptr, nullptr, n, W, in, out,
                                                                        counts, use_lds, unit0, Us);
@@ -618,14 +624,11 @@ static int rp_geometry(int64_t n, int64_t W, int64_t Us, int* grid, int* vw, int
 // Infinity Cache between the sweeps that re-read it.
 static int64_t units_of(int64_t W) { return (W % 2 == 0) ? W / 2 : W; }
 
-static int auto_slices(int64_t n, int64_t W) {
-    const int64_t U = units_of(W);
-    const int64_t vwb = (W % 2 == 0) ? 16 : 8;
-    int S = 1;
-    // slice footprint <= 64 MiB and >= 128 B of every node row
-    while (S < U && U % (2 * S) == 0 && n * (U / S) * vwb > (64ll << 20) && (U / (2 * S)) * vwb >= 128) S *= 2;
-    return S;
-}
+// Measured on MI355X (tools/slice_sweep.py, profiles/r01_slice_sweep.log): at
+// N=1e6, R=4096 one slice (512-B rows) runs at 6.2 TB/s, 2 slices at 6.1, 4 at
+// 4.9, 8 at 2.8 -- shorter contiguous gathers cost more than the Infinity Cache
+// returns -- so the automatic choice is a single slice.
+static int auto_slices(int64_t, int64_t) { return 1; }
 
 static int launch_sweep_ell_rp(const int32_t* adj, int64_t n, int d, int64_t W, const u64* in, u64* out,
                                unsigned long long* counts, int64_t unit0, int64_t Us, hipStream_t st) {
