@@ -55,6 +55,11 @@ def parse():
     ap.add_argument("--giant-d", type=int, default=6)
     ap.add_argument("--giant-sweeps", type=int, default=10)
     ap.add_argument("--no-giant", action="store_true")
+    ap.add_argument("--er-n", type=int, default=10_000_000)
+    ap.add_argument("--er-deg", type=float, default=5.0)
+    ap.add_argument("--er-replicas", type=int, default=4096)
+    ap.add_argument("--er-steps", type=int, default=5)
+    ap.add_argument("--no-er", action="store_true")
     return ap.parse_args()
 
 
@@ -154,6 +159,49 @@ def bench_sa(args, rank, world, dist, dev):
         }
         del sa
     return out
+
+
+def bench_er(args, rank, world, dist, dev):
+    """configs[3]: Erdos-Renyi mean degree 5, N=1e7 (irregular CSR), replica
+    parallel: every rank its own graph instance and R bit-packed replicas
+    (weak scaling); p+c-1 = 2 sweeps + fused count per step."""
+    import torch
+    import mjx
+    n, R, K = args.er_n, args.er_replicas, args.er_steps
+    W = (R + 63) // 64
+    t0 = time.perf_counter()
+    rp, col = mjx.erdos_renyi(n, args.er_deg / (n - 1), seed=args.seed + 31 + 1000 * rank)
+    g = mjx.Graph.csr(rp, col)
+    gen_s = time.perf_counter() - t0
+    gen = torch.Generator(device=dev).manual_seed(args.seed + 5 + rank)
+    s0 = torch.randint(-2 ** 62, 2 ** 62, (n * W,), dtype=torch.int64, device=dev, generator=gen)
+    out, tmp = torch.empty_like(s0), torch.empty_like(s0)
+    counts = torch.zeros(W * 64, dtype=torch.int64, device=dev)
+    T = args.p + args.c - 1
+
+    def step():
+        counts.zero_()
+        mjx.rollout(g, s0, T, words=W, out=out, tmp=tmp, counts=counts)
+
+    step()
+    el = _timed(lambda: [step() for _ in range(K)], dist, dev)
+    nnz = int(rp[-1])
+    dbar = nnz / n
+    bytes_per_sweep = 4 * nnz + 8 * (n + 1) + (W * 8) * n * (dbar + 2)
+    # sanity: an all-(+1) state is a fixed point of every node (isolated ones included)
+    ones = torch.full_like(s0, -1)
+    ck = torch.zeros_like(counts)
+    assert torch.equal(mjx.rollout(g, ones, T, words=W, counts=ck), ones) and bool((ck == n).all())
+    del s0, out, tmp, ones
+    return {
+        "config": f"configs[3]: ER mean degree {args.er_deg:g} N={n} (CSR, own instance per GPU), {R} bit-packed "
+                  f"replicas per GPU, {T} sweeps + fused count per step",
+        "scaling": "weak", "ranks": world, "n": n, "nnz": nnz, "replicas_per_gpu": R, "steps": K,
+        "host_graph_s": gen_s,
+        "ms_per_step": 1e3 * el / K,
+        "node_updates_per_s": world * n * R * T * K / el,
+        "algorithmic_GBps_per_gpu": bytes_per_sweep * T * K / el / 1e9,
+    }
 
 
 def bench_giant(args, rank, world, dist, dev):
@@ -290,10 +338,14 @@ def main():
     if not args.no_sa and args.sa_steps > 0:
         sa_res = bench_sa(args, rank, world, dist, dev)
 
+    del s0, out, tmp, counts, chk, o2
+    torch.cuda.empty_cache()
+    er = None
+    if not args.no_er and args.er_n > 0:
+        er = bench_er(args, rank, world, dist, dev)
+        torch.cuda.empty_cache()
     giant = None
     if not args.no_giant and args.giant_n > 0:
-        del s0, out, tmp, counts, chk, o2
-        torch.cuda.empty_cache()
         giant = bench_giant(args, rank, world, dist, dev)
 
     if rank == 0:
@@ -329,6 +381,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "sa": sa_res,
+            "er": er,
             "giant": giant,
         }
         print(json.dumps(line), flush=True)

@@ -334,8 +334,8 @@ __device__ __forceinline__ void count_epilogue(VertCounter<VW>& vc, bool active,
     }
 }
 
-// BS: block size; the counting sweep runs 1024-thread blocks so that 4x fewer
-// blocks each add their per-replica counts to global memory once.
+// BS: block size (a 1024-thread counting sweep, 4x fewer global count atomics,
+// measured slower on MI355X: 537 vs 508 us at the bench size -- kept at 256).
 template <int D, int VW, bool COUNT, int BS = kBlock>
 __global__ void __launch_bounds__(BS) k_sweep_ell_rp(const int32_t* __restrict__ adj, int64_t n, int64_t W,
                                                      const u64* __restrict__ s_in, u64* __restrict__ s_out,
@@ -588,7 +588,7 @@ static int launch_sweep_csr_np(const int64_t* rp, const int32_t* col, int64_t n,
     return MJX_OK;
 }
 
-constexpr int kCountBlock = 1024;
+constexpr int kCountBlock = kBlock;
 
 template <int VW, bool COUNT>
 static void launch_ell_rp_vw(const int32_t* adj, int64_t n, int d, int64_t W, const u64* in, u64* out,

@@ -132,11 +132,11 @@ def csr_from_edges(n, u, v):
     """Undirected edge list -> CSR (row_ptr int64, col int32), rows sorted by neighbour."""
     src = np.concatenate([u, v]).astype(np.int64)
     dst = np.concatenate([v, u]).astype(np.int64)
-    order = np.lexsort((dst, src))
-    src, dst = src[order], dst[order]
+    keys = src * int(n) + dst
+    keys.sort()                      # one int64 sort (radix-friendly) instead of a lexsort
     row_ptr = np.zeros(n + 1, dtype=np.int64)
-    np.cumsum(np.bincount(src, minlength=n), out=row_ptr[1:])
-    return row_ptr, dst.astype(np.int32)
+    np.cumsum(np.bincount(keys // n, minlength=n), out=row_ptr[1:])
+    return row_ptr, (keys % n).astype(np.int32)
 
 
 def erdos_renyi_edges(n, p, seed=None, chunk=1 << 22):
