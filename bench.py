@@ -60,6 +60,8 @@ def parse():
     ap.add_argument("--er-replicas", type=int, default=4096)
     ap.add_argument("--er-steps", type=int, default=5)
     ap.add_argument("--no-er", action="store_true")
+    ap.add_argument("--bdcm-iters", type=int, default=100)
+    ap.add_argument("--no-bdcm", action="store_true")
     return ap.parse_args()
 
 
@@ -204,6 +206,47 @@ def bench_er(args, rank, world, dist, dev):
     }
 
 
+def bench_bdcm(args, rank, world, dist, dev):
+    """BDCM message passing at the notebook's regime (ER mean degree 5, n=1000,
+    p=c=1, code/ER_BDCM_entropy.ipynb): BDCM_ER iterations/s with the
+    convergence read-back the lambda loop does (nb:422-431), float64; the
+    numpy restatement of one iteration timed beside it on one host core."""
+    import torch
+    import mjx
+    from oracle import bdcm as orc
+    n, deg, p, c = 1000, 5.0, 1, 1
+    plan = mjx.bdcm_er_plan(n, deg / (n - 1), seed=args.seed + 77 + rank)
+    rng = np.random.default_rng(args.seed + rank)
+    chi0 = rng.random((2 * plan.E, 4 ** (p + c)))
+    chi0 /= chi0.sum(axis=1, keepdims=True)
+    chi = torch.from_numpy(chi0).to(dev)
+    mjx.bdcm_leaf_reset(chi, plan, p, c, 1, 0.5)
+    K = args.bdcm_iters
+    dbits = plan._delta
+
+    def run():
+        for _ in range(K):
+            dbits.zero_()
+            mjx.BDCM_ER(chi, plan, p, c, 1, 0.5, 0.1, delta=dbits)
+            float(dbits.view(torch.float64).item())
+
+    run()
+    el = _timed(run, dist, dev)
+    res = {"config": "ER mean degree 5, n=1000, p=c=1, lambda=0.5, damp 0.1 (the notebook's regime), float64",
+           "iters_per_s": world * K / el, "ms_per_iter": 1e3 * el / K, "classes": len(plan.edge_classes)}
+    if rank == 0 and world == 1:
+        hp = orc.Plan.from_csr(plan.edges_host, plan.row_ptr_host, plan.col_host, plan.n, plan.n_iso)
+        x = chi.cpu().numpy()
+        t0 = time.perf_counter()
+        reps = 0
+        while time.perf_counter() - t0 < 3.0:
+            x = orc.BDCM_ER(x, hp, p, c, 1, 0.5, 0.1)
+            reps += 1
+        res["cpu_ms_per_iter"] = 1e3 * (time.perf_counter() - t0) / reps
+        res["cpu_kind"] = "port (oracle/bdcm.py numpy restatement, 1 core)"
+    return res
+
+
 def bench_giant(args, rank, world, dist, dev):
     """configs[4]: ONE d=6 RRG with N=1e9 nodes, partitioned by node range over
     the ranks (strong scaling); each rank generates its own rows on its GPU and
@@ -344,6 +387,9 @@ def main():
     if not args.no_er and args.er_n > 0:
         er = bench_er(args, rank, world, dist, dev)
         torch.cuda.empty_cache()
+    bdcm = None
+    if not args.no_bdcm and args.bdcm_iters > 0:
+        bdcm = bench_bdcm(args, rank, world, dist, dev)
     giant = None
     if not args.no_giant and args.giant_n > 0:
         giant = bench_giant(args, rank, world, dist, dev)
@@ -382,6 +428,7 @@ def main():
             "cpu_baseline": cpu,
             "sa": sa_res,
             "er": er,
+            "bdcm": bdcm,
             "giant": giant,
         }
         print(json.dumps(line), flush=True)
