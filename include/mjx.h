@@ -98,6 +98,13 @@ int mjx_rollout_csr_rp(const int64_t* row_ptr, const int32_t* col, int64_t n, in
                        const uint64_t* s_in, uint64_t* s_out, uint64_t* tmp,
                        int steps, unsigned long long* counts, void* stream);
 
+/* mjx_rollout_csr_rp with a node visiting order (int32 permutation of 0..n-1,
+ * nullable): sorted by degree, the two nodes a wavefront holds share one trip
+ * count.  Results do not depend on the order. */
+int mjx_rollout_csr_rp_ordered(const int64_t* row_ptr, const int32_t* col, const int32_t* order, int64_t n,
+                               int64_t words, const uint64_t* s_in, uint64_t* s_out, uint64_t* tmp,
+                               int steps, unsigned long long* counts, void* stream);
+
 /* per-replica count of +1 spins, ADDED into counts (m(s) = (2*count-n)/n) */
 int mjx_popcount_np(const uint64_t* bits, int64_t n, unsigned long long* counts, void* stream);
 int mjx_popcount_rp(const uint64_t* bits, int64_t n, int64_t words,

@@ -29,6 +29,7 @@ SIGNATURES = {
     "mjx_rollout_ell_np": [c_vp, c_i64, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp],
     "mjx_rollout_ell_rp": [c_vp, c_i64, c_int, c_i64, c_vp, c_vp, c_vp, c_int, c_vp, c_vp],
     "mjx_rollout_ell_rp_sliced": [c_vp, c_i64, c_int, c_i64, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp],
+    "mjx_rollout_csr_rp_ordered": [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_int, c_vp, c_vp],
     "mjx_rollout_csr_np": [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_int, c_vp, c_vp],
     "mjx_rollout_csr_rp": [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_int, c_vp, c_vp],
     "mjx_popcount_np": [c_vp, c_i64, c_vp, c_vp],

@@ -89,8 +89,9 @@ __global__ void __launch_bounds__(kBlock) k_unpack_rp(const u64* __restrict__ bi
 constexpr int KC = 8;                 // planes -> up to 255 words between flushes
 constexpr int kMaxLdsReplicas = 8192; // 32 KiB of LDS counters per block
 
-template <int VW>
+template <int VW, int NK = KC>
 struct VertCounter {
+    static constexpr int KC = NK;
     u64 c[VW][KC];
     int added;
     __device__ __forceinline__ void reset() {
@@ -299,8 +300,8 @@ __device__ __forceinline__ void stv(u64* __restrict__ p, const u64* x) {
 
 // A launch covers the units [unit0, unit0 + Us) of every node (a "slice" of
 // the replicas); LDS counters are indexed relative to the slice.
-template <int VW>
-__device__ __forceinline__ void flush_to(VertCounter<VW>& vc, int use_lds, unsigned* lds,
+template <int VW, int NK>
+__device__ __forceinline__ void flush_to(VertCounter<VW, NK>& vc, int use_lds, unsigned* lds,
                                          unsigned long long* counts, int64_t unit, int64_t unit0) {
     if (use_lds) vc.flush(lds + (unit - unit0) * VW * 64);
     else vc.flush(counts + unit * VW * 64);
@@ -315,8 +316,8 @@ __device__ __forceinline__ void lds_count_init(unsigned* lds, int64_t Us, bool u
 }
 
 // Shared epilogue for the fused per-replica counts.
-template <int VW, bool COUNT, int BS = kBlock>
-__device__ __forceinline__ void count_epilogue(VertCounter<VW>& vc, bool active, int64_t unit, int64_t unit0,
+template <int VW, bool COUNT, int BS = kBlock, int NK = KC>
+__device__ __forceinline__ void count_epilogue(VertCounter<VW, NK>& vc, bool active, int64_t unit, int64_t unit0,
                                                int64_t Us, unsigned* lds, bool use_lds,
                                                unsigned long long* __restrict__ counts) {
     if constexpr (COUNT) {
@@ -369,7 +370,7 @@ __global__ void __launch_bounds__(BS) k_sweep_ell_rp(const int32_t* __restrict__
             stv<VW>(s_out + v * W + unit * VW, out);
             if constexpr (COUNT) {
                 vc.add(out);
-                if (vc.added == (1 << KC) - 1) flush_to<VW>(vc, use_lds, lds_cnt, counts, unit, unit0);
+                if (vc.added == (1 << KC) - 1) flush_to(vc, use_lds, lds_cnt, counts, unit, unit0);
             }
         }
     }
@@ -380,22 +381,26 @@ __global__ void __launch_bounds__(BS) k_sweep_ell_rp(const int32_t* __restrict__
 template <int VW, bool COUNT, bool CSR>
 __global__ void __launch_bounds__(kBlock) k_sweep_gen_rp(const int32_t* __restrict__ adj, int d,
                                                          const int64_t* __restrict__ row_ptr,
-                                                         const int32_t* __restrict__ col, int64_t n, int64_t W,
+                                                         const int32_t* __restrict__ col,
+                                                         const int32_t* __restrict__ order, int64_t n, int64_t W,
                                                          const u64* __restrict__ s_in, u64* __restrict__ s_out,
                                                          unsigned long long* __restrict__ counts, int use_lds,
                                                          int64_t unit0, int64_t Us) {
+    // order (nullable): node visiting order; sorted by degree it keeps the two
+    // nodes a wave holds at one trip count (irregular ER rows)
     extern __shared__ unsigned lds_cnt[];
     const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int64_t slots = ((int64_t)gridDim.x * kBlock) / Us;
     const int64_t unit = unit0 + t % Us, slot = t / Us;
     const bool active = slot < slots;
-    VertCounter<VW> vc;
+    VertCounter<VW, 10> vc;     // up to 1023 nodes per thread between flushes (N = 1e7 rows)
     if constexpr (COUNT) {
         vc.reset();
         lds_count_init<VW>(lds_cnt, Us, use_lds);
     }
     if (active) {
-        for (int64_t v = slot; v < n; v += slots) {
+        for (int64_t i = slot; i < n; i += slots) {
+            const int64_t v = order ? (int64_t)order[i] : i;
             int64_t b, e;
             const int32_t* nbr;
             if constexpr (CSR) {
@@ -407,11 +412,34 @@ __global__ void __launch_bounds__(kBlock) k_sweep_gen_rp(const int32_t* __restri
             BitCounter<8> bc[VW];
 #pragma unroll
             for (int q = 0; q < VW; ++q) bc[q].reset();
-            for (int64_t j = b; j < e; ++j) {
-                u64 x[VW];
-                ldv<VW>(s_in + (int64_t)nbr[j] * W + unit * VW, x);
+            // four gathers in flight per step (rows have d = 5 on average at C4)
+            int64_t j = b;
+            for (; j + 4 <= e; j += 4) {
+                int32_t k[4];
 #pragma unroll
-                for (int q = 0; q < VW; ++q) bc[q].add(x[q]);
+                for (int m = 0; m < 4; ++m) k[m] = nbr[j + m];
+                u64 x[4][VW];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) ldv<VW>(s_in + (int64_t)k[m] * W + unit * VW, x[m]);
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+#pragma unroll
+                    for (int q = 0; q < VW; ++q) bc[q].add(x[m][q]);
+            }
+            if (j < e) {
+                const int rest = (int)(e - j);
+                int32_t k[3];
+#pragma unroll
+                for (int m = 0; m < 3; ++m) k[m] = m < rest ? nbr[j + m] : 0;
+                u64 x[3][VW];
+#pragma unroll
+                for (int m = 0; m < 3; ++m)
+                    if (m < rest) ldv<VW>(s_in + (int64_t)k[m] * W + unit * VW, x[m]);
+#pragma unroll
+                for (int m = 0; m < 3; ++m)
+                    if (m < rest)
+#pragma unroll
+                        for (int q = 0; q < VW; ++q) bc[q].add(x[m][q]);
             }
             u64 own[VW], out[VW];
             ldv<VW>(s_in + v * W + unit * VW, own);
@@ -420,11 +448,11 @@ __global__ void __launch_bounds__(kBlock) k_sweep_gen_rp(const int32_t* __restri
             stv<VW>(s_out + v * W + unit * VW, out);
             if constexpr (COUNT) {
                 vc.add(out);
-                if (vc.added == (1 << KC) - 1) flush_to<VW>(vc, use_lds, lds_cnt, counts, unit, unit0);
+                if (vc.added == (1 << decltype(vc)::KC) - 1) flush_to(vc, use_lds, lds_cnt, counts, unit, unit0);
             }
         }
     }
-    count_epilogue<VW, COUNT>(vc, active, unit, unit0, Us, lds_cnt, use_lds, counts);
+    count_epilogue<VW, COUNT, kBlock, 10>(vc, active, unit, unit0, Us, lds_cnt, use_lds, counts);
 }
 
 }  // namespace mjx
@@ -466,7 +494,7 @@ __global__ void __launch_bounds__(kBlock) k_popcount_rp(const u64* __restrict__ 
             u64 x[VW];
             ldv<VW>(bits + v * W + unit * VW, x);
             vc.add(x);
-            if (vc.added == (1 << KC) - 1) flush_to<VW>(vc, use_lds, lds_cnt, counts, unit, 0);
+            if (vc.added == (1 << KC) - 1) flush_to(vc, use_lds, lds_cnt, counts, unit, 0);
         }
     }
     count_epilogue<VW, true>(vc, active, unit, 0, U, lds_cnt, use_lds, counts);
@@ -601,7 +629,7 @@ static void launch_ell_rp_vw(const int32_t* adj, int64_t n, int d, int64_t W, co
         case 4: k_sweep_ell_rp<4, VW, COUNT, BS><<<g, BS, lds, st>>>(adj, n, W, in, out, counts, use_lds, unit0, Us); break;
         case 6: k_sweep_ell_rp<6, VW, COUNT, BS><<<g, BS, lds, st>>>(adj, n, W, in, out, counts, use_lds, unit0, Us); break;
         default:
-            k_sweep_gen_rp<VW, COUNT, false><<<grid, kBlock, lds, st>>>(adj, d, nullptr, nullptr, n, W, in, out,
+            k_sweep_gen_rp<VW, COUNT, false><<<grid, kBlock, lds, st>>>(adj, d, nullptr, nullptr, nullptr, n, W, in, out,
                                                                        counts, use_lds, unit0, Us);
             break;
     }
@@ -647,19 +675,21 @@ static int launch_sweep_ell_rp(const int32_t* adj, int64_t n, int d, int64_t W, 
     return MJX_OK;
 }
 
-static int launch_sweep_csr_rp(const int64_t* rp, const int32_t* col, int64_t n, int64_t W, const u64* in,
-                               u64* out, unsigned long long* counts, int64_t unit0, int64_t Us, hipStream_t st) {
+static int launch_sweep_csr_rp(const int64_t* rp, const int32_t* col, const int32_t* order, int64_t n, int64_t W,
+                               const u64* in, u64* out, unsigned long long* counts, int64_t unit0, int64_t Us,
+                               hipStream_t st) {
     int grid, vw, use_lds; size_t lds;
     int rc = rp_geometry(n, W, Us, &grid, &vw, &use_lds, &lds);
     if (rc) return rc;
     if (!counts) { lds = 0; use_lds = 0; }
+#define MJX_CSR(VWV, C) k_sweep_gen_rp<VWV, C, true><<<grid, kBlock, lds, st>>>(nullptr, 0, rp, col, order, n, W, in, \
+                                                                               out, counts, use_lds, unit0, Us)
     if (vw == 2) {
-        if (counts) k_sweep_gen_rp<2, true, true><<<grid, kBlock, lds, st>>>(nullptr, 0, rp, col, n, W, in, out, counts, use_lds, unit0, Us);
-        else k_sweep_gen_rp<2, false, true><<<grid, kBlock, lds, st>>>(nullptr, 0, rp, col, n, W, in, out, counts, use_lds, unit0, Us);
+        if (counts) MJX_CSR(2, true); else MJX_CSR(2, false);
     } else {
-        if (counts) k_sweep_gen_rp<1, true, true><<<grid, kBlock, lds, st>>>(nullptr, 0, rp, col, n, W, in, out, counts, use_lds, unit0, Us);
-        else k_sweep_gen_rp<1, false, true><<<grid, kBlock, lds, st>>>(nullptr, 0, rp, col, n, W, in, out, counts, use_lds, unit0, Us);
+        if (counts) MJX_CSR(1, true); else MJX_CSR(1, false);
     }
+#undef MJX_CSR
     MJX_LAUNCH_CHECK("sweep_csr_rp");
     return MJX_OK;
 }
@@ -790,9 +820,9 @@ extern "C" int mjx_rollout_csr_np(const int64_t* row_ptr, const int32_t* col, in
     return run_rollout(steps, (const u64*)s_in, (u64*)s_out, (u64*)tmp, counts, sweep);
 }
 
-extern "C" int mjx_rollout_csr_rp(const int64_t* row_ptr, const int32_t* col, int64_t n, int64_t words,
-                                  const uint64_t* s_in, uint64_t* s_out, uint64_t* tmp, int steps,
-                                  unsigned long long* counts, void* stream) {
+extern "C" int mjx_rollout_csr_rp_ordered(const int64_t* row_ptr, const int32_t* col, const int32_t* order,
+                                          int64_t n, int64_t words, const uint64_t* s_in, uint64_t* s_out,
+                                          uint64_t* tmp, int steps, unsigned long long* counts, void* stream) {
     if (n < 0 || words < 1 || (n > 0 && (!row_ptr || !s_in || !s_out))) return MJX_EINVAL;
     if (n > (int64_t)INT32_MAX) return MJX_ERANGE;
     if (overlaps(s_in, s_out) || overlaps(s_in, tmp) || overlaps(s_out, tmp)) return MJX_EINVAL;
@@ -809,10 +839,16 @@ extern "C" int mjx_rollout_csr_rp(const int64_t* row_ptr, const int32_t* col, in
     const int64_t Us = U / S;
     for (int q = 0; q < S; ++q) {
         auto sweep = [&](const u64* a, u64* b, unsigned long long* c) {
-            return launch_sweep_csr_rp(row_ptr, col, n, words, a, b, c, q * Us, Us, st);
+            return launch_sweep_csr_rp(row_ptr, col, order, n, words, a, b, c, q * Us, Us, st);
         };
         int rc = run_rollout(steps, (const u64*)s_in, (u64*)s_out, (u64*)tmp, counts, sweep);
         if (rc) return rc;
     }
     return MJX_OK;
+}
+
+extern "C" int mjx_rollout_csr_rp(const int64_t* row_ptr, const int32_t* col, int64_t n, int64_t words,
+                                  const uint64_t* s_in, uint64_t* s_out, uint64_t* tmp, int steps,
+                                  unsigned long long* counts, void* stream) {
+    return mjx_rollout_csr_rp_ordered(row_ptr, col, nullptr, n, words, s_in, s_out, tmp, steps, counts, stream);
 }

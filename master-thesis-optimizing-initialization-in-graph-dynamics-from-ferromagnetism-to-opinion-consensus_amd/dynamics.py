@@ -81,8 +81,9 @@ def rollout(graph, bits, steps, words=None, out=None, tmp=None, counts=None, sli
             _lib.call("mjx_rollout_csr_np", _device.ptr(graph.row_ptr), _device.ptr(graph.col), graph.n,
                       _device.ptr(bits), _device.ptr(out), tptr, int(steps), cptr, st)
         else:
-            _lib.call("mjx_rollout_csr_rp", _device.ptr(graph.row_ptr), _device.ptr(graph.col), graph.n,
-                      int(words), _device.ptr(bits), _device.ptr(out), tptr, int(steps), cptr, st)
+            _lib.call("mjx_rollout_csr_rp_ordered", _device.ptr(graph.row_ptr), _device.ptr(graph.col),
+                      _device.ptr(graph.order) if graph.order is not None else None, graph.n, int(words),
+                      _device.ptr(bits), _device.ptr(out), tptr, int(steps), cptr, st)
     return out
 
 

@@ -242,9 +242,10 @@ class Graph:
     kind == "csr": ``row_ptr`` int64 (n+1,), ``col`` int32 (nnz,) — any graph.
     """
 
-    def __init__(self, kind, n, d=None, adj=None, row_ptr=None, col=None):
+    def __init__(self, kind, n, d=None, adj=None, row_ptr=None, col=None, order=None):
         self.kind, self.n, self.d = kind, int(n), d
         self.adj, self.row_ptr, self.col = adj, row_ptr, col
+        self.order = order          # CSR: nodes sorted by degree (visiting order of the rp sweep)
 
     @classmethod
     def ell(cls, adj):
@@ -271,7 +272,8 @@ class Graph:
             raise ValueError("CSR column index out of range")
         if n and int(np.diff(rp).max()) > 255:
             raise ValueError("CSR rows longer than 255 are not supported by the bit-sliced counter")
-        return cls("csr", n, row_ptr=_device.to_device(rp), col=_device.to_device(cl))
+        order = np.argsort(np.diff(rp), kind="stable").astype(np.int32)
+        return cls("csr", n, row_ptr=_device.to_device(rp), col=_device.to_device(cl), order=_device.to_device(order))
 
     @property
     def nnz(self):
