@@ -94,6 +94,106 @@ __global__ void __launch_bounds__(64) k_sa_init_draw(int64_t n, int64_t R, int64
     }
 }
 
+// ---------------------------------------------------------------------------
+// init, wave per replica: the replica's MT19937 state in LDS, twisted by the
+// whole wave; the 312 node draws of each twist become node-packed bits of a
+// per-replica scratch row (ballot per 64-node word), then a 64x64 bit
+// transpose per (word column, node word) writes the replica-packed layout.
+// Same stream, same spins as k_sa_init_draw, with 64x the parallelism.
+// ---------------------------------------------------------------------------
+__device__ void lds_twist(uint32_t* buf, int lane) {
+    for (int k = lane; k < MT_N - MT_M; k += 64) {
+        const uint32_t v = mt_mix(buf[k], buf[k + 1], buf[k + MT_M]);
+        __builtin_amdgcn_wave_barrier();
+        buf[k] = v;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+    for (int k = MT_N - MT_M + lane; k < 2 * (MT_N - MT_M); k += 64) {
+        const uint32_t v = mt_mix(buf[k], buf[k + 1], buf[k + MT_M - MT_N]);
+        __builtin_amdgcn_wave_barrier();
+        buf[k] = v;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+    for (int k = 2 * (MT_N - MT_M) + lane; k < MT_N - 1; k += 64) {
+        const uint32_t v = mt_mix(buf[k], buf[k + 1], buf[k + MT_M - MT_N]);
+        __builtin_amdgcn_wave_barrier();
+        buf[k] = v;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (lane == 0) buf[MT_N - 1] = mt_mix(buf[MT_N - 1], buf[0], buf[MT_M - 1]);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+__global__ void __launch_bounds__(64) k_sa_init_np(int64_t n, int64_t R, int64_t r0, const uint32_t* __restrict__ seeds,
+                                                   u64* __restrict__ np_bits, uint32_t* __restrict__ mt_out,
+                                                   int32_t* __restrict__ idx_out) {
+    __shared__ uint32_t st[MT_N];
+    __shared__ uint32_t tw[MT_N];
+    const int lane = threadIdx.x;
+    const int64_t r = r0 + blockIdx.x;
+    const int64_t nw = (n + 63) >> 6;
+    u64* row = np_bits + (int64_t)blockIdx.x * nw;
+    if (r >= R) {                                    // padding replica: spins -1
+        for (int64_t w = lane; w < nw; w += 64) row[w] = 0;
+        return;
+    }
+    if (lane == 0) {                                 // init_genrand / numpy mt19937_seed
+        uint32_t x = seeds[r];
+        for (int k = 0; k < MT_N; ++k) {
+            st[k] = x;
+            x = 1812433253u * (x ^ (x >> 30)) + (uint32_t)(k + 1);
+        }
+    }
+    __syncthreads();
+    u64 acc = 0;
+    for (int64_t v = 0; v < n; v += MT_N / 2) {
+        lds_twist(st, lane);
+        for (int k = lane; k < MT_N; k += 64) tw[k] = mt_temper(st[k]);
+        __syncthreads();
+        const int64_t vend = (n - v < MT_N / 2) ? n : v + MT_N / 2;
+        for (int64_t c0 = v; c0 < vend;) {
+            const int64_t ws = c0 & ~63ll, we = ws + 64;
+            const int64_t node = ws + lane;
+            bool plus = false;
+            if (node >= c0 && node < vend) {
+                const int j = (int)(node - v);
+                plus = mt_double(tw[2 * j], tw[2 * j + 1]) > 0.5;      // binomial(1, .5) (code/SA_RRG.py:65)
+            }
+            acc |= __ballot(plus);
+            if (we <= vend || vend == n) {
+                if (lane == 0) row[ws >> 6] = acc;
+                acc = 0;
+            }
+            c0 = we < vend ? we : vend;
+        }
+        __syncthreads();
+    }
+    for (int k = lane; k < MT_N; k += 64) mt_out[r * MT_N + k] = st[k];
+    if (lane == 0) idx_out[r] = (int32_t)(2 * n - (int64_t)MT_N * ((2 * n + MT_N - 1) / MT_N - 1));
+}
+
+// word column w (64 replicas) x node word c: 64x64 bit transpose by ballots
+__global__ void __launch_bounds__(256) k_np_to_rp(const u64* __restrict__ np_bits, int64_t n, int64_t W,
+                                                  int64_t w0, int64_t ncols, u64* __restrict__ s) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (n + 63) >> 6;
+    const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+    if (wave >= ncols * nw) return;                  // whole wave exits together
+    const int64_t wl = wave / nw, c = wave % nw;
+    const u64 x = np_bits[(wl * 64 + lane) * nw + c];
+    u64 out = 0;
+    for (int j = 0; j < 64; ++j) {
+        const u64 b = __ballot((x >> j) & 1ull);
+        if (lane == j) out = b;
+    }
+    const int64_t node = c * 64 + lane;
+    if (node < n) s[node * W + (w0 + wl)] = out;
+}
+
 __global__ void k_sa_init_state(int64_t n, int64_t R, double a0, double b0,
                                 const unsigned long long* __restrict__ cnt, mjx_sa_state st) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -496,8 +596,24 @@ extern "C" int mjx_sa_init(const int32_t* adj, int64_t n, int d, int p, int c, i
     const int T = p + c - 1;
     if (T >= 2 && !tmp2) return MJX_EINVAL;
     hipStream_t hs = as_stream(stream);
-    k_sa_init_draw<<<(unsigned)W, 64, 0, hs>>>(n, R, W, seeds, (u64*)s, st.mt, st.mt_idx);
-    MJX_LAUNCH_CHECK("k_sa_init_draw");
+    // s0 draws, wave per replica, through node-packed rows in tmp1 (n*W words
+    // hold G word columns of 64 rows of ceil(n/64) words each)
+    const int64_t nw = (n + 63) / 64;
+    int64_t G = (n * W) / (64 * nw);
+    if (G > W) G = W;
+    if (G < 1) {                                     // tiny n: the lane-per-replica path
+        k_sa_init_draw<<<(unsigned)W, 64, 0, hs>>>(n, R, W, seeds, (u64*)s, st.mt, st.mt_idx);
+        MJX_LAUNCH_CHECK("k_sa_init_draw");
+    } else {
+        for (int64_t w0 = 0; w0 < W; w0 += G) {
+            const int64_t cols = (W - w0 < G) ? W - w0 : G;
+            k_sa_init_np<<<(unsigned)(cols * 64), 64, 0, hs>>>(n, R, w0 * 64, seeds, (u64*)tmp1, st.mt, st.mt_idx);
+            MJX_LAUNCH_CHECK("k_sa_init_np");
+            const int64_t waves = cols * nw;
+            k_np_to_rp<<<(unsigned)((waves + 3) / 4), 256, 0, hs>>>((const u64*)tmp1, n, W, w0, cols, (u64*)s);
+            MJX_LAUNCH_CHECK("k_np_to_rp");
+        }
+    }
     MJX_HIP(hipMemsetAsync(st.cnt, 0, (size_t)R * sizeof(unsigned long long), hs), "sa_init memset");
     int rc = mjx_rollout_ell_rp(adj, n, d, W, s, tmp1, tmp2, T, st.cnt, stream);
     if (rc) return rc;
