@@ -54,6 +54,7 @@ def parse():
     ap.add_argument("--giant-n", type=int, default=1_000_000_000)
     ap.add_argument("--giant-d", type=int, default=6)
     ap.add_argument("--giant-sweeps", type=int, default=10)
+    ap.add_argument("--giant-mode", default="binned", choices=["binned", "gather"])
     ap.add_argument("--no-giant", action="store_true")
     ap.add_argument("--er-n", type=int, default=10_000_000)
     ap.add_argument("--er-deg", type=float, default=5.0)
@@ -256,7 +257,8 @@ def bench_giant(args, rank, world, dist, dev):
     n, d, K = args.giant_n, args.giant_d, args.giant_sweeps
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    sh = mjx.ShardedRRG(d, n, seed=args.seed + 12345)
+    sh = mjx.ShardedRRG(d, n, seed=args.seed + 12345, mode=args.giant_mode)
+    sh.drop_adjacency()
     torch.cuda.synchronize()
     gen_s = time.perf_counter() - t0
     gen = torch.Generator(device=dev).manual_seed(args.seed + 99)     # same replicated state on every rank
@@ -277,9 +279,10 @@ def bench_giant(args, rank, world, dist, dev):
     per_update_bytes = 4 * d + (d + 2) / 8.0          # 4 d/R + (d+2)/8 at R = 1
     return {
         "config": f"configs[4]: one d={d} RRG N={n} partitioned by node range over {world} GPU(s), "
-                  "per-sweep in-place RCCL all-gather of the node-packed state",
-        "scaling": "strong", "ranks": world, "n": n, "d": d, "sweeps": K,
-        "gen_s": gen_s,
+                  "per-sweep in-place RCCL all-gather of the node-packed state; setup = device generation "
+                  "(+ source-binned plan)",
+        "scaling": "strong", "ranks": world, "n": n, "d": d, "sweeps": K, "mode": args.giant_mode,
+        "setup_s": gen_s,
         "ms_per_sweep": 1e3 * el / K,
         "node_updates_per_s": n * K / el,
         "algorithmic_GBps": n * K * per_update_bytes / el / 1e9,

@@ -212,6 +212,20 @@ int mjx_hpr_new_biases(int dtype, void* biases, const void* marg, const double* 
 int mjx_sweep_ell_np_range(const int32_t* adj, int64_t n, int d, int64_t row_lo, int64_t row_hi,
                            const uint64_t* s_in, uint64_t* s_out, unsigned long long* counts, void* stream);
 
+/* Source-binned sweep (one replica, huge n): a static plan bins the n_rows*d
+ * (destination, source) slots of rows [row_lo, row_hi) by source block (2 MB
+ * of state bits, L2-resident) and destination tile (8192 nodes); a sweep
+ * streams the plan instead of gathering one random cache line per slot.
+ * Same result as mjx_sweep_ell_np_range.  mjx_binned_plan_shape gives the
+ * sizes: src int32[slots], off uint16[slots], seg_ptr int64[segments+1],
+ * msg uint64[ceil(slots/64)] (per-sweep message bits); work >= 64 MiB.  */
+int mjx_binned_plan_shape(int64_t n, int d, int64_t row_lo, int64_t row_hi, int64_t* slots, int64_t* segments);
+int mjx_binned_build(const int32_t* adj, int64_t n, int d, int64_t row_lo, int64_t row_hi, int32_t* src,
+                     uint16_t* off, long long* seg_ptr, void* work, int64_t work_bytes, void* stream);
+int mjx_sweep_binned(const int32_t* src, const uint16_t* off, const long long* seg_ptr, int64_t n, int d,
+                     int64_t row_lo, int64_t row_hi, const uint64_t* s_in, uint64_t* msg, uint64_t* s_out,
+                     unsigned long long* counts, void* stream);
+
 /* ---- device graph generation ----------------------- */
 /* Random simple d-regular graph (configuration model through a keyed
  * pseudorandom stub permutation, then deterministic double-edge switches that

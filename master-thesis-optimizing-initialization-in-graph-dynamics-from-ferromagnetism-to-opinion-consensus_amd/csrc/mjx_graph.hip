@@ -17,6 +17,7 @@
 #include <unordered_map>
 #include <utility>
 #include <vector>
+#include <hipcub/hipcub.hpp>
 
 namespace mjx {
 namespace gen {
@@ -291,5 +292,190 @@ extern "C" int mjx_graph_check_ell(const int32_t* adj, int64_t n, int d, unsigne
     if (n == 0 || d == 0) return MJX_OK;
     k_check_ell<<<grid_for(n, 8), 256, 0, as_stream(stream)>>>(adj, n, d, counts);
     MJX_LAUNCH_CHECK("k_check_ell");
+    return MJX_OK;
+}
+
+// ===========================================================================
+// Source-binned sweep of a node-packed state (one replica, huge n: config C5).
+//
+// The gather sweep reads s[u] for 6e9 random u per sweep at N=1e9, d=6: every
+// 4-byte gather costs a cache line from a 125 MB state that no L2 holds, so it
+// runs at the random line rate.  Here the n*d (destination, source) slots of a
+// rank's rows are binned once (a static plan) by source block b = u >> kSrcShift
+// (2 MB of state bits each, L2-resident) and, inside a block, by destination
+// tile t = (v - lo) >> kTileShift.  A sweep is then
+//   phase 1: stream the slots block by block, read s[u] (an L2 hit: the whole
+//            chip works on one or two source blocks at a time) and write one
+//            message bit per slot, in slot order (coalesced);
+//   phase 2: one workgroup per destination tile gathers its K contiguous
+//            segments (message bits + 16-bit tile offsets), counts +1
+//            neighbours per node in LDS and applies the majority rule
+//            (always-stay ties, code/SA_RRG.py:19-20) against the node's own bit.
+// Traffic per sweep ~ 4 + 2 bytes of static plan and 2/8 bit of messages per
+// slot, all streamed, instead of a random line per slot.
+// ===========================================================================
+namespace mjx {
+namespace binned {
+
+constexpr int kSrcShift = 24;          // 16M nodes = 2 MB of bits per source block
+constexpr int kTileShift = 13;         // 8192 destinations per tile (32 KB of LDS counters)
+constexpr int kTile = 1 << kTileShift;
+
+__host__ __device__ inline int64_t nblocks(int64_t n) { return (n + (1ll << kSrcShift) - 1) >> kSrcShift; }
+__host__ __device__ inline int64_t ntiles(int64_t rows) { return (rows + kTile - 1) >> kTileShift; }
+
+// slot counts per (block, tile): one workgroup per tile, LDS histogram over blocks
+__global__ void __launch_bounds__(256) k_bin_count(const int32_t* __restrict__ adj, int64_t rows, int d, int64_t K,
+                                                   int64_t T, long long* __restrict__ cnt) {
+    extern __shared__ unsigned hist[];
+    const int64_t t = blockIdx.x;
+    for (int64_t b = threadIdx.x; b < K; b += 256) hist[b] = 0;
+    __syncthreads();
+    const int64_t s0 = t * kTile * d, s1 = ((t + 1) * kTile < rows ? (t + 1) * kTile : rows) * d;
+    for (int64_t q = s0 + threadIdx.x; q < s1; q += 256) atomicAdd(&hist[adj[q] >> kSrcShift], 1u);
+    __syncthreads();
+    for (int64_t b = threadIdx.x; b < K; b += 256) cnt[b * T + t] = hist[b];
+}
+
+// place every slot at seg_ptr[b*T + t] + (its rank inside the segment; order
+// inside a segment is free: phase 2 only counts)
+__global__ void __launch_bounds__(256) k_bin_fill(const int32_t* __restrict__ adj, int64_t rows, int d, int64_t K,
+                                                  int64_t T, const long long* __restrict__ seg_ptr,
+                                                  int32_t* __restrict__ src, uint16_t* __restrict__ off) {
+    extern __shared__ unsigned cur[];
+    const int64_t t = blockIdx.x;
+    for (int64_t b = threadIdx.x; b < K; b += 256) cur[b] = 0;
+    __syncthreads();
+    const int64_t s0 = t * kTile * d, s1 = ((t + 1) * kTile < rows ? (t + 1) * kTile : rows) * d;
+    for (int64_t q = s0 + threadIdx.x; q < s1; q += 256) {
+        const int32_t u = adj[q];
+        const int64_t b = u >> kSrcShift;
+        const int64_t pos = seg_ptr[b * T + t] + atomicAdd(&cur[b], 1u);
+        src[pos] = u;
+        off[pos] = (uint16_t)((q / d) - t * kTile);
+    }
+}
+
+// phase 1: message bit of every slot, in plan order
+__global__ void __launch_bounds__(256) k_bin_messages(const int32_t* __restrict__ src, int64_t slots,
+                                                      const uint32_t* __restrict__ s32, u64* __restrict__ msg) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nwords = (slots + 63) >> 6;
+    const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * 256) >> 6;
+    for (int64_t w = wave; w < nwords; w += nwaves) {
+        const int64_t e = (w << 6) + lane;
+        bool bit = false;
+        if (e < slots) {
+            const int32_t u = src[e];
+            bit = (s32[u >> 5] >> (u & 31)) & 1u;
+        }
+        const u64 word = __ballot(bit);
+        if (lane == 0) msg[w] = word;
+    }
+}
+
+// phase 2: one workgroup per destination tile
+__global__ void __launch_bounds__(256) k_bin_update(const uint16_t* __restrict__ off,
+                                                    const long long* __restrict__ seg_ptr, const u64* __restrict__ msg,
+                                                    int64_t K, int64_t T, int64_t lo, int64_t hi, int d,
+                                                    const uint32_t* __restrict__ s32, u64* __restrict__ s_out,
+                                                    unsigned long long* __restrict__ counts) {
+    __shared__ unsigned cnt[kTile];
+    __shared__ unsigned long long red[4];
+    const int64_t t = blockIdx.x;
+    for (int i = threadIdx.x; i < kTile; i += 256) cnt[i] = 0;
+    __syncthreads();
+    for (int64_t b = 0; b < K; ++b) {
+        const int64_t e0 = seg_ptr[b * T + t], e1 = seg_ptr[b * T + t + 1];
+        for (int64_t e = e0 + threadIdx.x; e < e1; e += 256) {
+            const unsigned bit = (unsigned)((msg[e >> 6] >> (e & 63)) & 1ull);
+            if (bit) atomicAdd(&cnt[off[e]], 1u);
+        }
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int64_t v0 = lo + t * kTile;
+    const int64_t v1 = (v0 + kTile < hi) ? v0 + kTile : hi;
+    unsigned long long ones = 0;
+    for (int64_t w = (v0 >> 6) + (threadIdx.x >> 6); w < ((v1 + 63) >> 6); w += 4) {
+        const int64_t v = (w << 6) + lane;
+        bool nb = false;
+        if (v < v1) {
+            const int c = (int)cnt[v - v0];
+            const int own = (s32[v >> 5] >> (v & 31)) & 1u;
+            nb = (2 * c > d) || ((2 * c == d) && own);
+        }
+        const u64 word = __ballot(nb);
+        if (lane == 0) {
+            s_out[w] = word;
+            ones += __popcll(word);
+        }
+    }
+    if (counts) {
+        if (lane == 0) red[threadIdx.x >> 6] = ones;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const unsigned long long tot = red[0] + red[1] + red[2] + red[3];
+            if (tot) atomicAdd(counts, tot);
+        }
+    }
+}
+
+}  // namespace binned
+}  // namespace mjx
+
+extern "C" int mjx_binned_plan_shape(int64_t n, int d, int64_t row_lo, int64_t row_hi, int64_t* slots,
+                                     int64_t* segments) {
+    using namespace mjx::binned;
+    if (n < 1 || d < 1 || d > 16 || row_lo < 0 || row_hi > n || row_lo > row_hi || !slots || !segments)
+        return MJX_EINVAL;
+    if ((row_lo & 63) || ((row_hi & 63) && row_hi != n)) return MJX_EINVAL;
+    *slots = (row_hi - row_lo) * d;
+    *segments = nblocks(n) * ntiles(row_hi - row_lo);
+    return MJX_OK;
+}
+
+extern "C" int mjx_binned_build(const int32_t* adj, int64_t n, int d, int64_t row_lo, int64_t row_hi, int32_t* src,
+                                uint16_t* off, long long* seg_ptr, void* work, int64_t work_bytes, void* stream) {
+    using namespace mjx::binned;
+    if (n < 1 || d < 1 || d > 16 || row_lo < 0 || row_hi > n || row_lo > row_hi) return MJX_EINVAL;
+    if ((row_lo & 63) || ((row_hi & 63) && row_hi != n)) return MJX_EINVAL;
+    if (n > (int64_t)INT32_MAX) return MJX_ERANGE;
+    const int64_t rows = row_hi - row_lo;
+    if (rows == 0) return MJX_OK;
+    if (!adj || !src || !off || !seg_ptr || !work) return MJX_EINVAL;
+    const int64_t K = nblocks(n), T = ntiles(rows), S = K * T;
+    if (K * 4 > 64 * 1024) return MJX_ERANGE;
+    hipStream_t st = as_stream(stream);
+    // counts into seg_ptr[0..S), then an in-place exclusive scan -> seg_ptr[0..S]
+    MJX_HIP(hipMemsetAsync(seg_ptr + S, 0, sizeof(long long), st), "bin memset");
+    k_bin_count<<<(unsigned)T, 256, K * sizeof(unsigned), st>>>(adj, rows, d, K, T, seg_ptr);
+    MJX_LAUNCH_CHECK("k_bin_count");
+    size_t need = 0;
+    MJX_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, need, seg_ptr, seg_ptr, S + 1, st), "bin scan size");
+    if ((int64_t)need > work_bytes) return MJX_ERANGE;
+    MJX_HIP(hipcub::DeviceScan::ExclusiveSum(work, need, seg_ptr, seg_ptr, S + 1, st), "bin scan");
+    k_bin_fill<<<(unsigned)T, 256, K * sizeof(unsigned), st>>>(adj, rows, d, K, T, seg_ptr, src, off);
+    MJX_LAUNCH_CHECK("k_bin_fill");
+    return MJX_OK;
+}
+
+extern "C" int mjx_sweep_binned(const int32_t* src, const uint16_t* off, const long long* seg_ptr, int64_t n, int d,
+                                int64_t row_lo, int64_t row_hi, const uint64_t* s_in, uint64_t* msg, uint64_t* s_out,
+                                unsigned long long* counts, void* stream) {
+    using namespace mjx::binned;
+    if (n < 1 || d < 1 || d > 16 || row_lo < 0 || row_hi > n || row_lo > row_hi) return MJX_EINVAL;
+    if (row_hi == row_lo) return MJX_OK;
+    if ((row_lo & 63) || ((row_hi & 63) && row_hi != n)) return MJX_EINVAL;
+    if (!src || !off || !seg_ptr || !s_in || !msg || !s_out || s_in == s_out) return MJX_EINVAL;
+    const int64_t rows = row_hi - row_lo, slots = rows * d;
+    const int64_t K = nblocks(n), T = ntiles(rows);
+    hipStream_t st = as_stream(stream);
+    k_bin_messages<<<grid_for(((slots + 63) / 64) * 64), 256, 0, st>>>(src, slots, (const uint32_t*)s_in, (u64*)msg);
+    MJX_LAUNCH_CHECK("k_bin_messages");
+    k_bin_update<<<(unsigned)T, 256, 0, st>>>(off, seg_ptr, (const u64*)msg, K, T, row_lo, row_hi, d,
+                                             (const uint32_t*)s_in, (u64*)s_out, counts);
+    MJX_LAUNCH_CHECK("k_bin_update");
     return MJX_OK;
 }

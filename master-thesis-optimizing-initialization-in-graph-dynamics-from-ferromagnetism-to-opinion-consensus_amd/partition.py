@@ -61,7 +61,7 @@ def unpack_host(words, n):
 class ShardedRRG:
     """This rank's part of one d-regular graph and the replicated spin state."""
 
-    def __init__(self, d, n, seed=0, group=None, adj_rows=None, local_sweep=None, device=None):
+    def __init__(self, d, n, seed=0, group=None, adj_rows=None, local_sweep=None, device=None, mode="binned"):
         import torch.distributed as dist
         self.dist = dist if dist.is_available() and dist.is_initialized() else None
         self.group = group
@@ -76,12 +76,20 @@ class ShardedRRG:
                 from .graph import random_regular_rows_device
                 adj_rows = random_regular_rows_device(self.d, self.n, self.seed, r.lo, r.hi)
             self.adj = _device.to_device(adj_rows, dtype=torch.int32)
-            self.local_sweep = self._hip_sweep
+            if mode == "binned":
+                self._build_binned()
+                self.local_sweep = self._binned_sweep
+            elif mode == "gather":
+                self.local_sweep = self._hip_sweep
+            else:
+                raise ValueError(f"unknown sweep mode {mode!r}")
+            self.mode = mode
         else:
             self.device = torch.device("cpu") if device is None else device
             self.adj = adj_rows
             self.local_sweep = local_sweep
-        if self.adj is not None and tuple(self.adj.shape) != (r.hi - r.lo, self.d):
+            self.mode = "custom"
+        if self.adj is not None and tuple(self.adj.shape) != (r.hi - r.lo, self.d):  # checked before the plan
             raise ValueError(f"rank {self.rank} owns rows [{r.lo}, {r.hi}): adjacency must be "
                              f"({r.hi - r.lo}, {self.d}), got {tuple(self.adj.shape)}")
         self.buf = [torch.zeros(r.words_padded, dtype=torch.int64, device=self.device) for _ in range(2)]
@@ -94,6 +102,37 @@ class ShardedRRG:
         _lib.call("mjx_sweep_ell_np_range", _device.ptr(self.adj) if self.adj.numel() else None, self.n, self.d,
                   r.lo, r.hi, _device.ptr(s_in), _device.ptr(s_out),
                   _device.ptr(counts) if counts is not None else None, _device.stream_handle())
+
+    def _build_binned(self):
+        """Static source-binned plan of this rank's rows (mjx_binned_build)."""
+        import ctypes
+        r = self.range
+        if tuple(self.adj.shape) != (r.hi - r.lo, self.d):
+            raise ValueError(f"rank {self.rank} owns rows [{r.lo}, {r.hi}): adjacency must be "
+                             f"({r.hi - r.lo}, {self.d}), got {tuple(self.adj.shape)}")
+        slots, segs = ctypes.c_int64(0), ctypes.c_int64(0)
+        _lib.call("mjx_binned_plan_shape", self.n, self.d, r.lo, r.hi, ctypes.byref(slots), ctypes.byref(segs))
+        dev = self.device
+        self.bin_src = torch.empty(max(slots.value, 1), dtype=torch.int32, device=dev)
+        self.bin_off = torch.empty(max(slots.value, 1), dtype=torch.int16, device=dev)
+        self.bin_seg = torch.empty(segs.value + 1, dtype=torch.int64, device=dev)
+        self.bin_msg = torch.empty(max((slots.value + 63) // 64, 1), dtype=torch.int64, device=dev)
+        work = torch.empty(64 << 20, dtype=torch.uint8, device=dev)
+        _lib.call("mjx_binned_build", _device.ptr(self.adj) if self.adj.numel() else None, self.n, self.d, r.lo, r.hi,
+                  _device.ptr(self.bin_src), _device.ptr(self.bin_off), _device.ptr(self.bin_seg), _device.ptr(work),
+                  work.numel(), _device.stream_handle())
+        del work
+
+    def _binned_sweep(self, s_in, s_out, counts):
+        r = self.range
+        _lib.call("mjx_sweep_binned", _device.ptr(self.bin_src), _device.ptr(self.bin_off), _device.ptr(self.bin_seg),
+                  self.n, self.d, r.lo, r.hi, _device.ptr(s_in), _device.ptr(self.bin_msg), _device.ptr(s_out),
+                  _device.ptr(counts) if counts is not None else None, _device.stream_handle())
+
+    def drop_adjacency(self):
+        """Free the ELL rows once the binned plan is built (24 GB at C5 on one GPU)."""
+        if self.mode == "binned":
+            self.adj = None
 
     def exchange(self, buf):
         """All-gather every rank's word slice into the replicated state (in place)."""
