@@ -11,6 +11,7 @@ from .graph import (Graph, neighbours, csr_from_networkx, random_regular_graph, 
                     erdos_renyi, erdos_renyi_edges, csr_from_edges, remove_isolated,
                     random_regular_rows_device, random_regular_graph_device, check_ell)
 from .partition import NodeRange, ShardedRRG, pack_host, unpack_host
+from .npz import save_sa_npz, save_hpr_npz, save_bdcm_npz, sa_arrays, hpr_arrays
 from .dynamics import onestep_majority, s_endstate, m, pack, unpack, rollout, popcount, as_graph
 from .sa import SAReplicas, E_delta, sa_run, schedule_constants
 from .hpr import HPRPlan, HPRState, HPr_dp, marginals_comp, new_biases_i, hpr_run

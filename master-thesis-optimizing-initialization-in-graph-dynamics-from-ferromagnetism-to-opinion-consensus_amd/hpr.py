@@ -204,9 +204,40 @@ class HPRState:
         self.t += 1
         return self.sum_end()
 
+    def steps_batched(self, k, generator):
+        """k iterations of the main loop (code/HPR_pytorch_RRG.py:345-356) with no
+        host read in between: the k uniform vectors are drawn up front from the
+        CPU generator in the reference's order (one torch.rand(n) per iteration,
+        :142), every iteration's trial configuration and sum(s_endstate(s)) are
+        kept on the device, and one read returns them all.
+        Returns (sums[k] int64 numpy, s_hist (k, n) int32 device tensor)."""
+        n = self.plan.n
+        dev = self.s.device
+        u = torch.stack([torch.rand(n, dtype=torch.float64, generator=generator) for _ in range(k)]).to(dev)
+        s_hist = torch.empty((k, n), dtype=torch.int32, device=dev)
+        cnt = torch.zeros(k, dtype=torch.int64, device=dev)
+        bits = torch.empty((n + 63) // 64, dtype=torch.int64, device=dev)
+        T = self.p + self.c - 1
+        for j in range(k):
+            HPr_dp(self.chi, self.biases, self.plan, self.p, self.c, self.attr_value, self.lmbd_in, self.damppar,
+                   out=self.chi_b)
+            self.chi, self.chi_b = self.chi_b, self.chi
+            marginals_comp(self.chi, self.plan, self.p, self.c, zwork=self.zwork, out=self.marg)
+            new_biases_i(self.biases, self.pie, self.gamma, self.marg, self.t + j, u=u[j], s_out=s_hist[j])
+            _lib.call("mjx_pack_np", _device.ptr(s_hist[j]), _lib.MJX_I32, n, _device.ptr(bits),
+                      _device.stream_handle())
+            if T:
+                rollout(self.plan.graph, bits, T, counts=cnt[j:j + 1])
+            else:
+                _lib.call("mjx_popcount_np", _device.ptr(bits), n, _device.ptr(cnt[j:j + 1]),
+                          _device.stream_handle())
+        self.t += k
+        self.s.copy_(s_hist[k - 1])
+        return 2 * cnt.cpu().numpy() - n, s_hist
+
 
 def hpr_run(d, n, p, c, damppar=0.4, attr_value=1, lmbd_in=None, pie=0.3, gamma=0.1, TT=10000, edges=None,
-            nbrs=None, seed=0, dtype=torch.float32, chi0=None, biases0=None, generator=None):
+            nbrs=None, seed=0, dtype=torch.float32, chi0=None, biases0=None, generator=None, batch=16):
     """The HPR experiment of code/HPR_pytorch_RRG.py:224-377 for one graph.
 
     Randomness follows the reference: with ``generator`` a torch CPU generator
@@ -233,13 +264,33 @@ def hpr_run(d, n, p, c, damppar=0.4, attr_value=1, lmbd_in=None, pie=0.3, gamma=
     st.s_from_biases()
     total = st.sum_end()
     m_final = total / n
+    s_dev = st.s
     while m_final < 1:                                     # code/HPR_pytorch_RRG.py:344-356
-        total = st.step(generator=generator)
-        if st.t > TT:
-            m_final = 2
+        if batch and batch > 1:
+            # `batch` iterations per host read; the run stops at the first
+            # iteration the reference would stop at (t > TT, or consensus)
+            t0 = st.t
+            sums, s_hist = st.steps_batched(batch, generator)
+            for j in range(batch):
+                t = t0 + j + 1
+                if t > TT:
+                    m_final = 2
+                elif sums[j] / n >= 1:
+                    m_final = sums[j] / n
+                if m_final >= 1:
+                    st.t = t
+                    s_dev = s_hist[j]
+                    break
+            else:
+                s_dev = st.s
         else:
-            m_final = total / n
-    s = st.s.cpu().numpy()
+            total = st.step(generator=generator)
+            s_dev = st.s
+            if st.t > TT:
+                m_final = 2
+            else:
+                m_final = total / n
+    s = s_dev.cpu().numpy()
     return {
         "mag_reached": np.array([np.sum(s) / n]),
         "num_steps": np.array([float(st.t)]),
