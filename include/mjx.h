@@ -212,17 +212,21 @@ int mjx_hpr_new_biases(int dtype, void* biases, const void* marg, const double* 
 int mjx_sweep_ell_np_range(const int32_t* adj, int64_t n, int d, int64_t row_lo, int64_t row_hi,
                            const uint64_t* s_in, uint64_t* s_out, unsigned long long* counts, void* stream);
 
-/* Source-binned sweep (one replica, huge n): a static plan bins the n_rows*d
- * (destination, source) slots of rows [row_lo, row_hi) by source block (2 MB
- * of state bits, L2-resident) and destination tile (8192 nodes); a sweep
- * streams the plan instead of gathering one random cache line per slot.
- * Same result as mjx_sweep_ell_np_range.  mjx_binned_plan_shape gives the
- * sizes: src int32[slots], off uint16[slots], seg_ptr int64[segments+1],
- * msg uint64[ceil(slots/64)] (per-sweep message bits); work >= 64 MiB.  */
-int mjx_binned_plan_shape(int64_t n, int d, int64_t row_lo, int64_t row_hi, int64_t* slots, int64_t* segments);
+/* Source-binned (propagation-blocking) sweep (one replica, huge n; config C5).
+ * Same result as mjx_sweep_ell_np_range (code/SA_RRG.py:18-20 on the rows
+ * [row_lo, row_hi)); replaces its one-random-cache-line-per-slot gather.  A
+ * static plan bins the (row_hi-row_lo)*d (destination, source) slots by source
+ * block (1M nodes, staged in LDS) and destination tile (64K nodes, LDS byte
+ * counters); a sweep is two streaming kernels (messages, then counts + rule).
+ * mjx_binned_plan_shape fills sizes[5] = {src_len (int32 elements), off_len
+ * (uint16 elements), index_len (int64 elements), msg_words (uint64 per-sweep
+ * message bits), work_bytes (device scratch for mjx_binned_build)}.
+ * Limits: n <= 2^31-1, d <= 16; row_lo a multiple of 64, row_hi too unless
+ * row_hi == n.  adj holds the rows' ELL entries (global node ids).  */
+int mjx_binned_plan_shape(int64_t n, int d, int64_t row_lo, int64_t row_hi, int64_t* sizes);
 int mjx_binned_build(const int32_t* adj, int64_t n, int d, int64_t row_lo, int64_t row_hi, int32_t* src,
-                     uint16_t* off, long long* seg_ptr, void* work, int64_t work_bytes, void* stream);
-int mjx_sweep_binned(const int32_t* src, const uint16_t* off, const long long* seg_ptr, int64_t n, int d,
+                     uint16_t* off, long long* index, void* work, int64_t work_bytes, void* stream);
+int mjx_sweep_binned(const int32_t* src, const uint16_t* off, const long long* index, int64_t n, int d,
                      int64_t row_lo, int64_t row_hi, const uint64_t* s_in, uint64_t* msg, uint64_t* s_out,
                      unsigned long long* counts, void* stream);
 

@@ -296,113 +296,307 @@ extern "C" int mjx_graph_check_ell(const int32_t* adj, int64_t n, int d, unsigne
 }
 
 // ===========================================================================
-// Source-binned sweep of a node-packed state (one replica, huge n: config C5).
+// Source-binned (propagation-blocking) sweep of a node-packed state (one
+// replica, huge n: config C5).
 //
-// The gather sweep reads s[u] for 6e9 random u per sweep at N=1e9, d=6: every
-// 4-byte gather costs a cache line from a 125 MB state that no L2 holds, so it
-// runs at the random line rate.  Here the n*d (destination, source) slots of a
-// rank's rows are binned once (a static plan) by source block b = u >> kSrcShift
-// (2 MB of state bits each, L2-resident) and, inside a block, by destination
-// tile t = (v - lo) >> kTileShift.  A sweep is then
-//   phase 1: stream the slots block by block, read s[u] (an L2 hit: the whole
-//            chip works on one or two source blocks at a time) and write one
-//            message bit per slot, in slot order (coalesced);
-//   phase 2: one workgroup per destination tile gathers its K contiguous
-//            segments (message bits + 16-bit tile offsets), counts +1
-//            neighbours per node in LDS and applies the majority rule
-//            (always-stay ties, code/SA_RRG.py:19-20) against the node's own bit.
-// Traffic per sweep ~ 4 + 2 bytes of static plan and 2/8 bit of messages per
-// slot, all streamed, instead of a random line per slot.
+// The gather sweep reads s[u] for n*d random u per sweep: at N=1e9, d=6 every
+// 4-byte gather costs a whole cache line of a 125 MB state, so it runs at the
+// random line rate (98-109 ms per sweep on one MI355X).  Here the rows*d
+// (destination v, source u) slots of a rank's rows are binned once, in a static
+// plan, by source block b = u >> kSrcShift (1M nodes = 128 KB of state bits,
+// staged in LDS) and destination tile t = (v - lo) >> kTileShift (64K nodes,
+// byte counters in LDS).  Segment (b, t) = the slots with source in block b and
+// destination in tile t.  A sweep is two streaming kernels:
+//   phase 1 (k_bin_msg, workgroups per source block): stage the block's state
+//     bits in LDS, stream the block's source offsets (phase-1 order: b-major,
+//     t inside) and write one message bit per slot;
+//   phase 2 (k_bin_apply, one workgroup per destination tile): for every
+//     segment (b, t) stream its 16-bit destination offsets (phase-2 order:
+//     t-major) and its message bits, count +1 neighbours in LDS, then apply the
+//     majority rule with always-stay ties (code/SA_RRG.py:19-20) against the
+//     node's own bit.
+// Slot i of segment (b, t) is slot i in both orders, so the phases agree
+// without a per-slot index.  Algorithmic traffic per slot: 4 B of source offset
+// + 2 B of destination offset + 2/8 B of message bit (written, read back), all
+// streamed, instead of one random line per slot.
+//
+// Plan (sizes from mjx_binned_plan_shape):
+//   src   int32[src_len]  phase-1 order; block starts padded to 256 slots and
+//                         every 256-slot chunk stored lane-transposed (slot r of
+//                         a chunk at 4*(r&63) + (r>>6)), so one 16-B load per
+//                         lane gives a wave the bits of four whole message words;
+//   off   uint16[off_len] phase-2 order; segment starts padded to 8 slots;
+//   index int64           blk[K+1]  phase-1 padded block starts |
+//                         p1T[S]    phase-1 start of segment (b,t), at t*K+b |
+//                         p2[S+1]   phase-2 padded start of segment (b,t) at
+//                                   t*K+b, its pad count in the low 3 bits.
 // ===========================================================================
 namespace mjx {
 namespace binned {
 
-constexpr int kSrcShift = 24;          // 16M nodes = 2 MB of bits per source block
-constexpr int kTileShift = 13;         // 8192 destinations per tile (32 KB of LDS counters)
-constexpr int kTile = 1 << kTileShift;
+constexpr int kSrcShift = 20;
+constexpr int64_t kSrc = 1ll << kSrcShift;
+constexpr int kSrcWords = (int)(kSrc >> 5);     // uint32 words of one block's state bits (128 KB)
+constexpr int kTileShift = 16;
+constexpr int64_t kTile = 1ll << kTileShift;
+constexpr int kCntWords = (int)(kTile >> 2);    // byte counters, four per LDS word (64 KB)
+constexpr int kMsgThreads = 1024;
+constexpr int kApplyThreads = 1024;
+constexpr int kMsgSplit = 4;                    // phase-1 workgroups per source block
+constexpr int64_t kScanScratch = 64ll << 20;
+constexpr int64_t kMaxBlocks = 16384;           // histogram of blocks in 64 KB of LDS
 
-__host__ __device__ inline int64_t nblocks(int64_t n) { return (n + (1ll << kSrcShift) - 1) >> kSrcShift; }
-__host__ __device__ inline int64_t ntiles(int64_t rows) { return (rows + kTile - 1) >> kTileShift; }
+struct Shape {
+    int64_t K, T, S, slots, src_len, off_len, index_len, msg_words, work_bytes;
+};
 
-// slot counts per (block, tile): one workgroup per tile, LDS histogram over blocks
-__global__ void __launch_bounds__(256) k_bin_count(const int32_t* __restrict__ adj, int64_t rows, int d, int64_t K,
-                                                   int64_t T, long long* __restrict__ cnt) {
+inline int64_t align256(int64_t x) { return (x + 255) & ~255ll; }
+
+inline Shape shape(int64_t n, int d, int64_t rows) {
+    Shape s;
+    s.K = (n + kSrc - 1) >> kSrcShift;
+    s.T = (rows + kTile - 1) >> kTileShift;
+    s.S = s.K * s.T;
+    s.slots = rows * d;
+    s.src_len = s.slots + 256 * s.K;
+    s.off_len = s.slots + 8 * s.S + 8;
+    s.index_len = (s.K + 1) + s.S + (s.S + 1);
+    s.msg_words = s.src_len / 64 + 2;
+    s.work_bytes = align256(4 * s.S) + align256(8 * s.S) + kScanScratch;
+    return s;
+}
+
+__host__ __device__ inline int64_t p1pos(int64_t j) { return (j & ~255ll) | ((j & 63) << 2) | ((j >> 6) & 3); }
+
+// ---- plan construction (setup, once per graph) ------------------------------
+
+// per-tile histogram over source blocks: cntB[b*T+t] (b-major) and the padded
+// count into p2[t*K+b] (t-major, scanned afterwards)
+__global__ void __launch_bounds__(256) k_bin_count(const int32_t* __restrict__ adj, int64_t rows, int d, int64_t n,
+                                                   int64_t K, int64_t T, uint32_t* __restrict__ cntB,
+                                                   long long* __restrict__ p2) {
     extern __shared__ unsigned hist[];
     const int64_t t = blockIdx.x;
     for (int64_t b = threadIdx.x; b < K; b += 256) hist[b] = 0;
     __syncthreads();
-    const int64_t s0 = t * kTile * d, s1 = ((t + 1) * kTile < rows ? (t + 1) * kTile : rows) * d;
-    for (int64_t q = s0 + threadIdx.x; q < s1; q += 256) atomicAdd(&hist[adj[q] >> kSrcShift], 1u);
+    const int64_t r1 = ((t + 1) * kTile < rows) ? (t + 1) * kTile : rows;
+    for (int64_t q = t * kTile * d + threadIdx.x; q < r1 * d; q += 256) {
+        const int32_t u = adj[q];
+        if (u >= 0 && u < n) atomicAdd(&hist[u >> kSrcShift], 1u);
+    }
     __syncthreads();
-    for (int64_t b = threadIdx.x; b < K; b += 256) cnt[b * T + t] = hist[b];
+    for (int64_t b = threadIdx.x; b < K; b += 256) {
+        const unsigned c = hist[b];
+        cntB[b * T + t] = c;
+        p2[t * K + b] = (long long)((c + 7u) & ~7u);
+    }
 }
 
-// place every slot at seg_ptr[b*T + t] + (its rank inside the segment; order
-// inside a segment is free: phase 2 only counts)
-__global__ void __launch_bounds__(256) k_bin_fill(const int32_t* __restrict__ adj, int64_t rows, int d, int64_t K,
-                                                  int64_t T, const long long* __restrict__ seg_ptr,
-                                                  int32_t* __restrict__ src, uint16_t* __restrict__ off) {
+// tag every phase-2 start with its segment's pad count (low 3 bits)
+__global__ void k_bin_tag(const uint32_t* __restrict__ cntB, int64_t K, int64_t T, long long* __restrict__ p2) {
+    const int64_t S = K * T;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < S; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t t = i / K, b = i - t * K;
+        const unsigned c = cntB[b * T + t];
+        p2[i] |= (long long)(((c + 7u) & ~7u) - c);
+    }
+}
+
+// per source block: exclusive scan of its segment sizes over t; padded total
+__global__ void __launch_bounds__(256) k_bin_blockscan(const uint32_t* __restrict__ cntB, int64_t T,
+                                                       long long* __restrict__ p1, long long* __restrict__ blk) {
+    __shared__ long long sh[256];
+    const int64_t b = blockIdx.x;
+    long long carry = 0;
+    for (int64_t t0 = 0; t0 < T; t0 += 256) {
+        const int64_t t = t0 + threadIdx.x;
+        const long long x = (t < T) ? (long long)cntB[b * T + t] : 0;
+        sh[threadIdx.x] = x;
+        __syncthreads();
+        for (int o = 1; o < 256; o <<= 1) {
+            const long long y = (threadIdx.x >= (unsigned)o) ? sh[threadIdx.x - o] : 0;
+            __syncthreads();
+            sh[threadIdx.x] += y;
+            __syncthreads();
+        }
+        if (t < T) p1[b * T + t] = carry + sh[threadIdx.x] - x;
+        carry += sh[255];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) blk[b] = (carry + 255) & ~255ll;
+}
+
+// absolute phase-1 starts (b-major, for the fill) and their t-major copy
+__global__ void k_bin_finish(long long* __restrict__ p1, const long long* __restrict__ blk, int64_t K, int64_t T,
+                             long long* __restrict__ p1T) {
+    const int64_t S = K * T;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < S; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t b = i / T, t = i - b * T;
+        const long long v = p1[i] + blk[b];
+        p1[i] = v;
+        p1T[t * K + b] = v;
+    }
+}
+
+// place every slot: rank r inside segment (b, t) (LDS cursor; any order works
+// as long as both layouts use the same r)
+__global__ void __launch_bounds__(256) k_bin_fill(const int32_t* __restrict__ adj, int64_t rows, int d, int64_t n,
+                                                  int64_t K, int64_t T, const long long* __restrict__ p1,
+                                                  const long long* __restrict__ p2, int32_t* __restrict__ src,
+                                                  uint16_t* __restrict__ off) {
     extern __shared__ unsigned cur[];
     const int64_t t = blockIdx.x;
     for (int64_t b = threadIdx.x; b < K; b += 256) cur[b] = 0;
     __syncthreads();
-    const int64_t s0 = t * kTile * d, s1 = ((t + 1) * kTile < rows ? (t + 1) * kTile : rows) * d;
-    for (int64_t q = s0 + threadIdx.x; q < s1; q += 256) {
+    const int64_t r1 = ((t + 1) * kTile < rows) ? (t + 1) * kTile : rows;
+    for (int64_t q = t * kTile * d + threadIdx.x; q < r1 * d; q += 256) {
         const int32_t u = adj[q];
+        if (u < 0 || u >= n) continue;
         const int64_t b = u >> kSrcShift;
-        const int64_t pos = seg_ptr[b * T + t] + atomicAdd(&cur[b], 1u);
-        src[pos] = u;
-        off[pos] = (uint16_t)((q / d) - t * kTile);
+        const unsigned r = atomicAdd(&cur[b], 1u);
+        src[p1pos(p1[b * T + t] + r)] = (int32_t)(u & (kSrc - 1));
+        off[(p2[t * K + b] & ~7ll) + r] = (uint16_t)(q / d - t * kTile);
     }
 }
 
-// phase 1: message bit of every slot, in plan order
-__global__ void __launch_bounds__(256) k_bin_messages(const int32_t* __restrict__ src, int64_t slots,
-                                                      const uint32_t* __restrict__ s32, u64* __restrict__ msg) {
-    const int lane = threadIdx.x & 63;
-    const int64_t nwords = (slots + 63) >> 6;
-    const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
-    const int64_t nwaves = ((int64_t)gridDim.x * 256) >> 6;
-    for (int64_t w = wave; w < nwords; w += nwaves) {
-        const int64_t e = (w << 6) + lane;
-        bool bit = false;
-        if (e < slots) {
-            const int32_t u = src[e];
-            bit = (s32[u >> 5] >> (u & 31)) & 1u;
-        }
-        const u64 word = __ballot(bit);
-        if (lane == 0) msg[w] = word;
+// ---- the sweep ----------------------------------------------------------------
+
+__device__ __forceinline__ bool state_bit(const uint32_t* sb, int32_t u) {
+    return (sb[(u & (int32_t)(kSrc - 1)) >> 5] >> (u & 31)) & 1u;
+}
+
+// phase 1: message bit of every slot of block b, in phase-1 order
+__global__ void __launch_bounds__(kMsgThreads) k_bin_msg(const int32_t* __restrict__ src,
+                                                         const long long* __restrict__ blk, int64_t n,
+                                                         const uint32_t* __restrict__ s32, u64* __restrict__ msg) {
+    extern __shared__ uint32_t sb[];
+    const int64_t b = blockIdx.x / kMsgSplit;
+    const int part = blockIdx.x % kMsgSplit;
+    const int64_t g0 = b * kSrcWords, nw32 = (n + 31) >> 5;
+    for (int i = threadIdx.x; i < kSrcWords; i += kMsgThreads) {
+        const int64_t g = g0 + i;
+        sb[i] = (g < nw32) ? s32[g] : 0u;
     }
+    __syncthreads();
+    const int64_t c0 = blk[b] >> 8, c1 = blk[b + 1] >> 8;   // 256-slot chunks of this block
+    const int64_t per = (c1 - c0 + kMsgSplit - 1) / kMsgSplit;
+    const int64_t a0 = c0 + part * per;
+    const int64_t a1 = (a0 + per < c1) ? a0 + per : c1;
+    constexpr int NW = kMsgThreads / 64;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int4* src4 = reinterpret_cast<const int4*>(src);
+    for (int64_t c = a0 + wave; c < a1; c += 2 * NW) {
+        const int64_t c2 = c + NW;
+        const bool two = c2 < a1;
+        const int4 x = src4[c * 64 + lane];
+        int4 y = make_int4(0, 0, 0, 0);
+        if (two) y = src4[c2 * 64 + lane];
+        const u64 w0 = __ballot(state_bit(sb, x.x)), w1 = __ballot(state_bit(sb, x.y));
+        const u64 w2 = __ballot(state_bit(sb, x.z)), w3 = __ballot(state_bit(sb, x.w));
+        const u64 w4 = __ballot(state_bit(sb, y.x)), w5 = __ballot(state_bit(sb, y.y));
+        const u64 w6 = __ballot(state_bit(sb, y.z)), w7 = __ballot(state_bit(sb, y.w));
+        u64 mine = (lane & 4) ? ((lane & 2) ? ((lane & 1) ? w7 : w6) : ((lane & 1) ? w5 : w4))
+                              : ((lane & 2) ? ((lane & 1) ? w3 : w2) : ((lane & 1) ? w1 : w0));
+        if (lane < 4) msg[c * 4 + lane] = mine;
+        else if (lane < 8 && two) msg[c2 * 4 + lane - 4] = mine;
+    }
+}
+
+struct Piece {
+    uint4 o;     // eight 16-bit destination offsets
+    unsigned bits;
+};
+
+__device__ __forceinline__ Piece load_piece(const uint16_t* __restrict__ off, const u64* __restrict__ msg,
+                                            long long s1, long long s2, int64_t len, int64_t j) {
+    Piece pc;
+    pc.bits = 0;
+    pc.o = make_uint4(0, 0, 0, 0);
+    if (j < len) {
+        pc.o = *reinterpret_cast<const uint4*>(off + s2 + j);
+        const int64_t p = s1 + j;
+        const u64 lo = msg[p >> 6], hi = msg[(p >> 6) + 1];
+        const int sh = (int)(p & 63);
+        const u64 w = sh ? ((lo >> sh) | (hi << (64 - sh))) : lo;
+        const int64_t nb = len - j;
+        pc.bits = (unsigned)(w & ((nb >= 8) ? 0xffull : ((1ull << nb) - 1)));
+    }
+    return pc;
+}
+
+__device__ __forceinline__ void apply_piece(uint32_t* cnt, const Piece& pc) {
+    const unsigned oo[4] = {pc.o.x, pc.o.y, pc.o.z, pc.o.w};
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        if ((pc.bits >> q) & 1u) {
+            const unsigned v = (oo[q >> 1] >> ((q & 1) * 16)) & 0xffffu;
+            atomicAdd(&cnt[v >> 2], 1u << ((v & 3) << 3));
+        }
+    }
+}
+
+struct Seg {
+    long long s1, s2;
+    int64_t len;
+};
+
+__device__ __forceinline__ Seg seg_of(long long m1, long long m2, long long m2e, int k) {
+    Seg s;
+    s.s1 = __shfl(m1, k);
+    const long long a = __shfl(m2, k), e = __shfl(m2e, k);
+    s.s2 = a & ~7ll;
+    s.len = (e & ~7ll) - s.s2 - (a & 7);
+    return s;
 }
 
 // phase 2: one workgroup per destination tile
-__global__ void __launch_bounds__(256) k_bin_update(const uint16_t* __restrict__ off,
-                                                    const long long* __restrict__ seg_ptr, const u64* __restrict__ msg,
-                                                    int64_t K, int64_t T, int64_t lo, int64_t hi, int d,
-                                                    const uint32_t* __restrict__ s32, u64* __restrict__ s_out,
-                                                    unsigned long long* __restrict__ counts) {
-    __shared__ unsigned cnt[kTile];
-    __shared__ unsigned long long red[4];
+__global__ void __launch_bounds__(kApplyThreads) k_bin_apply(const uint16_t* __restrict__ off,
+                                                             const long long* __restrict__ p1T,
+                                                             const long long* __restrict__ p2,
+                                                             const u64* __restrict__ msg, int64_t K, int64_t lo,
+                                                             int64_t hi, int d, const uint32_t* __restrict__ s32,
+                                                             u64* __restrict__ s_out,
+                                                             unsigned long long* __restrict__ counts) {
+    extern __shared__ uint32_t cnt[];
+    constexpr int NW = kApplyThreads / 64;
+    __shared__ unsigned long long red[NW];
     const int64_t t = blockIdx.x;
-    for (int i = threadIdx.x; i < kTile; i += 256) cnt[i] = 0;
+    for (int i = threadIdx.x; i < kCntWords; i += kApplyThreads) cnt[i] = 0;
     __syncthreads();
-    for (int64_t b = 0; b < K; ++b) {
-        const int64_t e0 = seg_ptr[b * T + t], e1 = seg_ptr[b * T + t + 1];
-        for (int64_t e = e0 + threadIdx.x; e < e1; e += 256) {
-            const unsigned bit = (unsigned)((msg[e >> 6] >> (e & 63)) & 1ull);
-            if (bit) atomicAdd(&cnt[off[e]], 1u);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const long long* q1 = p1T + t * K;
+    const long long* q2 = p2 + t * K;
+    for (int64_t g = (int64_t)wave * 64; g < K; g += NW * 64) {
+        const int64_t mb = g + lane;
+        long long m1 = 0, m2 = 0, m2e = 0;
+        if (mb < K) {
+            m1 = q1[mb];
+            m2 = q2[mb];
+            m2e = q2[mb + 1];
+        }
+        const int ns = (int)((K - g < 64) ? K - g : 64);
+        for (int k = 0; k < ns; k += 2) {
+            const Seg A = seg_of(m1, m2, m2e, k);
+            Seg B = seg_of(m1, m2, m2e, k + 1 < ns ? k + 1 : k);
+            if (k + 1 >= ns) B.len = 0;
+            const Piece pa = load_piece(off, msg, A.s1, A.s2, A.len, 8 * lane);
+            const Piece pb = load_piece(off, msg, B.s1, B.s2, B.len, 8 * lane);
+            apply_piece(cnt, pa);
+            apply_piece(cnt, pb);
+            for (int64_t i = 512; i < A.len; i += 512) apply_piece(cnt, load_piece(off, msg, A.s1, A.s2, A.len, i + 8 * lane));
+            for (int64_t i = 512; i < B.len; i += 512) apply_piece(cnt, load_piece(off, msg, B.s1, B.s2, B.len, i + 8 * lane));
         }
     }
     __syncthreads();
-    const int lane = threadIdx.x & 63;
     const int64_t v0 = lo + t * kTile;
     const int64_t v1 = (v0 + kTile < hi) ? v0 + kTile : hi;
     unsigned long long ones = 0;
-    for (int64_t w = (v0 >> 6) + (threadIdx.x >> 6); w < ((v1 + 63) >> 6); w += 4) {
+    for (int64_t w = (v0 >> 6) + wave; w < ((v1 + 63) >> 6); w += NW) {
         const int64_t v = (w << 6) + lane;
         bool nb = false;
         if (v < v1) {
-            const int c = (int)cnt[v - v0];
+            const int64_t lv = v - v0;
+            const int c = (int)((cnt[lv >> 2] >> ((lv & 3) << 3)) & 0xffu);
             const int own = (s32[v >> 5] >> (v & 31)) & 1u;
             nb = (2 * c > d) || ((2 * c == d) && own);
         }
@@ -413,69 +607,104 @@ __global__ void __launch_bounds__(256) k_bin_update(const uint16_t* __restrict__
         }
     }
     if (counts) {
-        if (lane == 0) red[threadIdx.x >> 6] = ones;
+        if (lane == 0) red[wave] = ones;
         __syncthreads();
         if (threadIdx.x == 0) {
-            const unsigned long long tot = red[0] + red[1] + red[2] + red[3];
+            unsigned long long tot = 0;
+            for (int i = 0; i < NW; ++i) tot += red[i];
             if (tot) atomicAdd(counts, tot);
         }
     }
 }
 
+inline int check_range(int64_t n, int d, int64_t row_lo, int64_t row_hi) {
+    if (n < 1 || d < 1 || d > 16 || row_lo < 0 || row_hi > n || row_lo > row_hi) return MJX_EINVAL;
+    if ((row_lo & 63) || ((row_hi & 63) && row_hi != n)) return MJX_EINVAL;
+    if (n > (int64_t)INT32_MAX) return MJX_ERANGE;
+    if (((n + kSrc - 1) >> kSrcShift) > kMaxBlocks) return MJX_ERANGE;
+    return MJX_OK;
+}
+
 }  // namespace binned
 }  // namespace mjx
 
-extern "C" int mjx_binned_plan_shape(int64_t n, int d, int64_t row_lo, int64_t row_hi, int64_t* slots,
-                                     int64_t* segments) {
+extern "C" int mjx_binned_plan_shape(int64_t n, int d, int64_t row_lo, int64_t row_hi, int64_t* sizes) {
     using namespace mjx::binned;
-    if (n < 1 || d < 1 || d > 16 || row_lo < 0 || row_hi > n || row_lo > row_hi || !slots || !segments)
-        return MJX_EINVAL;
-    if ((row_lo & 63) || ((row_hi & 63) && row_hi != n)) return MJX_EINVAL;
-    *slots = (row_hi - row_lo) * d;
-    *segments = nblocks(n) * ntiles(row_hi - row_lo);
+    if (!sizes) return MJX_EINVAL;
+    const int rc = check_range(n, d, row_lo, row_hi);
+    if (rc) return rc;
+    const Shape s = shape(n, d, row_hi - row_lo);
+    sizes[0] = s.src_len;
+    sizes[1] = s.off_len;
+    sizes[2] = s.index_len;
+    sizes[3] = s.msg_words;
+    sizes[4] = s.work_bytes;
     return MJX_OK;
 }
 
 extern "C" int mjx_binned_build(const int32_t* adj, int64_t n, int d, int64_t row_lo, int64_t row_hi, int32_t* src,
-                                uint16_t* off, long long* seg_ptr, void* work, int64_t work_bytes, void* stream) {
+                                uint16_t* off, long long* index, void* work, int64_t work_bytes, void* stream) {
     using namespace mjx::binned;
-    if (n < 1 || d < 1 || d > 16 || row_lo < 0 || row_hi > n || row_lo > row_hi) return MJX_EINVAL;
-    if ((row_lo & 63) || ((row_hi & 63) && row_hi != n)) return MJX_EINVAL;
-    if (n > (int64_t)INT32_MAX) return MJX_ERANGE;
+    const int rc = check_range(n, d, row_lo, row_hi);
+    if (rc) return rc;
     const int64_t rows = row_hi - row_lo;
     if (rows == 0) return MJX_OK;
-    if (!adj || !src || !off || !seg_ptr || !work) return MJX_EINVAL;
-    const int64_t K = nblocks(n), T = ntiles(rows), S = K * T;
-    if (K * 4 > 64 * 1024) return MJX_ERANGE;
-    hipStream_t st = as_stream(stream);
-    // counts into seg_ptr[0..S), then an in-place exclusive scan -> seg_ptr[0..S]
-    MJX_HIP(hipMemsetAsync(seg_ptr + S, 0, sizeof(long long), st), "bin memset");
-    k_bin_count<<<(unsigned)T, 256, K * sizeof(unsigned), st>>>(adj, rows, d, K, T, seg_ptr);
+    if (!adj || !src || !off || !index || !work) return MJX_EINVAL;
+    const Shape s = shape(n, d, rows);
+    if (work_bytes < s.work_bytes) return MJX_ERANGE;
+    const int64_t K = s.K, T = s.T, S = s.S;
+    uint32_t* cntB = reinterpret_cast<uint32_t*>(work);
+    long long* p1 = reinterpret_cast<long long*>(static_cast<char*>(work) + align256(4 * S));
+    void* scan = static_cast<char*>(work) + align256(4 * S) + align256(8 * S);
+    long long* blk = index;
+    long long* p1T = index + (K + 1);
+    long long* p2 = p1T + S;
+    hipStream_t st = mjx::as_stream(stream);
+    size_t need2 = 0, needk = 0;
+    MJX_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, need2, p2, p2, S + 1, st), "bin scan size");
+    MJX_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, needk, blk, blk, K + 1, st), "bin scan size");
+    if ((int64_t)need2 > kScanScratch || (int64_t)needk > kScanScratch) return MJX_ERANGE;
+    MJX_HIP(hipMemsetAsync(src, 0, sizeof(int32_t) * s.src_len, st), "bin memset src");
+    MJX_HIP(hipMemsetAsync(off, 0, sizeof(uint16_t) * s.off_len, st), "bin memset off");
+    MJX_HIP(hipMemsetAsync(p2 + S, 0, sizeof(long long), st), "bin memset p2");
+    MJX_HIP(hipMemsetAsync(blk + K, 0, sizeof(long long), st), "bin memset blk");
+    k_bin_count<<<(unsigned)T, 256, K * sizeof(unsigned), st>>>(adj, rows, d, n, K, T, cntB, p2);
     MJX_LAUNCH_CHECK("k_bin_count");
-    size_t need = 0;
-    MJX_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, need, seg_ptr, seg_ptr, S + 1, st), "bin scan size");
-    if ((int64_t)need > work_bytes) return MJX_ERANGE;
-    MJX_HIP(hipcub::DeviceScan::ExclusiveSum(work, need, seg_ptr, seg_ptr, S + 1, st), "bin scan");
-    k_bin_fill<<<(unsigned)T, 256, K * sizeof(unsigned), st>>>(adj, rows, d, K, T, seg_ptr, src, off);
+    MJX_HIP(hipcub::DeviceScan::ExclusiveSum(scan, need2, p2, p2, S + 1, st), "bin scan p2");
+    k_bin_tag<<<mjx::grid_for(S), 256, 0, st>>>(cntB, K, T, p2);
+    MJX_LAUNCH_CHECK("k_bin_tag");
+    k_bin_blockscan<<<(unsigned)K, 256, 0, st>>>(cntB, T, p1, blk);
+    MJX_LAUNCH_CHECK("k_bin_blockscan");
+    MJX_HIP(hipcub::DeviceScan::ExclusiveSum(scan, needk, blk, blk, K + 1, st), "bin scan blk");
+    k_bin_finish<<<mjx::grid_for(S), 256, 0, st>>>(p1, blk, K, T, p1T);
+    MJX_LAUNCH_CHECK("k_bin_finish");
+    k_bin_fill<<<(unsigned)T, 256, K * sizeof(unsigned), st>>>(adj, rows, d, n, K, T, p1, p2, src, off);
     MJX_LAUNCH_CHECK("k_bin_fill");
     return MJX_OK;
 }
 
-extern "C" int mjx_sweep_binned(const int32_t* src, const uint16_t* off, const long long* seg_ptr, int64_t n, int d,
+extern "C" int mjx_sweep_binned(const int32_t* src, const uint16_t* off, const long long* index, int64_t n, int d,
                                 int64_t row_lo, int64_t row_hi, const uint64_t* s_in, uint64_t* msg, uint64_t* s_out,
                                 unsigned long long* counts, void* stream) {
     using namespace mjx::binned;
-    if (n < 1 || d < 1 || d > 16 || row_lo < 0 || row_hi > n || row_lo > row_hi) return MJX_EINVAL;
+    const int rc = check_range(n, d, row_lo, row_hi);
+    if (rc) return rc;
     if (row_hi == row_lo) return MJX_OK;
-    if ((row_lo & 63) || ((row_hi & 63) && row_hi != n)) return MJX_EINVAL;
-    if (!src || !off || !seg_ptr || !s_in || !msg || !s_out || s_in == s_out) return MJX_EINVAL;
-    const int64_t rows = row_hi - row_lo, slots = rows * d;
-    const int64_t K = nblocks(n), T = ntiles(rows);
-    hipStream_t st = as_stream(stream);
-    k_bin_messages<<<grid_for(((slots + 63) / 64) * 64), 256, 0, st>>>(src, slots, (const uint32_t*)s_in, (u64*)msg);
-    MJX_LAUNCH_CHECK("k_bin_messages");
-    k_bin_update<<<(unsigned)T, 256, 0, st>>>(off, seg_ptr, (const u64*)msg, K, T, row_lo, row_hi, d,
-                                             (const uint32_t*)s_in, (u64*)s_out, counts);
-    MJX_LAUNCH_CHECK("k_bin_update");
+    if (!src || !off || !index || !s_in || !msg || !s_out || s_in == s_out) return MJX_EINVAL;
+    const Shape s = shape(n, d, row_hi - row_lo);
+    const long long* blk = index;
+    const long long* p1T = index + (s.K + 1);
+    const long long* p2 = p1T + s.S;
+    hipStream_t st = mjx::as_stream(stream);
+    MJX_HIP(hipFuncSetAttribute((const void*)k_bin_msg, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                kSrcWords * (int)sizeof(uint32_t)), "k_bin_msg lds");
+    MJX_HIP(hipFuncSetAttribute((const void*)k_bin_apply, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                kCntWords * (int)sizeof(uint32_t)), "k_bin_apply lds");
+    k_bin_msg<<<(unsigned)(s.K * kMsgSplit), kMsgThreads, kSrcWords * sizeof(uint32_t), st>>>(
+        src, blk, n, (const uint32_t*)s_in, (mjx::u64*)msg);
+    MJX_LAUNCH_CHECK("k_bin_msg");
+    k_bin_apply<<<(unsigned)s.T, kApplyThreads, kCntWords * sizeof(uint32_t), st>>>(
+        off, p1T, p2, (const mjx::u64*)msg, s.K, row_lo, row_hi, d, (const uint32_t*)s_in, (mjx::u64*)s_out, counts);
+    MJX_LAUNCH_CHECK("k_bin_apply");
     return MJX_OK;
 }

@@ -58,6 +58,35 @@ def unpack_host(words, n):
     return 2 * bits.astype(np.int64) - 1
 
 
+class BinnedPlan:
+    """Source-binned sweep plan of the rows [lo, hi) of a d-regular graph
+    (mjx_binned_plan_shape / mjx_binned_build / mjx_sweep_binned): the same
+    words and counts as mjx_sweep_ell_np_range on those rows."""
+
+    def __init__(self, adj_rows, n, d, lo, hi):
+        import ctypes
+        self.n, self.d, self.lo, self.hi = int(n), int(d), int(lo), int(hi)
+        sizes = (ctypes.c_int64 * 5)()
+        _lib.call("mjx_binned_plan_shape", self.n, self.d, self.lo, self.hi, sizes)
+        src_len, off_len, index_len, msg_words, work_bytes = (int(x) for x in sizes)
+        dev = adj_rows.device
+        self.src = torch.empty(max(src_len, 1), dtype=torch.int32, device=dev)
+        self.off = torch.empty(max(off_len, 1), dtype=torch.int16, device=dev)
+        self.index = torch.empty(max(index_len, 1), dtype=torch.int64, device=dev)
+        self.msg = torch.empty(max(msg_words, 1), dtype=torch.int64, device=dev)
+        if self.hi > self.lo:
+            work = torch.empty(work_bytes, dtype=torch.uint8, device=dev)
+            _lib.call("mjx_binned_build", _device.ptr(adj_rows), self.n, self.d, self.lo, self.hi,
+                      _device.ptr(self.src), _device.ptr(self.off), _device.ptr(self.index), _device.ptr(work),
+                      work.numel(), _device.stream_handle())
+            del work
+
+    def sweep(self, s_in, s_out, counts=None):
+        _lib.call("mjx_sweep_binned", _device.ptr(self.src), _device.ptr(self.off), _device.ptr(self.index),
+                  self.n, self.d, self.lo, self.hi, _device.ptr(s_in), _device.ptr(self.msg), _device.ptr(s_out),
+                  _device.ptr(counts) if counts is not None else None, _device.stream_handle())
+
+
 class ShardedRRG:
     """This rank's part of one d-regular graph and the replicated spin state."""
 
@@ -105,29 +134,14 @@ class ShardedRRG:
 
     def _build_binned(self):
         """Static source-binned plan of this rank's rows (mjx_binned_build)."""
-        import ctypes
         r = self.range
         if tuple(self.adj.shape) != (r.hi - r.lo, self.d):
             raise ValueError(f"rank {self.rank} owns rows [{r.lo}, {r.hi}): adjacency must be "
                              f"({r.hi - r.lo}, {self.d}), got {tuple(self.adj.shape)}")
-        slots, segs = ctypes.c_int64(0), ctypes.c_int64(0)
-        _lib.call("mjx_binned_plan_shape", self.n, self.d, r.lo, r.hi, ctypes.byref(slots), ctypes.byref(segs))
-        dev = self.device
-        self.bin_src = torch.empty(max(slots.value, 1), dtype=torch.int32, device=dev)
-        self.bin_off = torch.empty(max(slots.value, 1), dtype=torch.int16, device=dev)
-        self.bin_seg = torch.empty(segs.value + 1, dtype=torch.int64, device=dev)
-        self.bin_msg = torch.empty(max((slots.value + 63) // 64, 1), dtype=torch.int64, device=dev)
-        work = torch.empty(64 << 20, dtype=torch.uint8, device=dev)
-        _lib.call("mjx_binned_build", _device.ptr(self.adj) if self.adj.numel() else None, self.n, self.d, r.lo, r.hi,
-                  _device.ptr(self.bin_src), _device.ptr(self.bin_off), _device.ptr(self.bin_seg), _device.ptr(work),
-                  work.numel(), _device.stream_handle())
-        del work
+        self.plan = BinnedPlan(self.adj, self.n, self.d, r.lo, r.hi)
 
     def _binned_sweep(self, s_in, s_out, counts):
-        r = self.range
-        _lib.call("mjx_sweep_binned", _device.ptr(self.bin_src), _device.ptr(self.bin_off), _device.ptr(self.bin_seg),
-                  self.n, self.d, r.lo, r.hi, _device.ptr(s_in), _device.ptr(self.bin_msg), _device.ptr(s_out),
-                  _device.ptr(counts) if counts is not None else None, _device.stream_handle())
+        self.plan.sweep(s_in, s_out, counts)
 
     def drop_adjacency(self):
         """Free the ELL rows once the binned plan is built (24 GB at C5 on one GPU)."""

@@ -117,10 +117,12 @@ def test_range_sweep_argument_checks(mjx_mod):
     assert lib.mjx_sweep_ell_np_range(None, 1000, 4, 1000, 1000, None, None, None, None) == 0     # empty rank
 
 
-@pytest.mark.parametrize("n,d,world", [(100_000, 6, 1), (100_037 + 1, 3, 3), (40_000_000, 3, 2), (5000, 4, 8)])
+@pytest.mark.parametrize("n,d,world", [(100_000, 6, 1), (100_037 + 1, 3, 3), (40_000_000, 3, 2), (5000, 4, 8),
+                                        (3_000_000, 16, 1), (2_500_002, 5, 4)])
 def test_binned_sweep_equals_gather_sweep(mjx_mod, n, d, world):
-    """The source-binned plan (several 16M-node source blocks at n = 4e7) gives
-    the gather sweep's words and counts for every rank's rows."""
+    """The source-binned plan (several 1M-node source blocks and 64K-node
+    destination tiles from n = 2.5e6 on) gives the gather sweep's words and
+    counts for every rank's rows; d = 16 fills the byte counters to the top."""
     seed = 9
     ranges = [mjx_mod.NodeRange(n, world, r) for r in range(world)]
     lib = mjx_mod.load_library()
@@ -139,19 +141,8 @@ def test_binned_sweep_equals_gather_sweep(mjx_mod, n, d, world):
         assert lib.mjx_sweep_ell_np_range(rows.data_ptr(), n, d, r.lo, r.hi, s_in.data_ptr(), want.data_ptr(),
                                           cw.data_ptr(), st) == 0
         # a plan per rank range, built through the same entry points ShardedRRG uses
-        import ctypes
-        slots, segs = ctypes.c_int64(0), ctypes.c_int64(0)
-        assert lib.mjx_binned_plan_shape(n, d, r.lo, r.hi, ctypes.byref(slots), ctypes.byref(segs)) == 0
-        src = torch.empty(slots.value, dtype=torch.int32, device="cuda")
-        off = torch.empty(slots.value, dtype=torch.int16, device="cuda")
-        seg = torch.empty(segs.value + 1, dtype=torch.int64, device="cuda")
-        msg = torch.empty((slots.value + 63) // 64, dtype=torch.int64, device="cuda")
-        work = torch.empty(64 << 20, dtype=torch.uint8, device="cuda")
-        assert lib.mjx_binned_build(rows.data_ptr(), n, d, r.lo, r.hi, src.data_ptr(), off.data_ptr(), seg.data_ptr(),
-                                    work.data_ptr(), work.numel(), st) == 0
-        assert int(seg[-1].item()) == slots.value
-        assert lib.mjx_sweep_binned(src.data_ptr(), off.data_ptr(), seg.data_ptr(), n, d, r.lo, r.hi,
-                                    s_in.data_ptr(), msg.data_ptr(), got.data_ptr(), cg.data_ptr(), st) == 0
+        plan = mjx_mod.BinnedPlan(rows, n, d, r.lo, r.hi)
+        plan.sweep(s_in, got, cg)
         if sh is not None:
             out = torch.zeros_like(s_in)
             c3 = torch.zeros(1, dtype=torch.int64, device="cuda")
