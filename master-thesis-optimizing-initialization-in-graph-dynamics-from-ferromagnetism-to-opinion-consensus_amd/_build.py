@@ -54,10 +54,19 @@ def build(force=False, verbose=True):
     base = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
             "-Wno-unused-function", "-I", INCLUDE]
     objs, cmds = [], []
+    # a unit is recompiled when its object is older than its source, any csrc
+    # header, include/mjx.h or this script (or always, with force)
+    hdrs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    hdrs += [os.path.join(INCLUDE, "mjx.h"), os.path.abspath(__file__)]
+    newest_hdr = max(os.path.getmtime(p) for p in hdrs if os.path.exists(p))
     for src, extra in UNITS:
         obj = os.path.join(objdir, src.replace(".hip", ".o"))
-        cmds.append(base + extra + ["-c", os.path.join(CSRC, src), "-o", obj])
+        srcp = os.path.join(CSRC, src)
         objs.append(obj)
+        if (not force and os.path.exists(obj)
+                and os.path.getmtime(obj) > max(os.path.getmtime(srcp), newest_hdr)):
+            continue
+        cmds.append(base + extra + ["-c", srcp, "-o", obj])
     # translation units compile in parallel (the HPR instantiation units dominate)
     from concurrent.futures import ThreadPoolExecutor
     jobs = max(1, min(len(cmds), os.cpu_count() or 1, 8))
@@ -67,7 +76,7 @@ def build(force=False, verbose=True):
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
 
-    with ThreadPoolExecutor(jobs) as ex:
+    with ThreadPoolExecutor(max(1, min(jobs, len(cmds)))) as ex:
         list(ex.map(run, cmds))
     tmp = LIB + ".tmp"
     cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs

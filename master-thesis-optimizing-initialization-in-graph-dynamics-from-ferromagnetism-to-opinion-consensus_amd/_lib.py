@@ -51,8 +51,8 @@ SIGNATURES = {
     "mjx_rrg_partner_host": [c_i64, c_int, c_u64, c_i64],
     "mjx_graph_check_ell": [c_vp, c_i64, c_int, c_vp, c_vp],
     "mjx_binned_plan_shape": [c_i64, c_int, c_i64, c_i64, c_vp],
-    "mjx_binned_build": [c_vp, c_i64, c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp],
-    "mjx_sweep_binned": [c_vp, c_vp, c_vp, c_i64, c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "mjx_binned_build": [c_vp, c_i64, c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp],
+    "mjx_sweep_binned": [c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp],
     "mjx_bdcm_lds_bytes": [c_int, c_int, c_int],
     "mjx_bdcm_update_class": [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_int, c_dbl, c_dbl, c_dbl, c_vp,
                               c_vp, c_vp],

@@ -316,15 +316,19 @@ extern "C" int mjx_graph_check_ell(const int32_t* adj, int64_t n, int d, unsigne
 //     majority rule with always-stay ties (code/SA_RRG.py:19-20) against the
 //     node's own bit.
 // Slot i of segment (b, t) is slot i in both orders, so the phases agree
-// without a per-slot index.  Algorithmic traffic per slot: 4 B of source offset
-// + 2 B of destination offset + 2/8 B of message bit (written, read back), all
-// streamed, instead of one random line per slot.
+// without a per-slot index.  Algorithmic traffic per slot: 2.5 B of source
+// offset (20 bits: a 16-bit low part and a 4-bit high part) + 2 B of
+// destination offset + 2/8 B of message bit (written, read back), all streamed,
+// instead of one random line per slot.
 //
 // Plan (sizes from mjx_binned_plan_shape):
-//   src   int32[src_len]  phase-1 order; block starts padded to 256 slots and
-//                         every 256-slot chunk stored lane-transposed (slot r of
-//                         a chunk at 4*(r&63) + (r>>6)), so one 16-B load per
-//                         lane gives a wave the bits of four whole message words;
+//   src_lo uint16[src_len]   phase-1 order; block starts padded to 256 slots
+//                            and every 256-slot chunk stored lane-transposed
+//                            (slot r of chunk c at 256c + 4*(r&63) + (r>>6)), so
+//                            one 8-B load per lane gives a wave the low parts of
+//                            four whole message words;
+//   src_hi uint16[src_len/4] the four high nibbles of lane l of chunk c in
+//                            entry 64c + l (nibble k = slot 64k + l);
 //   off   uint16[off_len] phase-2 order; segment starts padded to 8 slots;
 //   index int64           blk[K+1]  phase-1 padded block starts |
 //                         p1T[S]    phase-1 start of segment (b,t), at t*K+b |
@@ -342,7 +346,7 @@ constexpr int64_t kTile = 1ll << kTileShift;
 constexpr int kCntWords = (int)(kTile >> 2);    // byte counters, four per LDS word (64 KB)
 constexpr int kMsgThreads = 1024;
 constexpr int kApplyThreads = 1024;
-constexpr int kMsgSplit = 4;                    // phase-1 workgroups per source block
+constexpr int kMsgSplitMax = 4;                 // phase-1 workgroups per source block (all rows of n)
 constexpr int64_t kScanScratch = 64ll << 20;
 constexpr int64_t kMaxBlocks = 16384;           // histogram of blocks in 64 KB of LDS
 
@@ -358,11 +362,11 @@ inline Shape shape(int64_t n, int d, int64_t rows) {
     s.T = (rows + kTile - 1) >> kTileShift;
     s.S = s.K * s.T;
     s.slots = rows * d;
-    s.src_len = s.slots + 256 * s.K;
+    s.src_len = ((s.slots + 255) & ~255ll) + 256 * s.K;
     s.off_len = s.slots + 8 * s.S + 8;
     s.index_len = (s.K + 1) + s.S + (s.S + 1);
     s.msg_words = s.src_len / 64 + 2;
-    s.work_bytes = align256(4 * s.S) + align256(8 * s.S) + kScanScratch;
+    s.work_bytes = align256(4 * s.S) + align256(8 * s.S) + kScanScratch + 4 * s.src_len;
     return s;
 }
 
@@ -459,19 +463,41 @@ __global__ void __launch_bounds__(256) k_bin_fill(const int32_t* __restrict__ ad
     }
 }
 
+// int32 source offsets (20 bits) -> 16-bit low parts + 4-bit high parts
+__global__ void k_bin_pack(const int32_t* __restrict__ src32, int64_t chunks, uint16_t* __restrict__ lo,
+                           uint16_t* __restrict__ hi) {
+    const int64_t lanes = chunks * 64;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < lanes; i += (int64_t)gridDim.x * blockDim.x) {
+        const int4 x = reinterpret_cast<const int4*>(src32)[i];
+        uint2 l;
+        l.x = ((unsigned)x.x & 0xffffu) | (((unsigned)x.y & 0xffffu) << 16);
+        l.y = ((unsigned)x.z & 0xffffu) | (((unsigned)x.w & 0xffffu) << 16);
+        reinterpret_cast<uint2*>(lo)[i] = l;
+        hi[i] = (uint16_t)((((unsigned)x.x >> 16) & 15u) | ((((unsigned)x.y >> 16) & 15u) << 4) |
+                           ((((unsigned)x.z >> 16) & 15u) << 8) | ((((unsigned)x.w >> 16) & 15u) << 12));
+    }
+}
+
 // ---- the sweep ----------------------------------------------------------------
 
 __device__ __forceinline__ bool state_bit(const uint32_t* sb, int32_t u) {
     return (sb[(u & (int32_t)(kSrc - 1)) >> 5] >> (u & 31)) & 1u;
 }
 
-// phase 1: message bit of every slot of block b, in phase-1 order
-__global__ void __launch_bounds__(kMsgThreads) k_bin_msg(const int32_t* __restrict__ src,
-                                                         const long long* __restrict__ blk, int64_t n,
+__device__ __forceinline__ int4 unpack_src(uint2 l, unsigned h) {
+    return make_int4((int)((l.x & 0xffffu) | ((h & 15u) << 16)), (int)((l.x >> 16) | (((h >> 4) & 15u) << 16)),
+                     (int)((l.y & 0xffffu) | (((h >> 8) & 15u) << 16)), (int)((l.y >> 16) | (((h >> 12) & 15u) << 16)));
+}
+
+// phase 1: message bit of every slot of block b, in phase-1 order; `split`
+// workgroups share a block (each stages the block's 128 KB of state bits)
+__global__ void __launch_bounds__(kMsgThreads) k_bin_msg(const uint16_t* __restrict__ src_lo,
+                                                         const uint16_t* __restrict__ src_hi,
+                                                         const long long* __restrict__ blk, int64_t n, int split,
                                                          const uint32_t* __restrict__ s32, u64* __restrict__ msg) {
     extern __shared__ uint32_t sb[];
-    const int64_t b = blockIdx.x / kMsgSplit;
-    const int part = blockIdx.x % kMsgSplit;
+    const int64_t b = blockIdx.x / split;
+    const int part = blockIdx.x % split;
     const int64_t g0 = b * kSrcWords, nw32 = (n + 31) >> 5;
     for (int i = threadIdx.x; i < kSrcWords; i += kMsgThreads) {
         const int64_t g = g0 + i;
@@ -479,26 +505,39 @@ __global__ void __launch_bounds__(kMsgThreads) k_bin_msg(const int32_t* __restri
     }
     __syncthreads();
     const int64_t c0 = blk[b] >> 8, c1 = blk[b + 1] >> 8;   // 256-slot chunks of this block
-    const int64_t per = (c1 - c0 + kMsgSplit - 1) / kMsgSplit;
+    const int64_t per = (c1 - c0 + split - 1) / split;
     const int64_t a0 = c0 + part * per;
     const int64_t a1 = (a0 + per < c1) ? a0 + per : c1;
     constexpr int NW = kMsgThreads / 64;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int4* src4 = reinterpret_cast<const int4*>(src);
-    for (int64_t c = a0 + wave; c < a1; c += 2 * NW) {
-        const int64_t c2 = c + NW;
-        const bool two = c2 < a1;
-        const int4 x = src4[c * 64 + lane];
-        int4 y = make_int4(0, 0, 0, 0);
-        if (two) y = src4[c2 * 64 + lane];
-        const u64 w0 = __ballot(state_bit(sb, x.x)), w1 = __ballot(state_bit(sb, x.y));
-        const u64 w2 = __ballot(state_bit(sb, x.z)), w3 = __ballot(state_bit(sb, x.w));
-        const u64 w4 = __ballot(state_bit(sb, y.x)), w5 = __ballot(state_bit(sb, y.y));
-        const u64 w6 = __ballot(state_bit(sb, y.z)), w7 = __ballot(state_bit(sb, y.w));
-        u64 mine = (lane & 4) ? ((lane & 2) ? ((lane & 1) ? w7 : w6) : ((lane & 1) ? w5 : w4))
-                              : ((lane & 2) ? ((lane & 1) ? w3 : w2) : ((lane & 1) ? w1 : w0));
-        if (lane < 4) msg[c * 4 + lane] = mine;
-        else if (lane < 8 && two) msg[c2 * 4 + lane - 4] = mine;
+    const uint2* lo2 = reinterpret_cast<const uint2*>(src_lo);
+    // UC chunks per step: lane 4u+k stores message word k of chunk u
+    constexpr int UC = 4;
+    for (int64_t c = a0 + wave; c < a1; c += UC * NW) {
+        uint2 l[UC];
+        unsigned h[UC];
+#pragma unroll
+        for (int u = 0; u < UC; ++u) {
+            const int64_t cc = c + u * NW;
+            l[u] = make_uint2(0, 0);
+            h[u] = 0;
+            if (cc < a1) {
+                l[u] = lo2[cc * 64 + lane];
+                h[u] = src_hi[cc * 64 + lane];
+            }
+        }
+        u64 mine = 0;
+#pragma unroll
+        for (int u = 0; u < UC; ++u) {
+            const int4 x = unpack_src(l[u], h[u]);
+            const u64 w0 = __ballot(state_bit(sb, x.x)), w1 = __ballot(state_bit(sb, x.y));
+            const u64 w2 = __ballot(state_bit(sb, x.z)), w3 = __ballot(state_bit(sb, x.w));
+            if ((lane >> 2) == u) mine = (lane & 2) ? ((lane & 1) ? w3 : w2) : ((lane & 1) ? w1 : w0);
+        }
+        if (lane < 4 * UC) {
+            const int64_t cc = c + (lane >> 2) * NW;
+            if (cc < a1) msg[cc * 4 + (lane & 3)] = mine;
+        }
     }
 }
 
@@ -540,16 +579,30 @@ struct Seg {
     int64_t len;
 };
 
+// lane k's 64-bit value as a wave-uniform (scalar) value
+__device__ __forceinline__ long long readlane64(long long x, int k) {
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)(x & 0xffffffffll), k);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)((unsigned long long)x >> 32), k);
+    return (long long)(((unsigned long long)hi << 32) | lo);
+}
+
 __device__ __forceinline__ Seg seg_of(long long m1, long long m2, long long m2e, int k) {
     Seg s;
-    s.s1 = __shfl(m1, k);
-    const long long a = __shfl(m2, k), e = __shfl(m2e, k);
+    s.s1 = readlane64(m1, k);
+    const long long a = readlane64(m2, k), e = readlane64(m2e, k);
     s.s2 = a & ~7ll;
     s.len = (e & ~7ll) - s.s2 - (a & 7);
     return s;
 }
 
-// phase 2: one workgroup per destination tile
+// workgroup id -> tile, XCD-contiguous: the first (T % 8) XCDs take one extra tile
+__device__ __forceinline__ int64_t xcd_tile(int64_t bid, int64_t T) {
+    const int64_t x = bid & 7, i = bid >> 3, q = T >> 3, r = T & 7;
+    return x * q + (x < r ? x : r) + i;
+}
+
+// phase 2: one workgroup per destination tile; U segments per step
+template <int U>
 __global__ void __launch_bounds__(kApplyThreads) k_bin_apply(const uint16_t* __restrict__ off,
                                                              const long long* __restrict__ p1T,
                                                              const long long* __restrict__ p2,
@@ -560,31 +613,49 @@ __global__ void __launch_bounds__(kApplyThreads) k_bin_apply(const uint16_t* __r
     extern __shared__ uint32_t cnt[];
     constexpr int NW = kApplyThreads / 64;
     __shared__ unsigned long long red[NW];
-    const int64_t t = blockIdx.x;
+    // XCD-aware order: workgroups are placed round-robin on the 8 XCDs, so XCD x
+    // takes the consecutive tiles [x*T/8, (x+1)*T/8) and the message lines that
+    // neighbouring tiles share (segments (b,t), (b,t+1), ... are adjacent in
+    // phase-1 order) are hit in that XCD's L2
+    const int64_t T = gridDim.x;
+    const int64_t t = xcd_tile(blockIdx.x, T);
     for (int i = threadIdx.x; i < kCntWords; i += kApplyThreads) cnt[i] = 0;
     __syncthreads();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const long long* q1 = p1T + t * K;
     const long long* q2 = p2 + t * K;
-    for (int64_t g = (int64_t)wave * 64; g < K; g += NW * 64) {
-        const int64_t mb = g + lane;
+    // segments interleaved over the waves (wave w takes g + w, g + w + NW, ...):
+    // at every step the workgroup's waves read NW neighbouring segments, one
+    // contiguous stretch of off[] (a wave-private run of 64 segments reads
+    // 16 scattered ~1 KB pieces per step and streams ~25% slower)
+    for (int64_t g = 0; g < K; g += NW * 64) {
+        const int64_t mb = g + (int64_t)lane * NW + wave;
         long long m1 = 0, m2 = 0, m2e = 0;
         if (mb < K) {
             m1 = q1[mb];
             m2 = q2[mb];
             m2e = q2[mb + 1];
         }
-        const int ns = (int)((K - g < 64) ? K - g : 64);
-        for (int k = 0; k < ns; k += 2) {
-            const Seg A = seg_of(m1, m2, m2e, k);
-            Seg B = seg_of(m1, m2, m2e, k + 1 < ns ? k + 1 : k);
-            if (k + 1 >= ns) B.len = 0;
-            const Piece pa = load_piece(off, msg, A.s1, A.s2, A.len, 8 * lane);
-            const Piece pb = load_piece(off, msg, B.s1, B.s2, B.len, 8 * lane);
-            apply_piece(cnt, pa);
-            apply_piece(cnt, pb);
-            for (int64_t i = 512; i < A.len; i += 512) apply_piece(cnt, load_piece(off, msg, A.s1, A.s2, A.len, i + 8 * lane));
-            for (int64_t i = 512; i < B.len; i += 512) apply_piece(cnt, load_piece(off, msg, B.s1, B.s2, B.len, i + 8 * lane));
+        const int64_t left = K - g - wave;   // segments g + wave + NW*l with l < ns
+        const int ns = (left <= 0) ? 0 : (int)((left + NW - 1) / NW < 64 ? (left + NW - 1) / NW : 64);
+        // U segments per step: their first 512-slot pieces are all in flight
+        // before any count lands in LDS
+        for (int k = 0; k < ns; k += U) {
+            Seg sg[U];
+            Piece pc[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                sg[u] = seg_of(m1, m2, m2e, (k + u < ns) ? k + u : k);
+                if (k + u >= ns) sg[u].len = 0;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) pc[u] = load_piece(off, msg, sg[u].s1, sg[u].s2, sg[u].len, 8 * lane);
+#pragma unroll
+            for (int u = 0; u < U; ++u) apply_piece(cnt, pc[u]);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                for (int64_t i = 512; i < sg[u].len; i += 512)
+                    apply_piece(cnt, load_piece(off, msg, sg[u].s1, sg[u].s2, sg[u].len, i + 8 * lane));
         }
     }
     __syncthreads();
@@ -635,27 +706,30 @@ extern "C" int mjx_binned_plan_shape(int64_t n, int d, int64_t row_lo, int64_t r
     if (rc) return rc;
     const Shape s = shape(n, d, row_hi - row_lo);
     sizes[0] = s.src_len;
-    sizes[1] = s.off_len;
-    sizes[2] = s.index_len;
-    sizes[3] = s.msg_words;
-    sizes[4] = s.work_bytes;
+    sizes[1] = s.src_len / 4;
+    sizes[2] = s.off_len;
+    sizes[3] = s.index_len;
+    sizes[4] = s.msg_words;
+    sizes[5] = s.work_bytes;
     return MJX_OK;
 }
 
-extern "C" int mjx_binned_build(const int32_t* adj, int64_t n, int d, int64_t row_lo, int64_t row_hi, int32_t* src,
-                                uint16_t* off, long long* index, void* work, int64_t work_bytes, void* stream) {
+extern "C" int mjx_binned_build(const int32_t* adj, int64_t n, int d, int64_t row_lo, int64_t row_hi,
+                                uint16_t* src_lo, uint16_t* src_hi, uint16_t* off, long long* index, void* work,
+                                int64_t work_bytes, void* stream) {
     using namespace mjx::binned;
     const int rc = check_range(n, d, row_lo, row_hi);
     if (rc) return rc;
     const int64_t rows = row_hi - row_lo;
     if (rows == 0) return MJX_OK;
-    if (!adj || !src || !off || !index || !work) return MJX_EINVAL;
+    if (!adj || !src_lo || !src_hi || !off || !index || !work) return MJX_EINVAL;
     const Shape s = shape(n, d, rows);
     if (work_bytes < s.work_bytes) return MJX_ERANGE;
     const int64_t K = s.K, T = s.T, S = s.S;
     uint32_t* cntB = reinterpret_cast<uint32_t*>(work);
     long long* p1 = reinterpret_cast<long long*>(static_cast<char*>(work) + align256(4 * S));
     void* scan = static_cast<char*>(work) + align256(4 * S) + align256(8 * S);
+    int32_t* src = reinterpret_cast<int32_t*>(static_cast<char*>(scan) + kScanScratch);
     long long* blk = index;
     long long* p1T = index + (K + 1);
     long long* p2 = p1T + S;
@@ -680,17 +754,20 @@ extern "C" int mjx_binned_build(const int32_t* adj, int64_t n, int d, int64_t ro
     MJX_LAUNCH_CHECK("k_bin_finish");
     k_bin_fill<<<(unsigned)T, 256, K * sizeof(unsigned), st>>>(adj, rows, d, n, K, T, p1, p2, src, off);
     MJX_LAUNCH_CHECK("k_bin_fill");
+    k_bin_pack<<<mjx::grid_for(s.src_len / 4), 256, 0, st>>>(src, s.src_len / 256, src_lo, src_hi);
+    MJX_LAUNCH_CHECK("k_bin_pack");
     return MJX_OK;
 }
 
-extern "C" int mjx_sweep_binned(const int32_t* src, const uint16_t* off, const long long* index, int64_t n, int d,
+extern "C" int mjx_sweep_binned(const uint16_t* src_lo, const uint16_t* src_hi, const uint16_t* off,
+                                const long long* index, int64_t n, int d,
                                 int64_t row_lo, int64_t row_hi, const uint64_t* s_in, uint64_t* msg, uint64_t* s_out,
                                 unsigned long long* counts, void* stream) {
     using namespace mjx::binned;
     const int rc = check_range(n, d, row_lo, row_hi);
     if (rc) return rc;
     if (row_hi == row_lo) return MJX_OK;
-    if (!src || !off || !index || !s_in || !msg || !s_out || s_in == s_out) return MJX_EINVAL;
+    if (!src_lo || !src_hi || !off || !index || !s_in || !msg || !s_out || s_in == s_out) return MJX_EINVAL;
     const Shape s = shape(n, d, row_hi - row_lo);
     const long long* blk = index;
     const long long* p1T = index + (s.K + 1);
@@ -698,12 +775,20 @@ extern "C" int mjx_sweep_binned(const int32_t* src, const uint16_t* off, const l
     hipStream_t st = mjx::as_stream(stream);
     MJX_HIP(hipFuncSetAttribute((const void*)k_bin_msg, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 kSrcWords * (int)sizeof(uint32_t)), "k_bin_msg lds");
-    MJX_HIP(hipFuncSetAttribute((const void*)k_bin_apply, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                kCntWords * (int)sizeof(uint32_t)), "k_bin_apply lds");
-    k_bin_msg<<<(unsigned)(s.K * kMsgSplit), kMsgThreads, kSrcWords * sizeof(uint32_t), st>>>(
-        src, blk, n, (const uint32_t*)s_in, (mjx::u64*)msg);
+    // a rank with all rows: 4 workgroups per source block (~4 per CU); with
+    // fewer rows fewer, so that staging the block stays a small share
+    const int64_t rows = row_hi - row_lo;
+    int split = (int)((kMsgSplitMax * rows + n - 1) / n);
+    split = split < 1 ? 1 : (split > kMsgSplitMax ? kMsgSplitMax : split);
+    k_bin_msg<<<(unsigned)(s.K * split), kMsgThreads, kSrcWords * sizeof(uint32_t), st>>>(
+        src_lo, src_hi, blk, n, split, (const uint32_t*)s_in, (mjx::u64*)msg);
     MJX_LAUNCH_CHECK("k_bin_msg");
-    k_bin_apply<<<(unsigned)s.T, kApplyThreads, kCntWords * sizeof(uint32_t), st>>>(
+    // two segments per phase-2 step (measured at N=1e9, d=6: one 8.30 ms per
+    // sweep, two 8.19, four 10.5 -- the LDS counts are not the bound: without
+    // them the sweep takes 7.7 ms)
+    MJX_HIP(hipFuncSetAttribute((const void*)k_bin_apply<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                kCntWords * (int)sizeof(uint32_t)), "k_bin_apply lds");
+    k_bin_apply<2><<<(unsigned)s.T, kApplyThreads, kCntWords * sizeof(uint32_t), st>>>(
         off, p1T, p2, (const mjx::u64*)msg, s.K, row_lo, row_hi, d, (const uint32_t*)s_in, (mjx::u64*)s_out, counts);
     MJX_LAUNCH_CHECK("k_bin_apply");
     return MJX_OK;

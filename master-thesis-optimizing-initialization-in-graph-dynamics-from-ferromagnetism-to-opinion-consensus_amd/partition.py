@@ -66,23 +66,26 @@ class BinnedPlan:
     def __init__(self, adj_rows, n, d, lo, hi):
         import ctypes
         self.n, self.d, self.lo, self.hi = int(n), int(d), int(lo), int(hi)
-        sizes = (ctypes.c_int64 * 5)()
+        sizes = (ctypes.c_int64 * 6)()
         _lib.call("mjx_binned_plan_shape", self.n, self.d, self.lo, self.hi, sizes)
-        src_len, off_len, index_len, msg_words, work_bytes = (int(x) for x in sizes)
+        lo_len, hi_len, off_len, index_len, msg_words, work_bytes = (int(x) for x in sizes)
         dev = adj_rows.device
-        self.src = torch.empty(max(src_len, 1), dtype=torch.int32, device=dev)
+        self.src_lo = torch.empty(max(lo_len, 1), dtype=torch.int16, device=dev)
+        self.src_hi = torch.empty(max(hi_len, 1), dtype=torch.int16, device=dev)
         self.off = torch.empty(max(off_len, 1), dtype=torch.int16, device=dev)
         self.index = torch.empty(max(index_len, 1), dtype=torch.int64, device=dev)
         self.msg = torch.empty(max(msg_words, 1), dtype=torch.int64, device=dev)
         if self.hi > self.lo:
             work = torch.empty(work_bytes, dtype=torch.uint8, device=dev)
             _lib.call("mjx_binned_build", _device.ptr(adj_rows), self.n, self.d, self.lo, self.hi,
-                      _device.ptr(self.src), _device.ptr(self.off), _device.ptr(self.index), _device.ptr(work),
+                      _device.ptr(self.src_lo), _device.ptr(self.src_hi), _device.ptr(self.off),
+                      _device.ptr(self.index), _device.ptr(work),
                       work.numel(), _device.stream_handle())
             del work
 
     def sweep(self, s_in, s_out, counts=None):
-        _lib.call("mjx_sweep_binned", _device.ptr(self.src), _device.ptr(self.off), _device.ptr(self.index),
+        _lib.call("mjx_sweep_binned", _device.ptr(self.src_lo), _device.ptr(self.src_hi), _device.ptr(self.off),
+                  _device.ptr(self.index),
                   self.n, self.d, self.lo, self.hi, _device.ptr(s_in), _device.ptr(self.msg), _device.ptr(s_out),
                   _device.ptr(counts) if counts is not None else None, _device.stream_handle())
 
