@@ -55,6 +55,9 @@ def parse():
     ap.add_argument("--giant-d", type=int, default=6)
     ap.add_argument("--giant-sweeps", type=int, default=10)
     ap.add_argument("--giant-mode", default="binned", choices=["binned", "gather"])
+    ap.add_argument("--giant-pieces", type=int, default=None,
+                    help="node ranges per rank (exchange of piece g overlaps the sweep of g+1); "
+                         "default 1 on one GPU, 2 otherwise")
     ap.add_argument("--no-giant", action="store_true")
     ap.add_argument("--er-n", type=int, default=10_000_000)
     ap.add_argument("--er-deg", type=float, default=5.0)
@@ -257,7 +260,7 @@ def bench_giant(args, rank, world, dist, dev):
     n, d, K = args.giant_n, args.giant_d, args.giant_sweeps
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    sh = mjx.ShardedRRG(d, n, seed=args.seed + 12345, mode=args.giant_mode)
+    sh = mjx.ShardedRRG(d, n, seed=args.seed + 12345, mode=args.giant_mode, pieces=args.giant_pieces)
     sh.drop_adjacency()
     torch.cuda.synchronize()
     gen_s = time.perf_counter() - t0
@@ -287,7 +290,7 @@ def bench_giant(args, rank, world, dist, dev):
         "node_updates_per_s": n * K / el,
         "algorithmic_GBps": n * K * per_update_bytes / el / 1e9,
         "stream_ms_per_sweep": ev_ms / K,
-        "rows_per_rank": sh.range.hi - sh.range.lo,
+        "rows_per_rank": sh.range.rows, "pieces_per_rank": sh.range.npieces,
     }
 
 

@@ -27,18 +27,39 @@ from . import _device, _lib
 
 
 class NodeRange:
-    """Word-aligned node range of ``rank`` among ``world`` ranks: rank r owns
-    words [r*chunk, (r+1)*chunk) of the padded state (chunk*world words)."""
+    """Word-aligned node ranges of ``rank`` among ``world`` ranks.
 
-    def __init__(self, n, world, rank):
-        self.n, self.world, self.rank = int(n), int(world), int(rank)
+    The padded state of words_padded = sub*world*pieces words is cut into
+    world*pieces sub-chunks of ``sub`` words; rank r owns sub-chunk g*world + r
+    for every piece g (``pieces``: list of (w_lo, w_hi, lo, hi)).  Piece g of
+    all ranks is then one contiguous stretch of words, so its exchange is one
+    in-place all-gather, and piece g's exchange overlaps piece g+1's sweep.
+    With pieces=1 rank r owns words [r*chunk, (r+1)*chunk) (lo, hi, w_lo, w_hi)."""
+
+    def __init__(self, n, world, rank, pieces=1):
+        self.n, self.world, self.rank, self.npieces = int(n), int(world), int(rank), int(pieces)
+        if self.npieces < 1:
+            raise ValueError("pieces must be >= 1")
         self.words = (self.n + 63) // 64
-        self.chunk = max(1, -(-self.words // self.world))
-        self.words_padded = self.chunk * self.world
-        self.w_lo = min(self.words, self.rank * self.chunk)
-        self.w_hi = min(self.words, (self.rank + 1) * self.chunk)
-        self.lo = min(self.n, self.w_lo * 64)
-        self.hi = min(self.n, self.w_hi * 64)
+        self.sub = max(1, -(-self.words // (self.world * self.npieces)))
+        self.chunk = self.sub * self.npieces           # words per rank
+        self.words_padded = self.sub * self.world * self.npieces
+        self.pieces = []
+        for g in range(self.npieces):
+            w0 = min(self.words, (g * self.world + self.rank) * self.sub)
+            w1 = min(self.words, (g * self.world + self.rank + 1) * self.sub)
+            self.pieces.append((w0, w1, min(self.n, w0 * 64), min(self.n, w1 * 64)))
+        self.w_lo, self.w_hi, self.lo, self.hi = self.pieces[0]
+        self.rows = sum(p[3] - p[2] for p in self.pieces)
+
+    def piece_words(self, g):
+        """Slice of the padded state that piece g's all-gather fills."""
+        return slice(g * self.world * self.sub, (g + 1) * self.world * self.sub)
+
+    def own_words(self, g):
+        """This rank's sub-chunk of piece g (padded; may extend past the last node)."""
+        w0 = (g * self.world + self.rank) * self.sub
+        return slice(w0, w0 + self.sub)
 
 
 def pack_host(s, words=None):
@@ -91,9 +112,16 @@ class BinnedPlan:
 
 
 class ShardedRRG:
-    """This rank's part of one d-regular graph and the replicated spin state."""
+    """This rank's part of one d-regular graph and the replicated spin state.
 
-    def __init__(self, d, n, seed=0, group=None, adj_rows=None, local_sweep=None, device=None, mode="binned"):
+    ``pieces`` (default 1 on one rank, 2 otherwise): the rank's rows are cut
+    into that many node ranges (NodeRange), each with its own sweep plan; the
+    all-gather of piece g runs on RCCL's stream while piece g+1 is swept.
+    ``local_sweep(s_in, s_out, counts, g)`` may replace the HIP sweep of piece
+    g (CPU tests over gloo)."""
+
+    def __init__(self, d, n, seed=0, group=None, adj_rows=None, local_sweep=None, device=None, mode="binned",
+                 pieces=None):
         import torch.distributed as dist
         self.dist = dist if dist.is_available() and dist.is_initialized() else None
         self.group = group
@@ -101,15 +129,24 @@ class ShardedRRG:
         self.rank = self.dist.get_rank(group) if self.dist else 0
         self.backend = self.dist.get_backend(group) if self.dist else None
         self.d, self.n, self.seed = int(d), int(n), int(seed)
-        self.range = r = NodeRange(n, self.world, self.rank)
+        if pieces is None:
+            pieces = 1 if self.world == 1 else 2
+        self.range = r = NodeRange(n, self.world, self.rank, pieces)
+        if adj_rows is not None and not isinstance(adj_rows, (list, tuple)):
+            adj_rows = [adj_rows]
+        if adj_rows is not None and len(adj_rows) != r.npieces:
+            raise ValueError(f"adj_rows: one array per piece ({r.npieces}), got {len(adj_rows)}")
+        self.plans = None
         if local_sweep is None:
             self.device = _device.require_gpu()
             if adj_rows is None:
                 from .graph import random_regular_rows_device
-                adj_rows = random_regular_rows_device(self.d, self.n, self.seed, r.lo, r.hi)
-            self.adj = _device.to_device(adj_rows, dtype=torch.int32)
+                adj_rows = [random_regular_rows_device(self.d, self.n, self.seed, lo, hi)
+                            for (_, _, lo, hi) in r.pieces]
+            self.adj = [_device.to_device(a, dtype=torch.int32) for a in adj_rows]
+            self._check_adj()
             if mode == "binned":
-                self._build_binned()
+                self.plans = [BinnedPlan(a, self.n, self.d, lo, hi) for a, (_, _, lo, hi) in zip(self.adj, r.pieces)]
                 self.local_sweep = self._binned_sweep
             elif mode == "gather":
                 self.local_sweep = self._hip_sweep
@@ -119,50 +156,55 @@ class ShardedRRG:
         else:
             self.device = torch.device("cpu") if device is None else device
             self.adj = adj_rows
+            if self.adj is not None:
+                self._check_adj()
             self.local_sweep = local_sweep
             self.mode = "custom"
-        if self.adj is not None and tuple(self.adj.shape) != (r.hi - r.lo, self.d):  # checked before the plan
-            raise ValueError(f"rank {self.rank} owns rows [{r.lo}, {r.hi}): adjacency must be "
-                             f"({r.hi - r.lo}, {self.d}), got {tuple(self.adj.shape)}")
         self.buf = [torch.zeros(r.words_padded, dtype=torch.int64, device=self.device) for _ in range(2)]
         self.cnt = torch.zeros(1, dtype=torch.int64, device=self.device)
         self.cur = 0
 
+    def _check_adj(self):
+        for a, (_, _, lo, hi) in zip(self.adj, self.range.pieces):
+            if tuple(a.shape) != (hi - lo, self.d):
+                raise ValueError(f"rank {self.rank} owns rows [{lo}, {hi}): adjacency must be "
+                                 f"({hi - lo}, {self.d}), got {tuple(a.shape)}")
+
+    @property
+    def plan(self):
+        """The sweep plan of the first piece (the only one when pieces == 1)."""
+        return self.plans[0] if self.plans else None
+
     # -- one rank's rows ------------------------------------------------------
-    def _hip_sweep(self, s_in, s_out, counts):
-        r = self.range
-        _lib.call("mjx_sweep_ell_np_range", _device.ptr(self.adj) if self.adj.numel() else None, self.n, self.d,
-                  r.lo, r.hi, _device.ptr(s_in), _device.ptr(s_out),
+    def _hip_sweep(self, s_in, s_out, counts, g=0):
+        _, _, lo, hi = self.range.pieces[g]
+        a = self.adj[g]
+        _lib.call("mjx_sweep_ell_np_range", _device.ptr(a) if a.numel() else None, self.n, self.d,
+                  lo, hi, _device.ptr(s_in), _device.ptr(s_out),
                   _device.ptr(counts) if counts is not None else None, _device.stream_handle())
 
-    def _build_binned(self):
-        """Static source-binned plan of this rank's rows (mjx_binned_build)."""
-        r = self.range
-        if tuple(self.adj.shape) != (r.hi - r.lo, self.d):
-            raise ValueError(f"rank {self.rank} owns rows [{r.lo}, {r.hi}): adjacency must be "
-                             f"({r.hi - r.lo}, {self.d}), got {tuple(self.adj.shape)}")
-        self.plan = BinnedPlan(self.adj, self.n, self.d, r.lo, r.hi)
-
-    def _binned_sweep(self, s_in, s_out, counts):
-        self.plan.sweep(s_in, s_out, counts)
+    def _binned_sweep(self, s_in, s_out, counts, g=0):
+        self.plans[g].sweep(s_in, s_out, counts)
 
     def drop_adjacency(self):
-        """Free the ELL rows once the binned plan is built (24 GB at C5 on one GPU)."""
+        """Free the ELL rows once the binned plans are built (24 GB at C5 on one GPU)."""
         if self.mode == "binned":
             self.adj = None
 
-    def exchange(self, buf):
-        """All-gather every rank's word slice into the replicated state (in place)."""
+    def exchange(self, buf, g=0):
+        """All-gather piece g of every rank into the replicated state (in place).
+        Returns the pending RCCL work (or None): the caller waits on it before
+        the state is read again."""
         if self.world == 1:
-            return
+            return None
         r = self.range
-        mine = buf[self.rank * r.chunk:(self.rank + 1) * r.chunk]
+        whole, mine = buf[r.piece_words(g)], buf[r.own_words(g)]
         if self.backend == "nccl":
-            self.dist.all_gather_into_tensor(buf, mine, group=self.group)
-        else:
-            parts = [torch.empty_like(mine) for _ in range(self.world)]
-            self.dist.all_gather(parts, mine.clone(), group=self.group)
-            buf.view(self.world, r.chunk).copy_(torch.stack(parts))
+            return self.dist.all_gather_into_tensor(whole, mine, group=self.group, async_op=True)
+        parts = [torch.empty_like(mine) for _ in range(self.world)]
+        self.dist.all_gather(parts, mine.clone(), group=self.group)
+        whole.view(self.world, r.sub).copy_(torch.stack(parts))
+        return None
 
     # -- state ------------------------------------------------------------------
     @property
@@ -189,8 +231,13 @@ class ShardedRRG:
         src, dst = self.buf[self.cur], self.buf[1 - self.cur]
         if count:
             self.cnt.zero_()
-        self.local_sweep(src, dst, self.cnt if count else None)
-        self.exchange(dst)
+        pending = []
+        for g in range(self.range.npieces):
+            self.local_sweep(src, dst, self.cnt if count else None, g)
+            pending.append(self.exchange(dst, g))
+        for w in pending:        # the next sweep reads the whole state
+            if w is not None:
+                w.wait()
         self.cur = 1 - self.cur
 
     def total_plus(self):

@@ -97,9 +97,10 @@ def test_partitioned_sweeps_equal_single_gpu(mjx_mod, world):
     assert np.array_equal(mjx_mod.unpack(cur[:want_bits.numel()], n).cpu().numpy(), want)
 
 
-def test_sharded_rrg_single_rank(mjx_mod):
+@pytest.mark.parametrize("mode,pieces", [("binned", 1), ("binned", 3), ("gather", 1), ("gather", 4)])
+def test_sharded_rrg_single_rank(mjx_mod, mode, pieces):
     n, d = 50_000, 6
-    sh = mjx_mod.ShardedRRG(d, n, seed=3)
+    sh = mjx_mod.ShardedRRG(d, n, seed=3, mode=mode, pieces=pieces)
     g = mjx_mod.random_regular_graph_device(d, n, seed=3)
     s0 = 2 * np.random.default_rng(1).integers(0, 2, n).astype(np.int64) - 1
     sh.set_state(s0)

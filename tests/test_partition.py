@@ -21,7 +21,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, n, d, steps, s0, adj, out):
+def _worker(rank, world, port, n, d, steps, s0, adj, out, pieces):
     import sys
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -29,17 +29,19 @@ def _worker(rank, world, port, n, d, steps, s0, adj, out):
     try:
         import mjx
         from oracle import majority as orc
-        r = mjx.NodeRange(n, world, rank)
+        r = mjx.NodeRange(n, world, rank, pieces)
 
-        def local_sweep(s_in, s_out, counts):
+        def local_sweep(s_in, s_out, counts, g):
+            w_lo, w_hi, lo, hi = r.pieces[g]
             spins = mjx.unpack_host(s_in.numpy(), n)
-            new = orc.onestep_majority(adj, spins)[r.lo:r.hi]
-            words = mjx.pack_host(new, r.w_hi - r.w_lo)
-            s_out[r.w_lo:r.w_hi] = torch.from_numpy(words)
+            new = orc.onestep_majority(adj, spins)[lo:hi]
+            words = mjx.pack_host(new, w_hi - w_lo)
+            s_out[w_lo:w_hi] = torch.from_numpy(words)
             if counts is not None:
                 counts += int((new > 0).sum())
 
-        sh = mjx.ShardedRRG(d, n, adj_rows=torch.from_numpy(adj[r.lo:r.hi]), local_sweep=local_sweep)
+        rows = [torch.from_numpy(adj[lo:hi]) for (_, _, lo, hi) in r.pieces]
+        sh = mjx.ShardedRRG(d, n, adj_rows=rows, local_sweep=local_sweep, pieces=pieces)
         sh.set_state(s0)
         tot = sh.rollout(steps)
         out[rank] = (sh.state(), tot)
@@ -47,8 +49,10 @@ def _worker(rank, world, port, n, d, steps, s0, adj, out):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n,d,steps", [(2, 1000, 4, 3), (3, 778, 3, 2), (2, 64, 6, 1), (3, 130, 4, 4)])
-def test_sharded_rollout_matches_oracle(world, n, d, steps, mjx_mod):
+@pytest.mark.parametrize("world,n,d,steps,pieces", [(2, 1000, 4, 3, 1), (3, 778, 3, 2, 1), (2, 64, 6, 1, 1),
+                                                    (3, 130, 4, 4, 1), (2, 5000, 4, 3, 4), (3, 2000, 3, 2, 3),
+                                                    (2, 300, 6, 2, 4)])
+def test_sharded_rollout_matches_oracle(world, n, d, steps, pieces, mjx_mod):
     from oracle import majority as orc
     adj = mjx_mod.random_regular_graph(d, n, seed=world * 100 + n)
     s0 = 2 * np.random.default_rng(n).integers(0, 2, n).astype(np.int64) - 1
@@ -56,7 +60,7 @@ def test_sharded_rollout_matches_oracle(world, n, d, steps, mjx_mod):
     port = _free_port()
     with mp.Manager() as mgr:
         out = mgr.dict()
-        mp.spawn(_worker, args=(world, port, n, d, steps, s0, adj, out), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, port, n, d, steps, s0, adj, out, pieces), nprocs=world, join=True)
         res = dict(out)
     for rank in range(world):
         state, tot = res[rank]
@@ -73,6 +77,20 @@ def test_node_range_covers_every_node(mjx_mod):
                 assert a.hi == b.lo
             assert all((r.lo % 64 == 0 or r.lo == n) and (r.hi % 64 == 0 or r.hi == n) for r in rs)
             assert all(r.words_padded == rs[0].chunk * world for r in rs)
+    # several pieces per rank: every word owned exactly once, pieces contiguous across ranks
+    for n in (1, 65, 1000, 10 ** 6 + 3):
+        for world in (1, 2, 3, 8):
+            for pieces in (2, 3, 4):
+                rs = [mjx_mod.NodeRange(n, world, r, pieces) for r in range(world)]
+                owned = np.zeros(rs[0].words_padded, dtype=np.int64)
+                for r in rs:
+                    for g, (w0, w1, lo, hi) in enumerate(r.pieces):
+                        owned[w0:w1] += 1
+                        assert lo == min(n, 64 * w0) and hi == min(n, 64 * w1)
+                        sl = r.own_words(g)
+                        assert sl.start >= r.piece_words(g).start and sl.stop <= r.piece_words(g).stop
+                assert np.all(owned[:rs[0].words] == 1) and np.all(owned[rs[0].words:] == 0)
+                assert sum(r.rows for r in rs) == n
 
 
 def test_pack_host_roundtrip(mjx_mod):
