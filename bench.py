@@ -64,6 +64,9 @@ def parse():
     ap.add_argument("--er-replicas", type=int, default=4096)
     ap.add_argument("--er-steps", type=int, default=5)
     ap.add_argument("--no-er", action="store_true")
+    ap.add_argument("--hpr-n", type=int, default=100_000)
+    ap.add_argument("--hpr-iters", type=int, default=10)
+    ap.add_argument("--no-hpr", action="store_true")
     ap.add_argument("--bdcm-iters", type=int, default=100)
     ap.add_argument("--no-bdcm", action="store_true")
     return ap.parse_args()
@@ -175,9 +178,10 @@ def bench_er(args, rank, world, dist, dev):
     import mjx
     n, R, K = args.er_n, args.er_replicas, args.er_steps
     W = (R + 63) // 64
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
-    rp, col = mjx.erdos_renyi(n, args.er_deg / (n - 1), seed=args.seed + 31 + 1000 * rank)
-    g = mjx.Graph.csr(rp, col)
+    g = mjx.erdos_renyi_device(n, args.er_deg / (n - 1), seed=args.seed + 31 + 1000 * rank)
+    torch.cuda.synchronize()
     gen_s = time.perf_counter() - t0
     gen = torch.Generator(device=dev).manual_seed(args.seed + 5 + rank)
     s0 = torch.randint(-2 ** 62, 2 ** 62, (n * W,), dtype=torch.int64, device=dev, generator=gen)
@@ -191,7 +195,7 @@ def bench_er(args, rank, world, dist, dev):
 
     step()
     el = _timed(lambda: [step() for _ in range(K)], dist, dev)
-    nnz = int(rp[-1])
+    nnz = g.nnz
     dbar = nnz / n
     bytes_per_sweep = 4 * nnz + 8 * (n + 1) + (W * 8) * n * (dbar + 2)
     # sanity: an all-(+1) state is a fixed point of every node (isolated ones included)
@@ -200,10 +204,11 @@ def bench_er(args, rank, world, dist, dev):
     assert torch.equal(mjx.rollout(g, ones, T, words=W, counts=ck), ones) and bool((ck == n).all())
     del s0, out, tmp, ones
     return {
-        "config": f"configs[3]: ER mean degree {args.er_deg:g} N={n} (CSR, own instance per GPU), {R} bit-packed "
+        "config": f"configs[3]: ER mean degree {args.er_deg:g} N={n} (CSR generated on the device, own instance "
+                  f"per GPU), {R} bit-packed "
                   f"replicas per GPU, {T} sweeps + fused count per step",
         "scaling": "weak", "ranks": world, "n": n, "nnz": nnz, "replicas_per_gpu": R, "steps": K,
-        "host_graph_s": gen_s,
+        "device_graph_s": gen_s,
         "ms_per_step": 1e3 * el / K,
         "node_updates_per_s": world * n * R * T * K / el,
         "algorithmic_GBps_per_gpu": bytes_per_sweep * T * K / el / 1e9,
@@ -248,6 +253,76 @@ def bench_bdcm(args, rank, world, dist, dev):
             reps += 1
         res["cpu_ms_per_iter"] = 1e3 * (time.perf_counter() - t0) / reps
         res["cpu_kind"] = "port (oracle/bdcm.py numpy restatement, 1 core)"
+    return res
+
+
+def bench_hpr(args, rank, world, dist, dev):
+    """configs[2]: HPR on a d=4 RRG with N=1e5, p=2, c=2, fp32 edge messages
+    (code/HPR_pytorch_RRG.py:342-362): one iteration = HPr_dp (the message
+    update, dominant) + marginals_comp, timed with HIP events; each rank its own
+    graph (replicas only).  The numpy float64 restatement of HPr_dp
+    (oracle/hpr.py, the reference's dtype) is timed beside it on a bounded
+    sample of output rows of the same graph, one host core."""
+    import torch
+    import mjx
+    n, d, p, c = args.hpr_n, 4, 2, 2
+    edges = mjx.random_regular_edges(d, n, seed=args.seed + 31 + rank)
+    plan = mjx.HPRPlan(edges, n, d)
+    nc = plan.num_combs(p, c)
+    gen = torch.Generator(device=dev).manual_seed(args.seed + rank)
+    chi = torch.rand((2 * plan.E, nc), dtype=torch.float32, device=dev, generator=gen)
+    chi /= chi.sum(1, keepdim=True)
+    b = torch.rand((n, 2), dtype=torch.float32, device=dev, generator=gen)
+    b /= b.sum(1, keepdim=True)
+    out = torch.empty_like(chi)
+    z = torch.empty(4 * plan.E, dtype=chi.dtype, device=dev)
+    mg = torch.empty((n, 2), dtype=chi.dtype, device=dev)
+    lmbd = 25 * n
+    K = args.hpr_iters
+    stream = torch.cuda.current_stream()
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+
+    def run():
+        e[0].record(stream)
+        for _ in range(K):
+            mjx.HPr_dp(chi, b, plan, p, c, 1, lmbd, 0.4, out=out)
+        e[1].record(stream)
+        for _ in range(K):
+            mjx.marginals_comp(out, plan, p, c, zwork=z, out=mg)
+        e[2].record(stream)
+
+    run()
+    el = _timed(run, dist, dev)
+    upd_ms = e[0].elapsed_time(e[1]) / K
+    marg_ms = e[1].elapsed_time(e[2]) / K
+    msgs = 2 * plan.E
+    # per message update: d-1 incoming rows + its own row (damping) read, one row written
+    bytes_per_iter = msgs * (d + 1) * nc * 4
+    res = {"config": f"configs[2]: HPR d={d} RRG N={n}, p={p} c={c} ({nc} columns), fp32 messages, "
+                     "one iteration = HPr_dp + marginals_comp",
+           "scaling": "weak", "ranks": world, "messages": msgs,
+           "ms_per_iter": 1e3 * el / K, "iters_per_s": world * K / el,
+           "hpr_dp_ms": upd_ms, "marginals_ms": marg_ms,
+           "messages_per_s": world * msgs * K / el,
+           "hpr_dp_algorithmic_GBps": bytes_per_iter / (upd_ms / 1e3) / 1e9,
+           "hpr_dp_bytes_per_iter": bytes_per_iter}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import hpr as ohpr
+        inr, src = ohpr.incoming_rows(plan.edges, plan.nbrs_host)
+        chi_h = chi.double().cpu().numpy()
+        b_h = b.double().cpu().numpy()
+        rows = np.random.default_rng(0).choice(msgs, size=256, replace=False)
+        t0 = time.perf_counter()
+        done = 0
+        while time.perf_counter() - t0 < 4.0:
+            ohpr.HPr_dp(chi_h, b_h, inr, src, n, d, p, c, 1, lmbd, 0.4, rows=rows)
+            done += rows.size
+        cpu_s = time.perf_counter() - t0
+        res["cpu_baseline"] = {"messages_per_s": done / cpu_s, "cores": 1, "kind": "port",
+                               "sample": f"oracle/hpr.py HPr_dp (numpy float64, code/HPR_pytorch_RRG.py:183-218) "
+                                         f"on {rows.size} sampled output rows of the same graph, repeated "
+                                         f"for {cpu_s:.1f} s",
+                               "ms_per_iter_equiv": 1e3 * msgs / (done / cpu_s)}
     return res
 
 
@@ -393,6 +468,10 @@ def main():
     if not args.no_er and args.er_n > 0:
         er = bench_er(args, rank, world, dist, dev)
         torch.cuda.empty_cache()
+    hpr = None
+    if not args.no_hpr and args.hpr_iters > 0:
+        hpr = bench_hpr(args, rank, world, dist, dev)
+        torch.cuda.empty_cache()
     bdcm = None
     if not args.no_bdcm and args.bdcm_iters > 0:
         bdcm = bench_bdcm(args, rank, world, dist, dev)
@@ -434,6 +513,7 @@ def main():
             "cpu_baseline": cpu,
             "sa": sa_res,
             "er": er,
+            "hpr": hpr,
             "bdcm": bdcm,
             "giant": giant,
         }

@@ -231,6 +231,22 @@ int mjx_sweep_binned(const uint16_t* src_lo, const uint16_t* src_hi, const uint1
                      int64_t row_lo, int64_t row_hi, const uint64_t* s_in, uint64_t* msg, uint64_t* s_out,
                      unsigned long long* counts, void* stream);
 
+/* Device Erdos-Renyi G(n, p) into CSR, replacing
+ * nx.erdos_renyi_graph + isolate removal + relabelling of
+ * code/ER_BDCM_entropy.ipynb (cell 'ER graph', nb:278-291) with
+ * distributional parity: each pair i < j is an edge with probability p
+ * (geometric skipping per row, counter-based uniforms of (seed, row, k)).
+ * Rows are sorted; the result depends on (n, p, seed) only.  With
+ * drop_isolated the degree-0 nodes are removed and the rest relabelled in
+ * increasing order (nb:283-291).  row_ptr: int64[n+1] (the first *n_out + 1
+ * entries are written), col: int32[col_cap]; *n_out = rows kept, *nnz_out =
+ * 2 * edges.  If col_cap < *nnz_out the call returns MJX_ERANGE after setting
+ * both (retry with a larger col).  work: mjx_er_work_bytes(n) bytes of device
+ * scratch.  Setup call: synchronises `stream`.  n <= 2^31 - 2, 0 <= p < 1.  */
+int64_t mjx_er_work_bytes(int64_t n);
+int mjx_er_generate(int64_t n, double p, uint64_t seed, int drop_isolated, long long* row_ptr, int32_t* col,
+                    int64_t col_cap, int64_t* n_out, int64_t* nnz_out, void* work, int64_t work_bytes, void* stream);
+
 /* ---- device graph generation ----------------------- */
 /* Random simple d-regular graph (configuration model through a keyed
  * pseudorandom stub permutation, then deterministic double-edge switches that

@@ -9,7 +9,7 @@ from . import _lib
 from ._lib import MjxError, lib_path
 from .graph import (Graph, neighbours, csr_from_networkx, random_regular_graph, random_regular_edges,
                     erdos_renyi, erdos_renyi_edges, csr_from_edges, remove_isolated,
-                    random_regular_rows_device, random_regular_graph_device, check_ell)
+                    random_regular_rows_device, random_regular_graph_device, erdos_renyi_device, check_ell)
 from .partition import BinnedPlan, NodeRange, ShardedRRG, pack_host, unpack_host
 from .npz import save_sa_npz, save_hpr_npz, save_bdcm_npz, sa_arrays, hpr_arrays
 from .dynamics import onestep_majority, s_endstate, m, pack, unpack, rollout, popcount, as_graph
@@ -20,7 +20,7 @@ from .bdcm import (BDCMPlan, bdcm_er_plan, BDCM_ER, bdcm_leaf_reset, Zij, Zi_ER,
 
 __all__ = [
     "MjxError", "lib_path", "BinnedPlan", "Graph", "neighbours", "csr_from_networkx", "random_regular_graph",
-    "random_regular_edges", "erdos_renyi", "erdos_renyi_edges", "csr_from_edges", "remove_isolated",
+    "random_regular_edges", "erdos_renyi", "erdos_renyi_device", "erdos_renyi_edges", "csr_from_edges", "remove_isolated",
     "onestep_majority", "s_endstate", "m", "pack", "unpack", "rollout", "popcount", "as_graph",
     "SAReplicas", "E_delta", "sa_run", "schedule_constants",
     "HPRPlan", "HPRState", "HPr_dp", "marginals_comp", "new_biases_i", "hpr_run",

@@ -50,6 +50,8 @@ SIGNATURES = {
     "mjx_rrg_generate": [c_i64, c_int, c_u64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp],
     "mjx_rrg_partner_host": [c_i64, c_int, c_u64, c_i64],
     "mjx_graph_check_ell": [c_vp, c_i64, c_int, c_vp, c_vp],
+    "mjx_er_work_bytes": [c_i64],
+    "mjx_er_generate": [c_i64, c_dbl, c_u64, c_int, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp],
     "mjx_binned_plan_shape": [c_i64, c_int, c_i64, c_i64, c_vp],
     "mjx_binned_build": [c_vp, c_i64, c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp],
     "mjx_sweep_binned": [c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp],
@@ -62,7 +64,7 @@ SIGNATURES = {
 }
 _RESTYPES = {"mjx_strerror": ctypes.c_char_p, "mjx_last_hip_error": ctypes.c_char_p,
              "mjx_sa_lightcone_lds": c_i64, "mjx_bdcm_lds_bytes": c_i64,
-             "mjx_rrg_partner_host": c_i64}
+             "mjx_rrg_partner_host": c_i64, "mjx_er_work_bytes": c_i64}
 
 MJX_I8, MJX_I32, MJX_I64 = 1, 4, 8
 MJX_F32, MJX_F64 = 104, 108

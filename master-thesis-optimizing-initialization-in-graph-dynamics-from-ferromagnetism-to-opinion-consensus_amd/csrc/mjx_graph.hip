@@ -793,3 +793,186 @@ extern "C" int mjx_sweep_binned(const uint16_t* src_lo, const uint16_t* src_hi, 
     MJX_LAUNCH_CHECK("k_bin_apply");
     return MJX_OK;
 }
+
+// ===========================================================================
+// Device Erdos-Renyi G(n, p) generator into CSR.
+//
+// The notebook draws nx.erdos_renyi_graph(n, p) (code/ER_BDCM_entropy.ipynb,
+// cell 'ER graph', nb:278-282), removes isolated nodes and relabels the rest in
+// increasing order (nb:283-291); its dense adj_matrix (nb:294) is O(n^2) and
+// makes n = 1e7 (config C4) impossible.  Parity with networkx is
+// distributional: every pair (i, j), i < j, is an edge independently with
+// probability p.  Row i's upper pairs (i, j > i) are drawn by geometric
+// skipping, j <- j + 1 + floor(log(u) / log(1 - p)), with the k-th uniform u
+// of row i a counter-based hash of (seed, i, k): rows are independent, so the
+// count pass and the fill pass regenerate the same pairs.
+//   k_er_count: upper-pair count per row, degree histogram (atomics);
+//   (drop isolated: keep = deg > 0, new id = exclusive scan of keep);
+//   row_ptr = exclusive scan of the kept degrees;
+//   k_er_fill:  the upper neighbours of row i are the last up[i] entries of
+//               row i in ascending order; row i is also a lower neighbour of
+//               each of them, placed through a per-row cursor;
+//   k_er_sort:  each row's lower part is sorted, so the CSR (rows ascending)
+//               depends on the seed only.
+// Setup call: synchronises `stream` once to read the edge count.
+// ===========================================================================
+namespace mjx {
+namespace er {
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+// k-th uniform of row i, in (0, 1]
+__device__ __forceinline__ double uniform(uint64_t seed, int64_t i, int64_t k) {
+    const uint64_t h = mix64(mix64(seed ^ 0x9e3779b97f4a7c15ull) + mix64((uint64_t)i * 0x100000001b3ull + (uint64_t)k));
+    return ((double)(h >> 11) + 1.0) * 0x1.0p-53;
+}
+
+// visits the upper neighbours j > i of row i, ascending
+template <class F>
+__device__ __forceinline__ void row_pairs(uint64_t seed, int64_t i, int64_t n, double lq, F&& f) {
+    if (lq == 0.0) return;                          // p = 0
+    int64_t j = i;
+    for (int64_t k = 0;; ++k) {
+        const double g = floor(log(uniform(seed, i, k)) / lq);
+        if (!(g < (double)(n - 1 - j))) break;      // also catches +inf
+        j += 1 + (int64_t)g;
+        f(j);
+    }
+}
+
+__global__ void k_er_count(int64_t n, double lq, uint64_t seed, int* __restrict__ up, int* __restrict__ deg) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        int c = 0;
+        row_pairs(seed, i, n, lq, [&](int64_t j) {
+            ++c;
+            atomicAdd(&deg[j], 1);
+        });
+        up[i] = c;
+        if (c) atomicAdd(&deg[i], c);
+    }
+}
+
+// keep flag (deg > 0, or every node) as the value to scan into new ids
+__global__ void k_er_keep(int64_t n, int drop, const int* __restrict__ deg, int* __restrict__ keep,
+                          long long* __restrict__ kdeg) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        keep[i] = (!drop || deg[i] > 0) ? 1 : 0;
+        kdeg[i] = deg[i];
+    }
+}
+
+// row_ptr of the kept rows: scanned degrees compacted through the new ids
+__global__ void k_er_rowptr(int64_t n, const int* __restrict__ keep, const int* __restrict__ newid,
+                            const long long* __restrict__ sdeg, long long* __restrict__ row_ptr) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        if (keep[i]) row_ptr[newid[i]] = sdeg[i];
+}
+
+__global__ void k_er_fill(int64_t n, double lq, uint64_t seed, const int* __restrict__ up,
+                          const int* __restrict__ keep, const int* __restrict__ newid,
+                          const long long* __restrict__ row_ptr, int* __restrict__ cur, int32_t* __restrict__ col) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (!up[i]) continue;
+        const int32_t ni = newid[i];
+        long long pos = row_ptr[ni + 1] - up[i];
+        row_pairs(seed, i, n, lq, [&](int64_t j) {
+            const int32_t nj = newid[j];
+            col[pos++] = nj;
+            const int s = atomicAdd(&cur[nj], 1);
+            col[row_ptr[nj] + s] = ni;
+        });
+        (void)keep;
+    }
+}
+
+// sort the lower part (first cur[r] entries) of every kept row
+__global__ void k_er_sort(int64_t rows, const long long* __restrict__ row_ptr, const int* __restrict__ cur,
+                          int32_t* __restrict__ col) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += (int64_t)gridDim.x * blockDim.x) {
+        int32_t* a = col + row_ptr[r];
+        const int m = cur[r];
+        for (int x = 1; x < m; ++x) {
+            const int32_t v = a[x];
+            int y = x - 1;
+            while (y >= 0 && a[y] > v) {
+                a[y + 1] = a[y];
+                --y;
+            }
+            a[y + 1] = v;
+        }
+    }
+}
+
+constexpr int64_t kScan = 16ll << 20;
+
+inline int64_t work_bytes(int64_t n) {
+    // up, deg, keep, newid, cur: int32[n] each (padded); kdeg/sdeg: int64[n+1]; scan scratch
+    const int64_t a = (4 * n + 255) & ~255ll, b = (8 * (n + 1) + 255) & ~255ll;
+    return 5 * a + b + kScan;
+}
+
+}  // namespace er
+}  // namespace mjx
+
+extern "C" int64_t mjx_er_work_bytes(int64_t n) { return n < 1 ? 0 : mjx::er::work_bytes(n); }
+
+extern "C" int mjx_er_generate(int64_t n, double p, uint64_t seed, int drop_isolated, long long* row_ptr,
+                               int32_t* col, int64_t col_cap, int64_t* n_out, int64_t* nnz_out, void* work,
+                               int64_t work_bytes, void* stream) {
+    using namespace mjx::er;
+    if (n < 1 || n > (int64_t)INT32_MAX - 1 || !(p >= 0.0) || !(p < 1.0) || !row_ptr || !n_out || !nnz_out || !work)
+        return MJX_EINVAL;
+    if (work_bytes < mjx::er::work_bytes(n)) return MJX_ERANGE;
+    hipStream_t st = mjx::as_stream(stream);
+    const int64_t a = (4 * n + 255) & ~255ll;
+    char* w = static_cast<char*>(work);
+    int* up = reinterpret_cast<int*>(w);
+    int* deg = reinterpret_cast<int*>(w + a);
+    int* keep = reinterpret_cast<int*>(w + 2 * a);
+    int* newid = reinterpret_cast<int*>(w + 3 * a);
+    int* cur = reinterpret_cast<int*>(w + 4 * a);
+    long long* kdeg = reinterpret_cast<long long*>(w + 5 * a);
+    void* scan = w + 5 * a + ((8 * (n + 1) + 255) & ~255ll);
+    const double lq = (p > 0.0) ? log1p(-p) : 0.0;          // 0 marks p = 0 (no pairs)
+    const int grid = mjx::grid_for(n);
+    MJX_HIP(hipMemsetAsync(deg, 0, sizeof(int) * n, st), "er memset");
+    MJX_HIP(hipMemsetAsync(cur, 0, sizeof(int) * n, st), "er memset");
+    k_er_count<<<grid, 256, 0, st>>>(n, lq, seed, up, deg);
+    MJX_LAUNCH_CHECK("k_er_count");
+    k_er_keep<<<grid, 256, 0, st>>>(n, drop_isolated, deg, keep, kdeg);
+    MJX_LAUNCH_CHECK("k_er_keep");
+    MJX_HIP(hipMemsetAsync(kdeg + n, 0, sizeof(long long), st), "er memset");
+    size_t need1 = 0, need2 = 0;
+    MJX_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, need1, keep, newid, n, st), "er scan size");
+    MJX_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, need2, kdeg, kdeg, n + 1, st), "er scan size");
+    if ((int64_t)need1 > kScan || (int64_t)need2 > kScan) return MJX_ERANGE;
+    MJX_HIP(hipcub::DeviceScan::ExclusiveSum(scan, need1, keep, newid, n, st), "er scan ids");
+    MJX_HIP(hipcub::DeviceScan::ExclusiveSum(scan, need2, kdeg, kdeg, n + 1, st), "er scan degrees");
+    // kept count and edge total: newid[n-1] + keep[n-1], kdeg[n]
+    int last[2];
+    long long tot = 0;
+    MJX_HIP(hipMemcpyAsync(&last[0], newid + n - 1, sizeof(int), hipMemcpyDeviceToHost, st), "er read");
+    MJX_HIP(hipMemcpyAsync(&last[1], keep + n - 1, sizeof(int), hipMemcpyDeviceToHost, st), "er read");
+    MJX_HIP(hipMemcpyAsync(&tot, kdeg + n, sizeof(long long), hipMemcpyDeviceToHost, st), "er read");
+    MJX_HIP(hipStreamSynchronize(st), "er sync");
+    const int64_t n2 = (int64_t)last[0] + last[1];
+    *n_out = n2;
+    *nnz_out = tot;
+    if (tot > col_cap) return MJX_ERANGE;
+    if (tot > 0 && !col) return MJX_EINVAL;
+    k_er_rowptr<<<grid, 256, 0, st>>>(n, keep, newid, kdeg, row_ptr);
+    MJX_LAUNCH_CHECK("k_er_rowptr");
+    MJX_HIP(hipMemcpyAsync(row_ptr + n2, &tot, sizeof(long long), hipMemcpyHostToDevice, st), "er total");
+    if (tot > 0) {
+        k_er_fill<<<grid, 256, 0, st>>>(n, lq, seed, up, keep, newid, row_ptr, cur, col);
+        MJX_LAUNCH_CHECK("k_er_fill");
+        k_er_sort<<<mjx::grid_for(n2), 256, 0, st>>>(n2, row_ptr, cur, col);
+        MJX_LAUNCH_CHECK("k_er_sort");
+    }
+    MJX_HIP(hipStreamSynchronize(st), "er sync");   // `tot` lives on this stack frame
+    return MJX_OK;
+}

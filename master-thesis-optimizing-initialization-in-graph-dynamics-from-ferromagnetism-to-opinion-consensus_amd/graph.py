@@ -19,6 +19,8 @@ exactly when networkx is importable; ``random_regular_graph`` and
 double-edge-swap repair; Batagelj-Brandes geometric skipping), whose parity
 with networkx is distributional, not bit-exact.
 """
+import math
+
 import numpy as np
 import torch
 
@@ -217,6 +219,39 @@ def random_regular_rows_device(d, n, seed=0, row_lo=0, row_hi=None):
     return adj
 
 
+def erdos_renyi_device(n, p, seed=0, drop_isolated=False):
+    """G(n, p) generated on the device into CSR (mjx_er_generate): the
+    notebook's ER graph (code/ER_BDCM_entropy.ipynb nb:278-291) at sizes its
+    dense adjacency cannot reach (config C4: n = 1e7, p = 5/(n-1)).
+    Distributional parity with networkx; deterministic in (n, p, seed).
+    Returns a device ``Graph``; with ``drop_isolated`` also the number of
+    isolated nodes removed (the survivors are relabelled in increasing order)."""
+    from . import _lib
+    import ctypes
+    n, p = int(n), float(p)
+    if n < 1 or not 0.0 <= p < 1.0:
+        raise ValueError("need n >= 1 and 0 <= p < 1")
+    dev = _device.require_gpu()
+    row_ptr = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    work = torch.empty(int(_lib.load().mjx_er_work_bytes(n)), dtype=torch.uint8, device=dev)
+    mean = n * (n - 1) * p                       # E[2 * edges]
+    cap = int(mean + 12 * math.sqrt(2 * mean + 1) + 64)
+    n_out, nnz = ctypes.c_int64(0), ctypes.c_int64(0)
+    for _ in range(2):
+        col = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
+        rc = _lib.load().mjx_er_generate(n, p, int(seed) & 0xFFFFFFFFFFFFFFFF, int(bool(drop_isolated)),
+                                         _device.ptr(row_ptr), _device.ptr(col), cap, ctypes.byref(n_out),
+                                         ctypes.byref(nnz), _device.ptr(work), work.numel(), _device.stream_handle())
+        if rc == 3 and nnz.value > cap:          # MJX_ERANGE: a (very) unlikely edge count, retry at its size
+            cap = int(nnz.value)
+            continue
+        _lib.check(rc, "mjx_er_generate")
+        break
+    del work
+    g = Graph.csr_device(row_ptr[:n_out.value + 1], col[:nnz.value])
+    return (g, n - n_out.value) if drop_isolated else g
+
+
 def random_regular_graph_device(d, n, seed=0):
     """Device-resident ELL ``Graph`` of a random simple d-regular graph (for
     sizes networkx cannot reach, e.g. N = 1e9 at d = 6: 24 GB of int32)."""
@@ -274,6 +309,21 @@ class Graph:
             raise ValueError("CSR rows longer than 255 are not supported by the bit-sliced counter")
         order = np.argsort(np.diff(rp), kind="stable").astype(np.int32)
         return cls("csr", n, row_ptr=_device.to_device(rp), col=_device.to_device(cl), order=_device.to_device(order))
+
+    @classmethod
+    def csr_device(cls, row_ptr, col):
+        """CSR graph from device tensors (no host round trip of the arrays):
+        row_ptr int64 (n+1,), col int32 (nnz,)."""
+        rp = row_ptr.to(torch.int64).contiguous()
+        cl = col.to(torch.int32).contiguous()
+        n = rp.shape[0] - 1
+        if n < 0:
+            raise ValueError("malformed CSR")
+        deg = rp[1:] - rp[:-1]
+        if n and int(deg.max().item()) > 255:
+            raise ValueError("CSR rows longer than 255 are not supported by the bit-sliced counter")
+        order = torch.sort(deg, stable=True).indices.to(torch.int32)
+        return cls("csr", n, row_ptr=rp, col=cl, order=order)
 
     @property
     def nnz(self):
