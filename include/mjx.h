@@ -135,6 +135,12 @@ typedef struct mjx_sa_state {
     int64_t*  tr_sum;    /* [nsteps*R] sum_end after the step               */
     double*   tr_dE;     /* [nsteps*R] delta_H (code/SA_RRG.py:74)          */
     int32_t*  tr_tie;    /* [R] count of |u - exp(-dE)| < 4 ulp near-ties    */
+    /* optional proposal tape for mjx_sa_lightcone_steps (NULL / 0 to draw
+     * inside the step kernel): the (i, u) of up to tape_cap steps of every
+     * replica are drawn ahead by a wave per replica, row k = step k */
+    int32_t*  tape_i;    /* [tape_cap*R] */
+    double*   tape_u;    /* [tape_cap*R] */
+    int64_t   tape_cap;
 } mjx_sa_state;
 
 /* Seed replica r with seeds[r] (device uint32[R]), draw s0 into the

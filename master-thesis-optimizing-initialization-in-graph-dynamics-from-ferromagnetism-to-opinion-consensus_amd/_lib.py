@@ -77,6 +77,7 @@ class MjxSaState(ctypes.Structure):
         ("sum_end", c_vp), ("done", c_vp), ("prop_i", c_vp), ("prop_s", c_vp),
         ("prop_u", c_vp), ("cnt", c_vp),
         ("tr_i", c_vp), ("tr_acc", c_vp), ("tr_sum", c_vp), ("tr_dE", c_vp), ("tr_tie", c_vp),
+        ("tape_i", c_vp), ("tape_u", c_vp), ("tape_cap", c_i64),
     ]
 
 

@@ -222,34 +222,7 @@ __device__ void coop_twist(uint32_t* __restrict__ g, uint32_t* buf, int lane) {
     for (int k = lane; k < MT_N; k += 64) buf[k] = ld_nc(g + k);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    // phase A: k in [0, 227): every input is an old word
-    for (int k = lane; k < MT_N - MT_M; k += 64) {
-        uint32_t v = mt_mix(buf[k], buf[k + 1], buf[k + MT_M]);
-        __builtin_amdgcn_wave_barrier();
-        buf[k] = v;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-    }
-    // phase B: k in [227, 454): far word k-227 is new (phase A)
-    for (int k = MT_N - MT_M + lane; k < 2 * (MT_N - MT_M); k += 64) {
-        uint32_t v = mt_mix(buf[k], buf[k + 1], buf[k + MT_M - MT_N]);
-        __builtin_amdgcn_wave_barrier();
-        buf[k] = v;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-    }
-    // phase C: k in [454, 623): far word k-227 in [227, 396) is new (phase B)
-    for (int k = 2 * (MT_N - MT_M) + lane; k < MT_N - 1; k += 64) {
-        uint32_t v = mt_mix(buf[k], buf[k + 1], buf[k + MT_M - MT_N]);
-        __builtin_amdgcn_wave_barrier();
-        buf[k] = v;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-    }
-    // phase D: k = 623 uses the new word 0 and the new word 396
-    if (lane == 0) buf[MT_N - 1] = mt_mix(buf[MT_N - 1], buf[0], buf[MT_M - 1]);
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
+    lds_twist(buf, lane);
     for (int k = lane; k < MT_N; k += 64) g[k] = buf[k];
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -386,6 +359,8 @@ constexpr int LC_MAXD = 16;
 struct LcLevels {
     u64* s[LC_MAXT + 1];     // s[0] = current configuration, s[t] = onestep^t(s[0])
     int off[LC_MAXT + 2];    // list slot offset of level t; off[T+1] = candidate list
+    int tab;                 // slot offset of the ball table (node ids | adjacency rows | candidate entries)
+    int ball;                // table capacity: nodes of the radius-T ball (d-regular bound)
 };
 
 __device__ __forceinline__ u64 ld_word(const u64* p) {
@@ -472,11 +447,197 @@ __device__ int64_t lc_delta(const int32_t* __restrict__ adj, int d, int64_t W, i
     return ds;
 }
 
+// The same result as lc_delta, with the loads of a level issued together: the
+// ball's nodes and adjacency rows are kept in a per-lane LDS table (entries in
+// BFS order), the rows of the entries a level adds are loaded in one batch,
+// and the level words of up to CH candidates (own, D neighbours, cached next
+// level) in one batch, so a level costs two dependent memory round trips
+// instead of one per load.
 template <int D>
+struct LcChunk {
+    static constexpr int CH = (D <= 4) ? 16 : 8;
+};
+
+__device__ __forceinline__ int tab_find(const uint32_t* tnode, int nt, int32_t v) {
+    for (int e = 0; e < nt; ++e)
+        if ((int32_t)tnode[e * 64] == v) return e;
+    return -1;
+}
+
+template <int D>
+__device__ int64_t lc_delta_mlp(const int32_t* __restrict__ adj, int64_t W, int64_t col, u64 bit, int T,
+                                const LcLevels& L, uint32_t* lists, int32_t i, int* cnt, int* old_i) {
+    constexpr int CH = LcChunk<D>::CH;
+    uint32_t* tnode = lists + L.tab * 64;                  // [ball]
+    int32_t* tadj = (int32_t*)(lists + (L.tab + L.ball) * 64);     // [ball][D]
+    uint32_t* ul = lists + (L.tab + L.ball * (1 + D)) * 64;        // [ball] candidate entries
+    // level 0: the flipped node, its row and its word, in one round trip
+    int32_t r0[D];
+#pragma unroll
+    for (int m = 0; m < D; ++m) r0[m] = adj[(int64_t)i * D + m];
+    const u64 w0 = ld_word(L.s[0] + (int64_t)i * W + col);
+    tnode[0] = (uint32_t)i;
+#pragma unroll
+    for (int m = 0; m < D; ++m) tadj[m * 64] = r0[m];
+    int nt = 1, nadj = 1;
+    *old_i = (w0 & bit) ? 1 : 0;
+    lists[L.off[0] * 64] = (uint32_t)i | ((w0 & bit) ? 0u : 0x80000000u);
+    cnt[0] = 1;
+    int t = 1;
+    for (; t <= T; ++t) {
+        const uint32_t* prev = lists + L.off[t - 1] * 64;
+        uint32_t* cur = lists + L.off[t] * 64;
+        const int np = cnt[t - 1];
+        // candidates: the changed nodes of level t-1 and their neighbours
+        int nu = 0;
+        for (int q = 0; q < np; ++q) {
+            const int32_t v = (int32_t)(prev[q * 64] & 0x7fffffffu);
+            const int e = tab_find(tnode, nt, v);          // every changed node is a table entry
+            bool seen = false;
+            for (int x = 0; x < nu; ++x) seen |= ((int)ul[x * 64] == e);
+            if (!seen) ul[(nu++) * 64] = (uint32_t)e;
+            for (int m = 0; m < D; ++m) {
+                const int32_t k = tadj[(e * D + m) * 64];
+                int ek = tab_find(tnode, nt, k);
+                if (ek < 0) {
+                    ek = nt++;
+                    tnode[ek * 64] = (uint32_t)k;
+                }
+                bool s2 = false;
+                for (int x = 0; x < nu; ++x) s2 |= ((int)ul[x * 64] == ek);
+                if (!s2) ul[(nu++) * 64] = (uint32_t)ek;
+            }
+        }
+        // adjacency rows of the entries this level added, one batch per CH
+        for (int base = nadj; base < nt; base += CH) {
+            int32_t rr[CH][D];
+#pragma unroll
+            for (int e = 0; e < CH; ++e) {
+                if (base + e < nt) {
+                    const int64_t node = (int64_t)tnode[(base + e) * 64];
+#pragma unroll
+                    for (int m = 0; m < D; ++m) rr[e][m] = adj[node * D + m];
+                }
+            }
+#pragma unroll
+            for (int e = 0; e < CH; ++e) {
+                if (base + e < nt) {
+#pragma unroll
+                    for (int m = 0; m < D; ++m) tadj[((base + e) * D + m) * 64] = rr[e][m];
+                }
+            }
+        }
+        nadj = nt;
+        // level words of the candidates, one batch per CH, then the rule
+        int nc = 0;
+        const u64* lp = L.s[t - 1];
+        const u64* lt = L.s[t];
+        for (int base = 0; base < nu; base += CH) {
+            u64 wn[CH][D], wo[CH], wc[CH];
+#pragma unroll
+            for (int e = 0; e < CH; ++e) {
+                if (base + e < nu) {
+                    const int ent = (int)ul[(base + e) * 64];
+                    const int64_t node = (int64_t)tnode[ent * 64];
+                    wo[e] = ld_word(lp + node * W + col);
+                    wc[e] = ld_word(lt + node * W + col);
+#pragma unroll
+                    for (int m = 0; m < D; ++m) wn[e][m] = ld_word(lp + (int64_t)tadj[(ent * D + m) * 64] * W + col);
+                }
+            }
+#pragma unroll
+            for (int e = 0; e < CH; ++e) {
+                if (base + e < nu) {
+                    const int ent = (int)ul[(base + e) * 64];
+                    const int32_t j = (int32_t)tnode[ent * 64];
+                    int ones = 0;
+                    uint32_t own = (wo[e] & bit) ? 1u : 0u;
+#pragma unroll
+                    for (int m = 0; m < D; ++m) {
+                        const int32_t k = tadj[(ent * D + m) * 64];
+                        uint32_t v = (wn[e][m] & bit) ? 1u : 0u;
+                        for (int q = 0; q < np; ++q) {
+                            const uint32_t pe = prev[q * 64];
+                            if ((int32_t)(pe & 0x7fffffffu) == k) v = pe >> 31;
+                        }
+                        ones += (int)v;
+                    }
+                    for (int q = 0; q < np; ++q) {
+                        const uint32_t pe = prev[q * 64];
+                        if ((int32_t)(pe & 0x7fffffffu) == j) own = pe >> 31;
+                    }
+                    // always-stay majority (code/SA_RRG.py:19-20)
+                    const uint32_t nb = (2 * ones > D) ? 1u : ((2 * ones < D) ? 0u : own);
+                    const uint32_t ob = (wc[e] & bit) ? 1u : 0u;
+                    if (nb != ob) {
+                        cur[nc * 64] = (uint32_t)j | (nb << 31);
+                        ++nc;
+                    }
+                }
+            }
+        }
+        cnt[t] = nc;
+        if (nc == 0) break;          // nothing propagates further
+    }
+    for (int u = t + 1; u <= T; ++u) cnt[u] = 0;
+    if (t <= T) return 0;
+    int64_t ds = 0;
+    const uint32_t* last = lists + L.off[T] * 64;
+    for (int q = 0; q < cnt[T]; ++q) ds += (last[q * 64] >> 31) ? 2 : -2;
+    return ds;
+}
+
+// (i_t, u_t) tape of K proposals per running replica (code/SA_RRG.py:73,76):
+// wave per replica, its MT19937 state twisted in LDS; the draws are consumed
+// serially (uniform across the wave) exactly as k_sa_lightcone would.  The
+// stream does not depend on accept decisions, so the tape can run ahead of the
+// steps; a replica that finishes inside the tape leaves its tail unused.
+__global__ void __launch_bounds__(64) k_sa_tape(int64_t n, int64_t R, int64_t K, mjx_sa_state st,
+                                                int32_t* __restrict__ tape_i, double* __restrict__ tape_u) {
+    __shared__ uint32_t buf[MT_N];
+    const int64_t r = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (st.done[r]) return;
+    uint32_t* g = st.mt + r * MT_N;
+    for (int k = lane; k < MT_N; k += 64) buf[k] = ld_nc(g + k);
+    int idx = st.mt_idx[r];
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const uint64_t rng = (uint64_t)(n - 1);
+    uint32_t mask = (uint32_t)rng;
+    mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+    auto next = [&]() -> uint32_t {
+        if (idx >= MT_N) {
+            lds_twist(buf, lane);
+            idx = 0;
+        }
+        return mt_temper(buf[idx++]);
+    };
+    for (int64_t k = 0; k < K; ++k) {
+        uint32_t i = 0;
+        if (rng > 0) {
+            for (;;) {
+                const uint32_t v = next() & mask;
+                if (v <= (uint32_t)rng) { i = v; break; }
+            }
+        }
+        const uint32_t w1 = next();
+        const uint32_t w2 = next();
+        if (lane == 0) {
+            tape_i[k * R + r] = (int32_t)i;
+            tape_u[k * R + r] = mt_double(w1, w2);
+        }
+    }
+    for (int k = lane; k < MT_N; k += 64) g[k] = buf[k];
+    if (lane == 0) st.mt_idx[r] = idx;
+}
+
+template <int D, bool TAPE>
 __global__ void __launch_bounds__(64) k_sa_lightcone(const int32_t* __restrict__ adj, int d, int64_t n, int64_t R,
                                                      int64_t W, LcLevels L, int T, mjx_sa_state st, int64_t nsteps,
                                                      double par_a, double par_b, double a_cap, double b_cap,
-                                                     int64_t t_cap) {
+                                                     int64_t t_cap, const int32_t* __restrict__ tape_i,
+                                                     const double* __restrict__ tape_u) {
     extern __shared__ uint32_t lc_lists[];
     __shared__ uint32_t twist_buf[MT_N];
     const int lane = threadIdx.x;
@@ -493,26 +654,51 @@ __global__ void __launch_bounds__(64) k_sa_lightcone(const int32_t* __restrict__
     const uint64_t rng = (uint64_t)(n - 1);
     uint32_t mask = (uint32_t)rng;
     mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+    // tape mode: the next proposal's (i, u) is loaded one step ahead
+    int32_t nx_i = 0;
+    double nx_u = 0.0;
+    if constexpr (TAPE) {
+        if (live && nsteps > 0) {
+            nx_i = tape_i[r];
+            nx_u = tape_u[r];
+        }
+    }
     for (int64_t step = 0; step < nsteps; ++step) {
         const bool active = live && done == 0;
-        // randint(low=0, high=n) (code/SA_RRG.py:73): numpy legacy masked rejection
-        bool pending = active && rng > 0;
         uint32_t i = 0;
-        while (__ballot(pending)) {
-            const uint32_t y = g.draw(pending);
-            if (pending) {
-                const uint32_t v = y & mask;
-                if (v <= (uint32_t)rng) { i = v; pending = false; }
+        double u = 0.0;
+        if constexpr (TAPE) {
+            i = (uint32_t)nx_i;
+            u = nx_u;
+            if (live && step + 1 < nsteps) {
+                nx_i = tape_i[(step + 1) * R + r];
+                nx_u = tape_u[(step + 1) * R + r];
             }
+        } else {
+            // randint(low=0, high=n) (code/SA_RRG.py:73): numpy legacy masked rejection
+            bool pending = active && rng > 0;
+            while (__ballot(pending)) {
+                const uint32_t y = g.draw(pending);
+                if (pending) {
+                    const uint32_t v = y & mask;
+                    if (v <= (uint32_t)rng) { i = v; pending = false; }
+                }
+            }
+            // rand() (code/SA_RRG.py:76)
+            const uint32_t w1 = g.draw(active);
+            const uint32_t w2 = g.draw(active);
+            u = mt_double(w1, w2);
         }
-        // rand() (code/SA_RRG.py:76)
-        const uint32_t w1 = g.draw(active);
-        const uint32_t w2 = g.draw(active);
         if (active) {
-            const double u = mt_double(w1, w2);
             int cnt[LC_MAXT + 1];
             int old_i;
-            const int64_t ds = lc_delta<D>(adj, d, W, col, bit, T, L, lists, (int32_t)i, cnt, &old_i);
+            int64_t ds;
+            if constexpr (D > 0) {
+                if (L.tab >= 0) ds = lc_delta_mlp<D>(adj, W, col, bit, T, L, lists, (int32_t)i, cnt, &old_i);
+                else ds = lc_delta<D>(adj, d, W, col, bit, T, L, lists, (int32_t)i, cnt, &old_i);
+            } else {
+                ds = lc_delta<D>(adj, d, W, col, bit, T, L, lists, (int32_t)i, cnt, &old_i);
+            }
             const int64_t sum_new = sum_end + ds;
             // delta_H (code/SA_RRG.py:37), same operation order, no contraction
             const double si = old_i ? 1.0 : -1.0;
@@ -552,7 +738,7 @@ __global__ void __launch_bounds__(64) k_sa_lightcone(const int32_t* __restrict__
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     if (live) {
-        st.mt_idx[r] = g.idx;
+        if constexpr (!TAPE) st.mt_idx[r] = g.idx;
         st.a[r] = a;
         st.b[r] = b;
         st.t[r] = t;
@@ -562,8 +748,9 @@ __global__ void __launch_bounds__(64) k_sa_lightcone(const int32_t* __restrict__
     }
 }
 
-// list slots per lane: levels 0..T (ball bounds) + candidate list
-static int lc_slots(int d, int T, int* off) {
+// list slots per lane: levels 0..T (ball bounds) + candidate list; with
+// `table` also the ball table of lc_delta_mlp (node ids, rows, candidates)
+static int lc_slots(int d, int T, int* off, bool table = false, int* tab = nullptr, int* ballT = nullptr) {
     int64_t total = 0, ball = 1, shell = 1;
     for (int t = 0; t <= T; ++t) {
         if (t > 0) {
@@ -576,8 +763,19 @@ static int lc_slots(int d, int T, int* off) {
     }
     off[T + 1] = (int)total;
     total += ball;                    // candidates of the last level
+    if (table) {
+        *tab = (int)total;
+        *ballT = (int)ball;
+        total += ball * (2 + d);
+        if (total > (1 << 20)) return -1;
+    }
     return (int)total;
 }
+
+constexpr size_t kLcLdsMax = 150 * 1024;
+
+// the batched-load evaluation is instantiated for these degrees
+static bool lc_mlp_degree(int d) { return d == 3 || d == 4 || d == 6; }
 
 }  // namespace mjx
 
@@ -650,7 +848,11 @@ extern "C" int mjx_sa_steps(const int32_t* adj, int64_t n, int d, int p, int c, 
 extern "C" int64_t mjx_sa_lightcone_lds(int d, int p, int c) {
     const int T = p + c - 1;
     if (d < 1 || d > LC_MAXD || T < 1 || T > LC_MAXT) return -1;
-    int off[LC_MAXT + 2];
+    int off[LC_MAXT + 2], tab, ball;
+    if (lc_mlp_degree(d)) {
+        const int s2 = lc_slots(d, T, off, true, &tab, &ball);
+        if (s2 > 0 && (size_t)s2 * 64 * 4 <= kLcLdsMax) return (int64_t)s2 * 64 * 4;
+    }
     const int slots = lc_slots(d, T, off);
     if (slots < 0) return -1;
     return (int64_t)slots * 64 * 4;
@@ -679,9 +881,16 @@ extern "C" int mjx_sa_lightcone_steps(const int32_t* adj, int64_t n, int d, int 
     if (T < 1 || T > LC_MAXT) return MJX_ERANGE;
     if (n > (int64_t)INT32_MAX) return MJX_ERANGE;
     LcLevels L;
-    const int slots = lc_slots(d, T, L.off);
+    int slots = -1;
+    L.tab = -1;
+    L.ball = 0;
+    if (lc_mlp_degree(d)) {
+        slots = lc_slots(d, T, L.off, true, &L.tab, &L.ball);
+        if (slots < 0 || (size_t)slots * 64 * 4 > kLcLdsMax) L.tab = -1;
+    }
+    if (L.tab < 0) slots = lc_slots(d, T, L.off);
     const size_t lds = (size_t)slots * 64 * 4;
-    if (slots < 0 || lds > 150 * 1024) return MJX_ERANGE;
+    if (slots < 0 || lds > kLcLdsMax) return MJX_ERANGE;
     L.s[0] = (u64*)s;
     for (int t = 1; t <= T; ++t) {
         if (!levels[t - 1]) return MJX_EINVAL;
@@ -692,17 +901,36 @@ extern "C" int mjx_sa_lightcone_steps(const int32_t* adj, int64_t n, int d, int 
     const int64_t W = (R + 63) / 64;
     hipStream_t hs = as_stream(stream);
     const mjx_sa_state st = *stp;
-    auto launch = [&](auto kern) -> int {
+    const bool tape = st.tape_i && st.tape_u && st.tape_cap > 0;
+    // one launch per tape chunk (the tape kernel fills the chunk's (i, u) first)
+    auto launch = [&](auto kern, mjx_sa_state s2, int64_t k) -> int {
         MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
                 "lightcone lds");
-        kern<<<(unsigned)W, 64, lds, hs>>>(adj, d, n, R, W, L, T, st, nsteps, par_a, par_b, a_cap, b_cap, t_cap);
+        kern<<<(unsigned)W, 64, lds, hs>>>(adj, d, n, R, W, L, T, s2, k, par_a, par_b, a_cap, b_cap, t_cap,
+                                           st.tape_i, st.tape_u);
         MJX_LAUNCH_CHECK("k_sa_lightcone");
         return MJX_OK;
     };
+    auto run = [&](auto kern_plain, auto kern_tape) -> int {
+        if (!tape) return launch(kern_plain, st, nsteps);
+        for (int64_t k0 = 0; k0 < nsteps; k0 += st.tape_cap) {
+            const int64_t k = (nsteps - k0 < st.tape_cap) ? nsteps - k0 : st.tape_cap;
+            k_sa_tape<<<(unsigned)R, 64, 0, hs>>>(n, R, k, st, st.tape_i, st.tape_u);
+            MJX_LAUNCH_CHECK("k_sa_tape");
+            mjx_sa_state s2 = st;     // trace rows of this chunk
+            if (s2.tr_i) s2.tr_i += k0 * R;
+            if (s2.tr_acc) s2.tr_acc += k0 * R;
+            if (s2.tr_sum) s2.tr_sum += k0 * R;
+            if (s2.tr_dE) s2.tr_dE += k0 * R;
+            const int rc = launch(kern_tape, s2, k);
+            if (rc) return rc;
+        }
+        return MJX_OK;
+    };
     switch (d) {
-        case 3: return launch(k_sa_lightcone<3>);
-        case 4: return launch(k_sa_lightcone<4>);
-        case 6: return launch(k_sa_lightcone<6>);
-        default: return launch(k_sa_lightcone<0>);
+        case 3: return run(k_sa_lightcone<3, false>, k_sa_lightcone<3, true>);
+        case 4: return run(k_sa_lightcone<4, false>, k_sa_lightcone<4, true>);
+        case 6: return run(k_sa_lightcone<6, false>, k_sa_lightcone<6, true>);
+        default: return run(k_sa_lightcone<0, false>, k_sa_lightcone<0, true>);
     }
 }

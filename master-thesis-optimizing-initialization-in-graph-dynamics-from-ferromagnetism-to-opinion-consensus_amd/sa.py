@@ -46,7 +46,7 @@ def schedule_constants(n):
 class SAReplicas:
     """R bit-packed SA replicas on one random regular graph (device resident)."""
 
-    def __init__(self, N, p, c, seeds, par_a=PAR_A, par_b=PAR_B, a0=None, b0=None, mode="auto"):
+    def __init__(self, N, p, c, seeds, par_a=PAR_A, par_b=PAR_B, a0=None, b0=None, mode="auto", tape=1024):
         self.graph = as_graph(N)
         if self.graph.kind != "ell":
             raise ValueError("SA runs on random regular graphs (ELL adjacency), code/SA_RRG.py:59-61")
@@ -107,6 +107,14 @@ class SAReplicas:
             self._lvl = (_lib.ctypes.c_void_p * T)(*[t.data_ptr() for t in self.levels])
             _lib.call("mjx_sa_lightcone_prepare", _device.ptr(self.graph.adj), n, self.graph.d, self.p, self.c, R,
                       _device.ptr(self.s), self._lvl, _device.stream_handle())
+            # proposal tape: (i, u) of `tape` steps per replica drawn ahead by
+            # a wave per replica (0 = draw inside the step kernel)
+            self.tape_cap = int(tape) if tape else 0
+            if self.tape_cap > 0:
+                self.tape_i = torch.empty(self.tape_cap * R, dtype=torch.int32, device=dev)
+                self.tape_u = torch.empty(self.tape_cap * R, dtype=torch.float64, device=dev)
+                self._state.tape_i, self._state.tape_u = self.tape_i.data_ptr(), self.tape_u.data_ptr()
+                self._state.tape_cap = self.tape_cap
 
     # -- stepping -----------------------------------------------------------
     def steps(self, k, trace=False):

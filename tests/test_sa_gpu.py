@@ -33,15 +33,25 @@ def test_sa_init_draws_reference_s0(mjx_mod):
         assert np.array_equal(conf[r], 2 * rs.binomial(n=1, p=0.5, size=[n]) - 1)
 
 
-@pytest.mark.parametrize("mode", ["lightcone", "rollout"])
+def _sa(mjx_mod, N, p, c, seeds, mode):
+    """mode: "lightcone" (default tape), "lightcone-notape" (draws inside the
+    step kernel), "lightcone-tape7" (tape chunks of 7 steps), "rollout"."""
+    tape = {"lightcone-notape": 0, "lightcone-tape7": 7}.get(mode, 1024)
+    return mjx_mod.SAReplicas(N, p, c, seeds, mode=mode.split("-")[0], tape=tape)
+
+
+MODES = ["lightcone", "lightcone-notape", "lightcone-tape7", "rollout"]
+
+
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("name", ["sa_d4_n200_p3c1.npz", "sa_d3_n300_p2c1.npz", "sa_d4_n200_p1c1.npz",
                                   "sa_d4_n1000_p2c2.npz"])
 def test_sa_trace_bit_exact(mjx_mod, name, mode):
     z = load_golden(name)
     N, p, c = z["N"], int(z["p"]), int(z["c"])
     seeds = [int(s) for s in z["seeds"]]
-    sa = mjx_mod.SAReplicas(N, p, c, seeds, mode=mode)
-    assert sa.mode == mode
+    sa = _sa(mjx_mod, N, p, c, seeds, mode)
+    assert sa.mode == mode.split("-")[0]
     lens = [len(z[f"seed{sd}_i"]) for sd in seeds]
     steps = max(lens)
     done_at = 0
@@ -75,10 +85,12 @@ def test_sa_trace_bit_exact(mjx_mod, name, mode):
     assert int(res["near_ties"].sum()) == 0
 
 
-def test_sa_lightcone_levels_stay_consistent(mjx_mod):
+@pytest.mark.parametrize("d,p,c", [(4, 2, 2), (3, 2, 1), (6, 2, 1), (5, 1, 2)])
+def test_sa_lightcone_levels_stay_consistent(mjx_mod, d, p, c):
     """After many accepted flips the cached levels the light-cone kernel keeps
-    up to date must equal fresh rollouts of the current configuration."""
-    n, d, p, c = 2000, 4, 2, 2
+    up to date must equal fresh rollouts of the current configuration
+    (d = 3, 4, 6: batched-load evaluation; d = 5: the generic one)."""
+    n = 2000
     adj = mjx_mod.random_regular_graph(d, n, seed=9)
     sa = mjx_mod.SAReplicas(adj, p, c, list(range(130)), mode="lightcone")
     sa.steps(3000)
@@ -103,14 +115,14 @@ def test_sa_run_matches_full_reference_script(mjx_mod):
     assert np.array_equal(res["graphs"][0], N)
 
 
-@pytest.mark.parametrize("mode", ["lightcone", "rollout"])
+@pytest.mark.parametrize("mode", MODES)
 def test_sa_many_replicas_vs_oracle(mjx_mod, mode):
     """R = 200 replicas (ragged: 4 words, 56 padding bits) on a fresh graph,
     600 steps, sampled replicas' accept sequences against the oracle."""
     n, d, p, c = 500, 3, 2, 1
     adj = mjx_mod.random_regular_graph(d, n, seed=42)
     seeds = list(range(200))
-    sa = mjx_mod.SAReplicas(adj, p, c, seeds, mode=mode)
+    sa = _sa(mjx_mod, adj, p, c, seeds, mode)
     tr = {k: v.cpu().numpy() for k, v in sa.steps(600, trace=True).items()}
     for r in (0, 1, 63, 64, 127, 199):
         o = orc.sa_loop(adj, p, c, seeds[r], max_steps=600, trace=True)["trace"]
