@@ -464,48 +464,102 @@ __device__ __forceinline__ int tab_find(const uint32_t* tnode, int nt, int32_t v
     return -1;
 }
 
-template <int D>
+// 128-bit membership filter of node ids kept in two registers: a clear bit
+// proves absence, so most table / change-list lookups skip their LDS scan
+struct Bloom {
+    u64 lo = 0, hi = 0;
+    __device__ __forceinline__ static uint32_t slot(int32_t v) { return ((uint32_t)v * 0x9E3779B1u) >> 25; }
+    __device__ __forceinline__ void add(int32_t v) {
+        const uint32_t b = slot(v);
+        if (b < 64) lo |= 1ull << b; else hi |= 1ull << (b - 64);
+    }
+    __device__ __forceinline__ bool maybe(int32_t v) const {
+        const uint32_t b = slot(v);
+        return ((b < 64 ? lo >> b : hi >> (b - 64)) & 1ull) != 0;
+    }
+};
+
+// PRE: the rows of i (p0) and of its neighbours (p1) were loaded during the
+// previous step (tape lookahead), so level 1 starts with its word batch and
+// the word of i joins that batch.
+template <int D, bool PRE>
 __device__ int64_t lc_delta_mlp(const int32_t* __restrict__ adj, int64_t W, int64_t col, u64 bit, int T,
-                                const LcLevels& L, uint32_t* lists, int32_t i, int* cnt, int* old_i) {
+                                const LcLevels& L, uint32_t* lists, int32_t i, int* cnt, int* old_i,
+                                const int32_t (&p0)[D], const int32_t (&p1)[D][D]) {
     constexpr int CH = LcChunk<D>::CH;
-    uint32_t* tnode = lists + L.tab * 64;                  // [ball]
-    int32_t* tadj = (int32_t*)(lists + (L.tab + L.ball) * 64);     // [ball][D]
-    uint32_t* ul = lists + (L.tab + L.ball * (1 + D)) * 64;        // [ball] candidate entries
-    // level 0: the flipped node, its row and its word, in one round trip
-    int32_t r0[D];
-#pragma unroll
-    for (int m = 0; m < D; ++m) r0[m] = adj[(int64_t)i * D + m];
-    const u64 w0 = ld_word(L.s[0] + (int64_t)i * W + col);
-    tnode[0] = (uint32_t)i;
-#pragma unroll
-    for (int m = 0; m < D; ++m) tadj[m * 64] = r0[m];
+    const int B = L.ball;
+    uint32_t* tnode = lists + L.tab * 64;                                // [B] node id
+    int32_t* tadj = (int32_t*)(lists + (L.tab + B) * 64);                // [B][D] adjacency row
+    uint32_t* ul = lists + (L.tab + B * (1 + D)) * 64;                   // [B] candidates of this level
+    int32_t* tmark = (int32_t*)(lists + (L.tab + B * (2 + D)) * 64);     // [B] level it was last a candidate
+    int32_t* tval = (int32_t*)(lists + (L.tab + B * (3 + D)) * 64);      // [B] (level << 1 | value) if changed
+    uint32_t* cind = lists + (L.tab + B * (4 + D)) * 64;                 // entry of every change-list slot
+    Bloom tab;
     int nt = 1, nadj = 1;
-    *old_i = (w0 & bit) ? 1 : 0;
-    lists[L.off[0] * 64] = (uint32_t)i | ((w0 & bit) ? 0u : 0x80000000u);
+    tnode[0] = (uint32_t)i;
+    tmark[0] = 0;
+    tab.add(i);
+    cind[L.off[0] * 64] = 0;
     cnt[0] = 1;
+    if constexpr (PRE) {
+        // entries 0..D: i and its neighbours, rows known; the word of i and
+        // the level-0 list entry are completed inside level 1's batch
+#pragma unroll
+        for (int m = 0; m < D; ++m) {
+            tadj[m * 64] = p0[m];
+            tnode[(1 + m) * 64] = (uint32_t)p0[m];
+            tmark[(1 + m) * 64] = 0;
+            tval[(1 + m) * 64] = -2;
+            tab.add(p0[m]);
+#pragma unroll
+            for (int q = 0; q < D; ++q) tadj[((1 + m) * D + q) * 64] = p1[m][q];
+        }
+        nt = nadj = 1 + D;
+        lists[L.off[0] * 64] = (uint32_t)i;
+    } else {
+        // level 0: the flipped node, its row and its word, in one round trip
+        int32_t r0[D];
+#pragma unroll
+        for (int m = 0; m < D; ++m) r0[m] = adj[(int64_t)i * D + m];
+        const u64 w0 = ld_word(L.s[0] + (int64_t)i * W + col);
+#pragma unroll
+        for (int m = 0; m < D; ++m) tadj[m * 64] = r0[m];
+        const uint32_t flipped = (w0 & bit) ? 0u : 1u;
+        tval[0] = (int32_t)flipped;                       // level 0, new value
+        *old_i = (w0 & bit) ? 1 : 0;
+        lists[L.off[0] * 64] = (uint32_t)i | (flipped << 31);
+    }
     int t = 1;
     for (; t <= T; ++t) {
         const uint32_t* prev = lists + L.off[t - 1] * 64;
+        const uint32_t* pind = cind + L.off[t - 1] * 64;
         uint32_t* cur = lists + L.off[t] * 64;
+        uint32_t* cdst = cind + L.off[t] * 64;
         const int np = cnt[t - 1];
+        Bloom pb;                                      // the changed nodes of level t-1
         // candidates: the changed nodes of level t-1 and their neighbours
         int nu = 0;
         for (int q = 0; q < np; ++q) {
-            const int32_t v = (int32_t)(prev[q * 64] & 0x7fffffffu);
-            const int e = tab_find(tnode, nt, v);          // every changed node is a table entry
-            bool seen = false;
-            for (int x = 0; x < nu; ++x) seen |= ((int)ul[x * 64] == e);
-            if (!seen) ul[(nu++) * 64] = (uint32_t)e;
+            const int e = (int)pind[q * 64];
+            pb.add((int32_t)tnode[e * 64]);
+            if (tmark[e * 64] != t) {
+                tmark[e * 64] = t;
+                ul[(nu++) * 64] = (uint32_t)e;
+            }
             for (int m = 0; m < D; ++m) {
                 const int32_t k = tadj[(e * D + m) * 64];
-                int ek = tab_find(tnode, nt, k);
+                int ek = tab.maybe(k) ? tab_find(tnode, nt, k) : -1;
                 if (ek < 0) {
                     ek = nt++;
                     tnode[ek * 64] = (uint32_t)k;
+                    tmark[ek * 64] = 0;
+                    tval[ek * 64] = -2;
+                    tab.add(k);
                 }
-                bool s2 = false;
-                for (int x = 0; x < nu; ++x) s2 |= ((int)ul[x * 64] == ek);
-                if (!s2) ul[(nu++) * 64] = (uint32_t)ek;
+                if (tmark[ek * 64] != t) {
+                    tmark[ek * 64] = t;
+                    ul[(nu++) * 64] = (uint32_t)ek;
+                }
             }
         }
         // adjacency rows of the entries this level added, one batch per CH
@@ -532,6 +586,8 @@ __device__ int64_t lc_delta_mlp(const int32_t* __restrict__ adj, int64_t W, int6
         int nc = 0;
         const u64* lp = L.s[t - 1];
         const u64* lt = L.s[t];
+        u64 wi = 0;
+        if (PRE && t == 1) wi = ld_word(L.s[0] + (int64_t)i * W + col);
         for (int base = 0; base < nu; base += CH) {
             u64 wn[CH][D], wo[CH], wc[CH];
 #pragma unroll
@@ -545,32 +601,39 @@ __device__ int64_t lc_delta_mlp(const int32_t* __restrict__ adj, int64_t W, int6
                     for (int m = 0; m < D; ++m) wn[e][m] = ld_word(lp + (int64_t)tadj[(ent * D + m) * 64] * W + col);
                 }
             }
+            if (PRE && t == 1 && base == 0) {     // the level-0 entry, now that the word of i is in
+                const uint32_t flipped = (wi & bit) ? 0u : 1u;
+                tval[0] = (int32_t)flipped;
+                *old_i = (wi & bit) ? 1 : 0;
+                lists[L.off[0] * 64] = (uint32_t)i | (flipped << 31);
+            }
 #pragma unroll
             for (int e = 0; e < CH; ++e) {
                 if (base + e < nu) {
                     const int ent = (int)ul[(base + e) * 64];
                     const int32_t j = (int32_t)tnode[ent * 64];
                     int ones = 0;
-                    uint32_t own = (wo[e] & bit) ? 1u : 0u;
 #pragma unroll
                     for (int m = 0; m < D; ++m) {
                         const int32_t k = tadj[(ent * D + m) * 64];
                         uint32_t v = (wn[e][m] & bit) ? 1u : 0u;
-                        for (int q = 0; q < np; ++q) {
-                            const uint32_t pe = prev[q * 64];
-                            if ((int32_t)(pe & 0x7fffffffu) == k) v = pe >> 31;
+                        if (pb.maybe(k)) {
+                            for (int q = 0; q < np; ++q) {
+                                const uint32_t pe = prev[q * 64];
+                                if ((int32_t)(pe & 0x7fffffffu) == k) v = pe >> 31;
+                            }
                         }
                         ones += (int)v;
                     }
-                    for (int q = 0; q < np; ++q) {
-                        const uint32_t pe = prev[q * 64];
-                        if ((int32_t)(pe & 0x7fffffffu) == j) own = pe >> 31;
-                    }
+                    const int32_t tv = tval[ent * 64];
+                    const uint32_t own = ((tv >> 1) == t - 1) ? (uint32_t)(tv & 1) : ((wo[e] & bit) ? 1u : 0u);
                     // always-stay majority (code/SA_RRG.py:19-20)
                     const uint32_t nb = (2 * ones > D) ? 1u : ((2 * ones < D) ? 0u : own);
                     const uint32_t ob = (wc[e] & bit) ? 1u : 0u;
                     if (nb != ob) {
                         cur[nc * 64] = (uint32_t)j | (nb << 31);
+                        cdst[nc * 64] = (uint32_t)ent;
+                        tval[ent * 64] = (t << 1) | (int32_t)nb;
                         ++nc;
                     }
                 }
@@ -654,25 +717,51 @@ __global__ void __launch_bounds__(64) k_sa_lightcone(const int32_t* __restrict__
     const uint64_t rng = (uint64_t)(n - 1);
     uint32_t mask = (uint32_t)rng;
     mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
-    // tape mode: the next proposal's (i, u) is loaded one step ahead
-    int32_t nx_i = 0;
-    double nx_u = 0.0;
+    // tape mode: proposals k+1 and k+2 are held in registers while step k runs
+    // (tape rows come three steps ahead); with the batched evaluation the
+    // adjacency rows of i_{k+1}'s neighbours and of i_{k+2} are loaded during
+    // step k, so a step starts with its level-1 word batch
+    constexpr int DD = (D > 0) ? D : 1;
+    const bool pre = TAPE && D > 0 && L.tab >= 0 && live && done == 0;   // tape rows valid for this launch
+    int32_t nx_i = 0, n1i = 0, n2i = 0;
+    double nx_u = 0.0, n1u = 0.0, n2u = 0.0;
+    int32_t A0[DD], A1[DD][DD], B0[DD];        // rows of i_k, of N(i_k), of i_{k+1}
+    auto row = [&](int32_t v, int32_t (&o)[DD]) {
+        const int64_t base = (int64_t)((uint32_t)v < (uint32_t)n ? v : 0) * DD;   // never out of bounds
+#pragma unroll
+        for (int m = 0; m < DD; ++m) o[m] = adj[base + m];
+    };
     if constexpr (TAPE) {
-        if (live && nsteps > 0) {
-            nx_i = tape_i[r];
-            nx_u = tape_u[r];
+        if (live && nsteps > 0) { nx_i = tape_i[r]; nx_u = tape_u[r]; }
+        if (live && nsteps > 1) { n1i = tape_i[R + r]; n1u = tape_u[R + r]; }
+        if (live && nsteps > 2) { n2i = tape_i[2 * R + r]; n2u = tape_u[2 * R + r]; }
+        if (pre) {
+            row(nx_i, A0);
+#pragma unroll
+            for (int m = 0; m < DD; ++m) row(A0[m], A1[m]);
+            if (nsteps > 1) row(n1i, B0);
         }
     }
     for (int64_t step = 0; step < nsteps; ++step) {
         const bool active = live && done == 0;
         uint32_t i = 0;
         double u = 0.0;
+        int32_t A1n[DD][DD], B0n[DD];
         if constexpr (TAPE) {
             i = (uint32_t)nx_i;
             u = nx_u;
-            if (live && step + 1 < nsteps) {
-                nx_i = tape_i[(step + 1) * R + r];
-                nx_u = tape_u[(step + 1) * R + r];
+            if (pre) {
+                if (step + 1 < nsteps) {
+#pragma unroll
+                    for (int m = 0; m < DD; ++m) row(B0[m], A1n[m]);
+                }
+                if (step + 2 < nsteps) row(n2i, B0n);
+            }
+            nx_i = n1i; nx_u = n1u;
+            n1i = n2i; n1u = n2u;
+            if (live && step + 3 < nsteps) {
+                n2i = tape_i[(step + 3) * R + r];
+                n2u = tape_u[(step + 3) * R + r];
             }
         } else {
             // randint(low=0, high=n) (code/SA_RRG.py:73): numpy legacy masked rejection
@@ -694,7 +783,20 @@ __global__ void __launch_bounds__(64) k_sa_lightcone(const int32_t* __restrict__
             int old_i;
             int64_t ds;
             if constexpr (D > 0) {
-                if (L.tab >= 0) ds = lc_delta_mlp<D>(adj, W, col, bit, T, L, lists, (int32_t)i, cnt, &old_i);
+                // the prefetched entries assume i and its D neighbours are distinct
+                // (a simple graph); a row with a loop or a repeated neighbour
+                // takes the path that deduplicates through the table
+                bool simple = true;
+#pragma unroll
+                for (int m = 0; m < DD; ++m) {
+                    simple &= A0[m] != (int32_t)i;
+#pragma unroll
+                    for (int q = m + 1; q < DD; ++q) simple &= A0[m] != A0[q];
+                }
+                if (pre && simple)
+                    ds = lc_delta_mlp<D, true>(adj, W, col, bit, T, L, lists, (int32_t)i, cnt, &old_i, A0, A1);
+                else if (L.tab >= 0)
+                    ds = lc_delta_mlp<D, false>(adj, W, col, bit, T, L, lists, (int32_t)i, cnt, &old_i, A0, A1);
                 else ds = lc_delta<D>(adj, d, W, col, bit, T, L, lists, (int32_t)i, cnt, &old_i);
             } else {
                 ds = lc_delta<D>(adj, d, W, col, bit, T, L, lists, (int32_t)i, cnt, &old_i);
@@ -736,6 +838,17 @@ __global__ void __launch_bounds__(64) k_sa_lightcone(const int32_t* __restrict__
         }
         // this wave's flips must land before its next reads of the same words
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (TAPE) {
+            if (pre) {       // rotate the prefetched rows
+#pragma unroll
+                for (int m = 0; m < DD; ++m) {
+                    A0[m] = B0[m];
+                    B0[m] = B0n[m];
+#pragma unroll
+                    for (int q = 0; q < DD; ++q) A1[m][q] = A1n[m][q];
+                }
+            }
+        }
     }
     if (live) {
         if constexpr (!TAPE) st.mt_idx[r] = g.idx;
@@ -766,7 +879,7 @@ static int lc_slots(int d, int T, int* off, bool table = false, int* tab = nullp
     if (table) {
         *tab = (int)total;
         *ballT = (int)ball;
-        total += ball * (2 + d);
+        total += ball * (4 + d) + off[T + 1];   // node, row, candidate, mark, value; change-list entries
         if (total > (1 << 20)) return -1;
     }
     return (int)total;
