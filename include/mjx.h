@@ -167,7 +167,9 @@ int mjx_sa_steps(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R,
  * (n*W words each), kept consistent by the kernel as flips are accepted.
  * mjx_sa_lightcone_prepare fills them from s (call after mjx_sa_init).
  * Supported: 1 <= T <= 6, d <= 16 and mjx_sa_lightcone_lds(d,p,c) <= 150 KiB
- * (bytes of LDS per 64 replicas; -1 if unsupported). */
+ * (bytes of LDS per 64 replicas; -1 if unsupported).  The step kernel runs
+ * several waves per 64-replica word column when the column count is small
+ * (environment MJX_LC_SPLIT = 1, 2, 4, ..., 64 overrides the choice). */
 int64_t mjx_sa_lightcone_lds(int d, int p, int c);
 int mjx_sa_lightcone_prepare(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R,
                              const uint64_t* s, uint64_t* const* levels, void* stream);

@@ -20,6 +20,8 @@
 // numpy does (code/SA_RRG.py:37).
 #include "mjx_common.h"
 #include <math.h>
+#include <stdlib.h>
+#include <algorithm>
 
 #pragma clang fp contract(off)
 
@@ -650,6 +652,177 @@ __device__ int64_t lc_delta_mlp(const int32_t* __restrict__ adj, int64_t W, int6
     return ds;
 }
 
+// Radius-2 ball as a tree in registers (T <= 2, D <= 4): when i, its D
+// neighbours a_m and their D(D-1) other neighbours (the children) are all
+// distinct -- every ball of a random regular graph except the few that hold a
+// short cycle -- the positions of the ball's nodes are fixed by the adjacency
+// rows, so candidate sets are bit tests and every value is read from a
+// register: no table, no scans.  Level 1 is one batch of words (level-0 words
+// of i, the a_m and the row entries of every a_m; level-1 words of i and the
+// a_m), level 2 two batches (rows and words of the children whose parent
+// changed, level-2 words of the candidates; then the level-1 words of those
+// children's neighbours).  Same change lists and sum as lc_delta.  Returns
+// false (nothing written) when the ball is not such a tree.
+template <int D>
+__device__ bool lc_tree2(const int32_t* __restrict__ adj, int64_t W, int64_t col, u64 bit, int T,
+                         const LcLevels& L, uint32_t* lists, int32_t i, int* cnt, int* old_i,
+                         const int32_t (&r0)[D], const int32_t (&r1)[D][D], int64_t& ds) {
+    // shape: i once in every a_m's row, all 1 + D + D(D-1) nodes distinct
+    bool ok = true;
+#pragma unroll
+    for (int m = 0; m < D; ++m) {
+        int ci = 0;
+#pragma unroll
+        for (int x = 0; x < D; ++x) ci += (r1[m][x] == i);
+        ok &= (ci == 1) && (r0[m] != i);
+#pragma unroll
+        for (int m2 = m + 1; m2 < D; ++m2) ok &= r0[m] != r0[m2];
+    }
+    if (!ok) return false;
+#pragma unroll
+    for (int m = 0; m < D; ++m)
+#pragma unroll
+        for (int x = 0; x < D; ++x) {
+            const int32_t c = r1[m][x];
+            if (c == i) continue;
+#pragma unroll
+            for (int m2 = 0; m2 < D; ++m2) ok &= (c != r0[m2]);
+#pragma unroll
+            for (int m2 = m; m2 < D; ++m2)
+#pragma unroll
+                for (int x2 = 0; x2 < D; ++x2)
+                    if (m2 > m || x2 > x) ok &= (r1[m2][x2] == i) || (r1[m2][x2] != c);
+        }
+    if (!ok) return false;
+    const u64* s0 = L.s[0];
+    const u64* s1 = L.s[1];
+    auto w = [&](const u64* lv, int32_t v) { return ld_word(lv + (int64_t)v * W + col); };
+    auto b = [&](u64 x) -> uint32_t { return (x & bit) ? 1u : 0u; };
+    auto maj = [&](int ones, uint32_t own) -> uint32_t { return (2 * ones > D) ? 1u : ((2 * ones < D) ? 0u : own); };
+    // level 1: one batch
+    u64 wi0 = w(s0, i), wi1 = w(s1, i), wa0[D], wa1[D], wr0[D][D];
+#pragma unroll
+    for (int m = 0; m < D; ++m) {
+        wa0[m] = w(s0, r0[m]);
+        wa1[m] = w(s1, r0[m]);
+#pragma unroll
+        for (int x = 0; x < D; ++x) wr0[m][x] = w(s0, r1[m][x]);
+    }
+    const uint32_t f = b(wi0) ^ 1u;                  // flipped spin of i
+    *old_i = (int)b(wi0);
+    lists[L.off[0] * 64] = (uint32_t)i | (f << 31);
+    cnt[0] = 1;
+    uint32_t ch1 = 0, nv1 = 0;                       // bit e: entry e (0 = i, 1+m = a_m) changed / new value
+    {
+        int ones = 0;
+#pragma unroll
+        for (int m = 0; m < D; ++m) ones += (int)b(wa0[m]);
+        const uint32_t nb = maj(ones, f);
+        if (nb != b(wi1)) { ch1 |= 1u; nv1 |= nb; }
+    }
+#pragma unroll
+    for (int m = 0; m < D; ++m) {
+        int ones = 0;
+#pragma unroll
+        for (int x = 0; x < D; ++x) ones += (int)((r1[m][x] == i) ? f : b(wr0[m][x]));
+        const uint32_t nb = maj(ones, b(wa0[m]));
+        if (nb != b(wa1[m])) { ch1 |= 2u << m; nv1 |= nb << (1 + m); }
+    }
+    int n1 = 0;
+    uint32_t* l1 = lists + L.off[1] * 64;
+    if (ch1 & 1u) l1[(n1++) * 64] = (uint32_t)i | ((nv1 & 1u) << 31);
+#pragma unroll
+    for (int m = 0; m < D; ++m)
+        if ((ch1 >> (1 + m)) & 1u) l1[(n1++) * 64] = (uint32_t)r0[m] | (((nv1 >> (1 + m)) & 1u) << 31);
+    cnt[1] = n1;
+    if (T == 1 || n1 == 0) {
+        if (T >= 2) cnt[2] = 0;
+        ds = 0;
+        if (T == 1) {
+            for (int q = 0; q < n1; ++q) ds += (l1[q * 64] >> 31) ? 2 : -2;
+        }
+        return true;
+    }
+    // level 2
+    const u64* s2 = L.s[2];
+    const bool c0 = ch1 & 1u;
+    const bool u0 = ch1 != 0;                        // i is a candidate if it or any a_m changed
+    u64 wi2 = 0, wa2[D], wc1[D][D], wc2[D][D];
+    int32_t cr[D][D][D];
+    if (u0) wi2 = w(s2, i);
+#pragma unroll
+    for (int m = 0; m < D; ++m) {
+        const bool cm = (ch1 >> (1 + m)) & 1u;
+        wa2[m] = 0;
+        if (c0 || cm) wa2[m] = w(s2, r0[m]);
+#pragma unroll
+        for (int x = 0; x < D; ++x) {
+            wc1[m][x] = 0;
+            wc2[m][x] = 0;
+            if (r1[m][x] == i) continue;
+            if (c0 || cm) wc1[m][x] = w(s1, r1[m][x]);        // neighbour value of a_m
+            if (cm) {
+                wc2[m][x] = w(s2, r1[m][x]);
+#pragma unroll
+                for (int y = 0; y < D; ++y) cr[m][x][y] = adj[(int64_t)r1[m][x] * D + y];
+            }
+        }
+    }
+    u64 wg[D][D][D];
+#pragma unroll
+    for (int m = 0; m < D; ++m) {
+        const bool cm = (ch1 >> (1 + m)) & 1u;
+#pragma unroll
+        for (int x = 0; x < D; ++x)
+#pragma unroll
+            for (int y = 0; y < D; ++y) {
+                wg[m][x][y] = 0;
+                if (cm && r1[m][x] != i && cr[m][x][y] != r0[m]) wg[m][x][y] = w(s1, cr[m][x][y]);
+            }
+    }
+    int n2 = 0;
+    int64_t acc = 0;
+    uint32_t* l2 = lists + L.off[2] * 64;
+    auto emit = [&](int32_t node, uint32_t nb) {
+        l2[(n2++) * 64] = (uint32_t)node | (nb << 31);
+        acc += nb ? 2 : -2;
+    };
+    const uint32_t vi1 = c0 ? (nv1 & 1u) : b(wi1);   // level-1 value of i
+    if (u0) {
+        int ones = 0;
+#pragma unroll
+        for (int m = 0; m < D; ++m) ones += (int)(((ch1 >> (1 + m)) & 1u) ? ((nv1 >> (1 + m)) & 1u) : b(wa1[m]));
+        const uint32_t nb = maj(ones, vi1);
+        if (nb != b(wi2)) emit(i, nb);
+    }
+#pragma unroll
+    for (int m = 0; m < D; ++m) {
+        const bool cm = (ch1 >> (1 + m)) & 1u;
+        const uint32_t va1 = cm ? ((nv1 >> (1 + m)) & 1u) : b(wa1[m]);
+        if (c0 || cm) {
+            int ones = 0;
+#pragma unroll
+            for (int x = 0; x < D; ++x) ones += (int)((r1[m][x] == i) ? vi1 : b(wc1[m][x]));
+            const uint32_t nb = maj(ones, va1);
+            if (nb != b(wa2[m])) emit(r0[m], nb);
+        }
+        if (cm) {
+#pragma unroll
+            for (int x = 0; x < D; ++x) {
+                if (r1[m][x] == i) continue;
+                int ones = 0;
+#pragma unroll
+                for (int y = 0; y < D; ++y) ones += (int)((cr[m][x][y] == r0[m]) ? va1 : b(wg[m][x][y]));
+                const uint32_t nb = maj(ones, b(wc1[m][x]));
+                if (nb != b(wc2[m][x])) emit(r1[m][x], nb);
+            }
+        }
+    }
+    cnt[2] = n2;
+    ds = (n2 == 0) ? 0 : acc;
+    return true;
+}
+
 // (i_t, u_t) tape of K proposals per running replica (code/SA_RRG.py:73,76):
 // wave per replica, its MT19937 state twisted in LDS; the draws are consumed
 // serially (uniform across the wave) exactly as k_sa_lightcone would.  The
@@ -700,14 +873,19 @@ __global__ void __launch_bounds__(64) k_sa_lightcone(const int32_t* __restrict__
                                                      int64_t W, LcLevels L, int T, mjx_sa_state st, int64_t nsteps,
                                                      double par_a, double par_b, double a_cap, double b_cap,
                                                      int64_t t_cap, const int32_t* __restrict__ tape_i,
-                                                     const double* __restrict__ tape_u) {
+                                                     const double* __restrict__ tape_u, int split) {
     extern __shared__ uint32_t lc_lists[];
     __shared__ uint32_t twist_buf[MT_N];
+    // `split` waves share one 64-replica word column, each taking 64/split
+    // replicas (the rest of its lanes idle): the step is bound by one wave's
+    // latency, so more, thinner waves carry more replicas per unit of time
     const int lane = threadIdx.x;
-    const int64_t col = blockIdx.x;
-    const int64_t r = col * 64 + lane;
-    const bool live = r < R;
-    const u64 bit = 1ull << lane;
+    const int per = 64 / split;
+    const int64_t col = blockIdx.x / split;
+    const int rl = (int)(blockIdx.x % split) * per + lane;    // bit of this lane's replica in the column
+    const int64_t r = col * 64 + rl;
+    const bool live = lane < per && r < R;
+    const u64 bit = 1ull << (rl & 63);
     uint32_t* lists = lc_lists + lane;
     WaveMT g{st.mt, twist_buf, r, live ? st.mt_idx[r] : MT_N, lane};
     double a = live ? st.a[r] : 0.0, b = live ? st.b[r] : 0.0;
@@ -780,8 +958,8 @@ __global__ void __launch_bounds__(64) k_sa_lightcone(const int32_t* __restrict__
         }
         if (active) {
             int cnt[LC_MAXT + 1];
-            int old_i;
-            int64_t ds;
+            int old_i = 0;
+            int64_t ds = 0;
             if constexpr (D > 0) {
                 // the prefetched entries assume i and its D neighbours are distinct
                 // (a simple graph); a row with a loop or a repeated neighbour
@@ -793,7 +971,13 @@ __global__ void __launch_bounds__(64) k_sa_lightcone(const int32_t* __restrict__
 #pragma unroll
                     for (int q = m + 1; q < DD; ++q) simple &= A0[m] != A0[q];
                 }
-                if (pre && simple)
+                bool done_tree = false;
+                if constexpr (D <= 4) {
+                    if (pre && simple && T <= 2)
+                        done_tree = lc_tree2<D>(adj, W, col, bit, T, L, lists, (int32_t)i, cnt, &old_i, A0, A1, ds);
+                }
+                if (done_tree) {
+                } else if (pre && simple)
                     ds = lc_delta_mlp<D, true>(adj, W, col, bit, T, L, lists, (int32_t)i, cnt, &old_i, A0, A1);
                 else if (L.tab >= 0)
                     ds = lc_delta_mlp<D, false>(adj, W, col, bit, T, L, lists, (int32_t)i, cnt, &old_i, A0, A1);
@@ -886,6 +1070,15 @@ static int lc_slots(int d, int T, int* off, bool table = false, int* tab = nullp
 }
 
 constexpr size_t kLcLdsMax = 150 * 1024;
+
+// waves per word column: fill the CUs with about two waves each (LDS allowing)
+static int lc_split(int64_t W, size_t lds) {
+    const int64_t per_cu = (lds > 0) ? std::max<int64_t>(1, std::min<int64_t>(2, (int64_t)(160 * 1024) / (int64_t)lds)) : 2;
+    const int64_t target = (int64_t)kCUs * per_cu;
+    int s = 1;
+    while (s < 64 && W * s * 2 <= target) s *= 2;
+    return s;
+}
 
 // the batched-load evaluation is instantiated for these degrees
 static bool lc_mlp_degree(int d) { return d == 3 || d == 4 || d == 6; }
@@ -1015,12 +1208,15 @@ extern "C" int mjx_sa_lightcone_steps(const int32_t* adj, int64_t n, int d, int 
     hipStream_t hs = as_stream(stream);
     const mjx_sa_state st = *stp;
     const bool tape = st.tape_i && st.tape_u && st.tape_cap > 0;
+    int split = lc_split(W, lds);
+    if (const char* e = getenv("MJX_LC_SPLIT")) split = atoi(e);   // tuning experiment
+    if (split < 1 || split > 64 || (64 % split)) return MJX_EINVAL;
     // one launch per tape chunk (the tape kernel fills the chunk's (i, u) first)
     auto launch = [&](auto kern, mjx_sa_state s2, int64_t k) -> int {
         MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
                 "lightcone lds");
-        kern<<<(unsigned)W, 64, lds, hs>>>(adj, d, n, R, W, L, T, s2, k, par_a, par_b, a_cap, b_cap, t_cap,
-                                           st.tape_i, st.tape_u);
+        kern<<<(unsigned)(W * split), 64, lds, hs>>>(adj, d, n, R, W, L, T, s2, k, par_a, par_b, a_cap, b_cap,
+                                                     t_cap, st.tape_i, st.tape_u, split);
         MJX_LAUNCH_CHECK("k_sa_lightcone");
         return MJX_OK;
     };

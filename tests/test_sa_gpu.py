@@ -138,3 +138,19 @@ def test_E_delta_matches_oracle(mjx_mod):
     N, s0 = z["d4_n1000_N"], z["d4_n1000_s0"][0]
     for (a, b, p, c, i) in [(15.0, 10.0, 1, 1, 3), (150.3, 77.7, 2, 1, 999), (1.5, 4000.0, 3, 1, 0)]:
         assert mjx_mod.E_delta(N, s0, a, b, p, c, i) == orc.E_delta(N, s0, a, b, p, c, i)
+
+
+@pytest.mark.parametrize("split", ["1", "4", "64"])
+def test_sa_lightcone_wave_split_is_bit_exact(mjx_mod, split, monkeypatch):
+    """Waves per word column (1, 4, 64 replicas per wave ... 1) only change the
+    schedule: the accept sequences equal the oracle's."""
+    monkeypatch.setenv("MJX_LC_SPLIT", split)
+    n, d, p, c = 400, 3, 2, 1
+    adj = mjx_mod.random_regular_graph(d, n, seed=5)
+    sa = mjx_mod.SAReplicas(adj, p, c, list(range(70)), mode="lightcone")
+    tr = {k: v.cpu().numpy() for k, v in sa.steps(300, trace=True).items()}
+    for r in (0, 5, 63, 64, 69):
+        o = orc.sa_loop(adj, p, c, r, max_steps=300, trace=True)["trace"]
+        L = len(o["i"])
+        assert np.array_equal(tr["accept"][:L, r], o["accept"])
+        assert np.array_equal(tr["sum_end"][:L, r], o["sum_end"])
