@@ -37,7 +37,7 @@ def test_sa_state_struct_matches_header(mjx_mod):
     src = open(HEADER).read()
     body = src[src.index("typedef struct mjx_sa_state"):src.index("} mjx_sa_state;")]
     body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
-    fields = re.findall(r"\*\s*([A-Za-z_]+);", body)
+    fields = re.findall(r"([A-Za-z_][A-Za-z_0-9]*)\s*;", body)
     assert fields == [f for f, _ in mjx_mod._lib.MjxSaState._fields_]
 
 
