@@ -14,6 +14,7 @@
 // computes the same switches from the same scan.
 #include "mjx_common.h"
 #include <algorithm>
+#include <cstdlib>
 #include <unordered_map>
 #include <utility>
 #include <vector>
@@ -688,6 +689,129 @@ __global__ void __launch_bounds__(kApplyThreads) k_bin_apply(const uint16_t* __r
     }
 }
 
+// phase 2, flat form (K <= kFlatMaxK): the tile's segment starts (relative,
+// pad count in the low 3 bits) and phase-1 positions are staged in LDS, and
+// each wave streams one contiguous stretch of the tile's offsets in 512-slot
+// chunks (one coalesced 1 KB load per wave instruction), finding each 8-slot
+// piece's segment with a forward cursor in LDS; four chunks per step.
+constexpr int kFlatMaxK = 960;      // 64 KB of counters + 12 B per segment stay within half of the CU's LDS
+
+__device__ __forceinline__ void tile_rule(const uint32_t* cnt, int64_t t, int64_t lo, int64_t hi, int d,
+                                          const uint32_t* __restrict__ s32, u64* __restrict__ s_out,
+                                          unsigned long long* __restrict__ counts, unsigned long long* red,
+                                          int nw) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t v0 = lo + t * kTile;
+    const int64_t v1 = (v0 + kTile < hi) ? v0 + kTile : hi;
+    unsigned long long ones = 0;
+    for (int64_t w = (v0 >> 6) + wave; w < ((v1 + 63) >> 6); w += nw) {
+        const int64_t v = (w << 6) + lane;
+        bool nb = false;
+        if (v < v1) {
+            const int64_t lv = v - v0;
+            const int c = (int)((cnt[lv >> 2] >> ((lv & 3) << 3)) & 0xffu);
+            const int own = (s32[v >> 5] >> (v & 31)) & 1u;
+            nb = (2 * c > d) || ((2 * c == d) && own);       // always-stay ties (code/SA_RRG.py:19-20)
+        }
+        const u64 word = __ballot(nb);
+        if (lane == 0) {
+            s_out[w] = word;
+            ones += __popcll(word);
+        }
+    }
+    if (counts) {
+        if (lane == 0) red[wave] = ones;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long tot = 0;
+            for (int i = 0; i < nw; ++i) tot += red[i];
+            if (tot) atomicAdd(counts, tot);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(kApplyThreads) k_bin_apply_flat(const uint16_t* __restrict__ off,
+                                                                  const long long* __restrict__ p1T,
+                                                                  const long long* __restrict__ p2,
+                                                                  const u64* __restrict__ msg, int64_t K, int64_t lo,
+                                                                  int64_t hi, int d, const uint32_t* __restrict__ s32,
+                                                                  u64* __restrict__ s_out,
+                                                                  unsigned long long* __restrict__ counts) {
+    extern __shared__ uint32_t cnt[];
+    constexpr int NW = kApplyThreads / 64;
+    constexpr int UC = 4;
+    __shared__ unsigned long long red[NW];
+    __shared__ int32_t srel[kFlatMaxK + 1];          // segment start - tile start | pad count
+    __shared__ long long spos[kFlatMaxK];            // phase-1 position of the segment
+    const int64_t T = gridDim.x;
+    const int64_t t = xcd_tile(blockIdx.x, T);
+    const long long* q2 = p2 + t * K;
+    const long long P0 = q2[0] & ~7ll;
+    for (int i = threadIdx.x; i < kCntWords; i += kApplyThreads) cnt[i] = 0;
+    for (int64_t b = threadIdx.x; b <= K; b += kApplyThreads) {
+        const long long v = q2[b];
+        srel[b] = (int32_t)(((v & ~7ll) - P0) | (b < K ? (v & 7) : 0));
+        if (b < K) spos[b] = p1T[t * K + b];
+    }
+    __syncthreads();
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int32_t Lt = srel[K] & ~7;
+    const int32_t Lw = (((Lt + NW - 1) / NW) + 511) & ~511;   // this wave's stretch, whole chunks
+    const int32_t a0 = wave * Lw;
+    const int32_t a1 = (a0 + Lw < Lt) ? a0 + Lw : Lt;
+    // segment of this lane's first piece: last b with start <= j (binary search)
+    int32_t b = 0;
+    {
+        const int32_t j = a0 + 8 * lane;
+        int32_t lo_b = 0, hi_b = (int32_t)K;                  // invariant: start[lo_b] <= j < start[hi_b]
+        if (j < Lt) {
+            while (hi_b - lo_b > 1) {
+                const int32_t mid = (lo_b + hi_b) >> 1;
+                if ((srel[mid] & ~7) <= j) lo_b = mid; else hi_b = mid;
+            }
+        }
+        b = lo_b;
+    }
+    const uint16_t* offt = off + P0;
+    for (int32_t c = a0; c < a1; c += UC * 512) {
+        uint4 o[UC];
+        u64 m0[UC], m1[UC];
+        int sh[UC];
+        unsigned lim[UC];
+#pragma unroll
+        for (int u = 0; u < UC; ++u) {
+            const int32_t j = c + u * 512 + 8 * lane;
+            lim[u] = 0;
+            if (j < a1) {
+                while ((srel[b + 1] & ~7) <= j) ++b;           // forward cursor (start[K] = Lt > j)
+                const int32_t sb = srel[b];
+                const int32_t st0 = sb & ~7;
+                const int32_t len = (srel[b + 1] & ~7) - st0 - (sb & 7);
+                const int32_t rel = j - st0;
+                const long long pos = spos[b] + rel;
+                o[u] = *reinterpret_cast<const uint4*>(offt + j);
+                m0[u] = msg[pos >> 6];
+                m1[u] = msg[(pos >> 6) + 1];
+                sh[u] = (int)(pos & 63);
+                const int32_t nb = len - rel;
+                lim[u] = (nb >= 8) ? 0xffu : (nb > 0 ? ((1u << nb) - 1) : 0u);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < UC; ++u) {
+            if (lim[u]) {
+                Piece pc;
+                pc.o = o[u];
+                const u64 w = sh[u] ? ((m0[u] >> sh[u]) | (m1[u] << (64 - sh[u]))) : m0[u];
+                pc.bits = (unsigned)w & lim[u];
+                apply_piece(cnt, pc);
+            }
+        }
+    }
+    __syncthreads();
+    tile_rule(cnt, t, lo, hi, d, s32, s_out, counts, red, NW);
+}
+
 inline int check_range(int64_t n, int d, int64_t row_lo, int64_t row_hi) {
     if (n < 1 || d < 1 || d > 16 || row_lo < 0 || row_hi > n || row_lo > row_hi) return MJX_EINVAL;
     if ((row_lo & 63) || ((row_hi & 63) && row_hi != n)) return MJX_EINVAL;
@@ -786,6 +910,20 @@ extern "C" int mjx_sweep_binned(const uint16_t* src_lo, const uint16_t* src_hi, 
     // two segments per phase-2 step (measured at N=1e9, d=6: one 8.30 ms per
     // sweep, two 8.19, four 10.5 -- the LDS counts are not the bound: without
     // them the sweep takes 7.7 ms)
+    // the flat form streams the tile contiguously; it needs the tile's
+    // segment table in LDS (K <= kFlatMaxK: n <= ~1e9); MJX_BIN_APPLY=segments
+    // forces the per-segment form (tests)
+    const char* form = getenv("MJX_BIN_APPLY");
+    const bool flat = s.K <= kFlatMaxK && !(form && form[0] == 's');
+    if (flat) {
+        MJX_HIP(hipFuncSetAttribute((const void*)k_bin_apply_flat, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    kCntWords * (int)sizeof(uint32_t)), "k_bin_apply_flat lds");
+        k_bin_apply_flat<<<(unsigned)s.T, kApplyThreads, kCntWords * sizeof(uint32_t), st>>>(
+            off, p1T, p2, (const mjx::u64*)msg, s.K, row_lo, row_hi, d, (const uint32_t*)s_in, (mjx::u64*)s_out,
+            counts);
+        MJX_LAUNCH_CHECK("k_bin_apply_flat");
+        return MJX_OK;
+    }
     MJX_HIP(hipFuncSetAttribute((const void*)k_bin_apply<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 kCntWords * (int)sizeof(uint32_t)), "k_bin_apply lds");
     k_bin_apply<2><<<(unsigned)s.T, kApplyThreads, kCntWords * sizeof(uint32_t), st>>>(

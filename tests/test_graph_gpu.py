@@ -120,10 +120,14 @@ def test_range_sweep_argument_checks(mjx_mod):
 
 @pytest.mark.parametrize("n,d,world", [(100_000, 6, 1), (100_037 + 1, 3, 3), (40_000_000, 3, 2), (5000, 4, 8),
                                         (3_000_000, 16, 1), (2_500_002, 5, 4)])
-def test_binned_sweep_equals_gather_sweep(mjx_mod, n, d, world):
+@pytest.mark.parametrize("form", ["flat", "segments"])
+def test_binned_sweep_equals_gather_sweep(mjx_mod, n, d, world, form, monkeypatch):
     """The source-binned plan (several 1M-node source blocks and 64K-node
     destination tiles from n = 2.5e6 on) gives the gather sweep's words and
-    counts for every rank's rows; d = 16 fills the byte counters to the top."""
+    counts for every rank's rows; d = 16 fills the byte counters to the top.
+    Both phase-2 forms (flat tile stream, per-segment loop) are run."""
+    if form == "segments":
+        monkeypatch.setenv("MJX_BIN_APPLY", "segments")
     seed = 9
     ranges = [mjx_mod.NodeRange(n, world, r) for r in range(world)]
     lib = mjx_mod.load_library()
