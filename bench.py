@@ -183,6 +183,10 @@ def bench_er(args, rank, world, dist, dev):
     g = mjx.erdos_renyi_device(n, args.er_deg / (n - 1), seed=args.seed + 31 + 1000 * rank)
     torch.cuda.synchronize()
     gen_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    g.class_ell()                    # degree-class ELL (nb:113-117's layout): setup, not timed
+    torch.cuda.synchronize()
+    layout_s = time.perf_counter() - t0
     gen = torch.Generator(device=dev).manual_seed(args.seed + 5 + rank)
     s0 = torch.randint(-2 ** 62, 2 ** 62, (n * W,), dtype=torch.int64, device=dev, generator=gen)
     out, tmp = torch.empty_like(s0), torch.empty_like(s0)
@@ -197,7 +201,8 @@ def bench_er(args, rank, world, dist, dev):
     el = _timed(lambda: [step() for _ in range(K)], dist, dev)
     nnz = g.nnz
     dbar = nnz / n
-    bytes_per_sweep = 4 * nnz + 8 * (n + 1) + (W * 8) * n * (dbar + 2)
+    # degree-class ELL sweep: int32 neighbours + int32 node order + state rows
+    bytes_per_sweep = 4 * nnz + 4 * n + (W * 8) * n * (dbar + 2)
     # sanity: an all-(+1) state is a fixed point of every node (isolated ones included)
     ones = torch.full_like(s0, -1)
     ck = torch.zeros_like(counts)
@@ -208,7 +213,8 @@ def bench_er(args, rank, world, dist, dev):
                   f"per GPU), {R} bit-packed "
                   f"replicas per GPU, {T} sweeps + fused count per step",
         "scaling": "weak", "ranks": world, "n": n, "nnz": nnz, "replicas_per_gpu": R, "steps": K,
-        "device_graph_s": gen_s,
+        "device_graph_s": gen_s, "class_layout_s": layout_s,
+        "layout": "degree-class ELL, one launch per degree class (nb:113-117)",
         "ms_per_step": 1e3 * el / K,
         "node_updates_per_s": world * n * R * T * K / el,
         "algorithmic_GBps_per_gpu": bytes_per_sweep * T * K / el / 1e9,

@@ -105,6 +105,22 @@ int mjx_rollout_csr_rp_ordered(const int64_t* row_ptr, const int32_t* col, const
                                int64_t words, const uint64_t* s_in, uint64_t* s_out, uint64_t* tmp,
                                int steps, unsigned long long* counts, void* stream);
 
+/* Degree-class ELL: the notebook's own ER layout (nb:113-117 sums
+ * s[N_nodes_pos[d]] for the nodes nodes_with_d_positions[d] of each degree
+ * class; nb:359-361 builds them), replacing mjx_rollout_csr_rp(_ordered)
+ * (`onestep_majority`, nb:113-117; `s_endstate`, nb:120-123).
+ * classes: HOST int64 array of nclasses rows {i0, count, D, base}: positions
+ * [i0, i0+count) of `order` hold the class's nodes, all of degree D
+ * (0 <= D <= 255), and node order[i0+k]'s neighbours are cell[base+k*D ..
+ * base+k*D+D); base is a multiple of 4; the counts sum to n.
+ * mjx_class_ell_fill writes `cell` from CSR (setup); mjx_rollout_class_rp has
+ * the contract of mjx_rollout_csr_rp.  Results do not depend on the layout. */
+int mjx_class_ell_fill(const int64_t* row_ptr, const int32_t* col, const int32_t* order,
+                       const int64_t* classes, int nclasses, int64_t n, int32_t* cell, void* stream);
+int mjx_rollout_class_rp(const int32_t* order, const int32_t* cell, const int64_t* classes, int nclasses,
+                         int64_t n, int64_t words, const uint64_t* s_in, uint64_t* s_out, uint64_t* tmp,
+                         int steps, unsigned long long* counts, void* stream);
+
 /* per-replica count of +1 spins, ADDED into counts (m(s) = (2*count-n)/n) */
 int mjx_popcount_np(const uint64_t* bits, int64_t n, unsigned long long* counts, void* stream);
 int mjx_popcount_rp(const uint64_t* bits, int64_t n, int64_t words,

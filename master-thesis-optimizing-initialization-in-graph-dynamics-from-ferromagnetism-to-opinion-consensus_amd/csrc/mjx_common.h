@@ -38,6 +38,25 @@ inline int grid_for(int64_t items, int per_cu = 8) {
     return (int)g;
 }
 
+// Blocks of `kernel` (with `lds` dynamic LDS bytes) resident on one CU at once,
+// memoised per (kernel, block, lds); thread-safe.
+int resident_blocks_per_cu(const void* kernel, int block, size_t lds);
+
+// Grid for a grid-stride loop over `items` threads' worth of work, capped at
+// what is resident on the chip at once.  A larger grid runs in rounds over a
+// fixed node partition, and the last round is partly empty: the 141-VGPR
+// counting CSR sweep holds 3 waves per SIMD, so an 8-per-SIMD grid ran in
+// 3 rounds (the last 2/3 full).
+template <typename K>
+inline int resident_grid(K* kernel, int block, size_t lds, int64_t items) {
+    int per = resident_blocks_per_cu(reinterpret_cast<const void*>(kernel), block, lds);
+    int64_t g = (items + block - 1) / block;
+    const int64_t cap = (int64_t)kCUs * per;
+    if (g > cap) g = cap;
+    if (g < 1) g = 1;
+    return (int)g;
+}
+
 // Bit-sliced majority with always-stay tie breaking (code/SA_RRG.py:19-20):
 // new = +1 if 2*cnt > d, -1 if 2*cnt < d, old if 2*cnt == d, where cnt is the
 // number of +1 neighbours.  Every bit lane of a word is an independent node

@@ -12,6 +12,7 @@
 #include "mjx_common.h"
 #include <string.h>
 #include <stdio.h>
+#include <mutex>
 
 namespace mjx {
 
@@ -19,6 +20,23 @@ static thread_local char g_hip_err[256] = "";
 
 void set_hip_error(hipError_t e, const char* where) {
     snprintf(g_hip_err, sizeof(g_hip_err), "%s: %s (%d)", where, hipGetErrorString(e), (int)e);
+}
+
+int resident_blocks_per_cu(const void* kernel, int block, size_t lds) {
+    struct Entry { const void* k; int block; size_t lds; int per; };
+    static std::mutex mu;
+    static Entry cache[64];
+    static int used = 0;
+    std::lock_guard<std::mutex> lock(mu);
+    for (int i = 0; i < used; ++i)
+        if (cache[i].k == kernel && cache[i].block == block && cache[i].lds == lds) return cache[i].per;
+    int per = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, block, lds) != hipSuccess || per < 1) {
+        (void)hipGetLastError();
+        per = 1;
+    }
+    if (used < 64) cache[used++] = Entry{kernel, block, lds, per};
+    return per;
 }
 
 // ---------------------------------------------------------------------------
@@ -455,6 +473,105 @@ __global__ void __launch_bounds__(kBlock) k_sweep_gen_rp(const int32_t* __restri
     count_epilogue<VW, COUNT, kBlock, 10>(vc, active, unit, unit0, Us, lds_cnt, use_lds, counts);
 }
 
+// ---------------------------------------------------------------------------
+// Degree-class ELL sweep: the notebook's own ER layout (nb:113-117 sums
+// s[N_nodes_pos[d]] over the nodes nodes_with_d_positions[d] of each degree
+// class d; nb:359-361 builds them).  One launch per class: its `cnt` nodes
+// order[0..cnt) all have degree D and node order[k]'s neighbours are
+// cell[k*D .. k*D+D).  Against the CSR sweep this drops the row_ptr hop (the
+// chain is order/cell -> gather, as for the RRG) and, with D a template
+// parameter, the runtime bit counter (88 -> fewer VGPRs, more waves in
+// flight for a latency-bound gather).  D = -1: runtime degree `dd` (> 8).
+// ---------------------------------------------------------------------------
+template <int D, int VW, bool COUNT>
+__global__ void __launch_bounds__(kBlock) k_sweep_cls_rp(const int32_t* __restrict__ order,
+                                                         const int32_t* __restrict__ cell, int64_t cnt, int dd,
+                                                         int64_t W, const u64* __restrict__ s_in,
+                                                         u64* __restrict__ s_out,
+                                                         unsigned long long* __restrict__ counts, int use_lds,
+                                                         int64_t unit0, int64_t Us) {
+    extern __shared__ unsigned lds_cnt[];
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t slots = ((int64_t)gridDim.x * kBlock) / Us;
+    const int64_t unit = unit0 + t % Us, slot = t / Us;
+    const bool active = slot < slots;
+    VertCounter<VW> vc;
+    if constexpr (COUNT) {
+        vc.reset();
+        lds_count_init<VW>(lds_cnt, Us, use_lds);
+    }
+    if (active) {
+        for (int64_t i = slot; i < cnt; i += slots) {
+            const int64_t v = order[i];
+            u64 own[VW], out[VW];
+            if constexpr (D == 0) {
+                // no neighbours: S = 0, a tie, the spin stays (nb:113-117)
+                ldv<VW>(s_in + v * W + unit * VW, out);
+            } else if constexpr (D > 0) {
+                int32_t k[D];
+                load_adj<D>(cell, i, k);
+                u64 x[D][VW];
+#pragma unroll
+                for (int j = 0; j < D; ++j) ldv<VW>(s_in + (int64_t)k[j] * W + unit * VW, x[j]);
+                ldv<VW>(s_in + v * W + unit * VW, own);
+#pragma unroll
+                for (int q = 0; q < VW; ++q) {
+                    u64 xs[D];
+#pragma unroll
+                    for (int j = 0; j < D; ++j) xs[j] = x[j][q];
+                    out[q] = majority_fixed<D>(xs, own[q]);
+                }
+            } else {
+                const int32_t* row = cell + i * dd;
+                BitCounter<8> bc[VW];
+#pragma unroll
+                for (int q = 0; q < VW; ++q) bc[q].reset();
+                int j = 0;
+                for (; j + 4 <= dd; j += 4) {
+                    int32_t k[4];
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) k[m] = row[j + m];
+                    u64 x[4][VW];
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) ldv<VW>(s_in + (int64_t)k[m] * W + unit * VW, x[m]);
+#pragma unroll
+                    for (int m = 0; m < 4; ++m)
+#pragma unroll
+                        for (int q = 0; q < VW; ++q) bc[q].add(x[m][q]);
+                }
+                for (; j < dd; ++j) {
+                    u64 x[VW];
+                    ldv<VW>(s_in + (int64_t)row[j] * W + unit * VW, x);
+#pragma unroll
+                    for (int q = 0; q < VW; ++q) bc[q].add(x[q]);
+                }
+                ldv<VW>(s_in + v * W + unit * VW, own);
+#pragma unroll
+                for (int q = 0; q < VW; ++q) out[q] = bc[q].majority(dd, own[q]);
+            }
+            stv<VW>(s_out + v * W + unit * VW, out);
+            if constexpr (COUNT) {
+                vc.add(out);
+                if (vc.added == (1 << KC) - 1) flush_to(vc, use_lds, lds_cnt, counts, unit, unit0);
+            }
+        }
+    }
+    count_epilogue<VW, COUNT>(vc, active, unit, unit0, Us, lds_cnt, use_lds, counts);
+}
+
+// Fills the class-ELL cells of one class from CSR: cell[k*D + j] =
+// col[row_ptr[order[k]] + j], k < cnt.
+__global__ void __launch_bounds__(kBlock) k_class_ell_fill(const int64_t* __restrict__ row_ptr,
+                                                           const int32_t* __restrict__ col,
+                                                           const int32_t* __restrict__ order, int64_t cnt, int D,
+                                                           int32_t* __restrict__ cell) {
+    const int64_t total = cnt * D;
+    for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < total; e += (int64_t)gridDim.x * kBlock) {
+        const int64_t k = e / D, j = e - k * D;
+        cell[e] = col[row_ptr[order[k]] + j];
+    }
+}
+
 }  // namespace mjx
 
 // ---------------------------------------------------------------------------
@@ -623,15 +740,21 @@ static void launch_ell_rp_vw(const int32_t* adj, int64_t n, int d, int64_t W, co
                              unsigned long long* counts, int grid, size_t lds, int use_lds, int64_t unit0,
                              int64_t Us, hipStream_t st) {
     constexpr int BS = COUNT ? kCountBlock : kBlock;
-    const int g = COUNT ? (grid + kCountBlock / kBlock - 1) / (kCountBlock / kBlock) : grid;
+    (void)grid;
+    auto ell = [&](auto kern) {
+        const int g = resident_grid(kern, BS, lds, n * Us);
+        kern<<<g, BS, lds, st>>>(adj, n, W, in, out, counts, use_lds, unit0, Us);
+    };
     switch (d) {
-        case 3: k_sweep_ell_rp<3, VW, COUNT, BS><<<g, BS, lds, st>>>(adj, n, W, in, out, counts, use_lds, unit0, Us); break;
-        case 4: k_sweep_ell_rp<4, VW, COUNT, BS><<<g, BS, lds, st>>>(adj, n, W, in, out, counts, use_lds, unit0, Us); break;
-        case 6: k_sweep_ell_rp<6, VW, COUNT, BS><<<g, BS, lds, st>>>(adj, n, W, in, out, counts, use_lds, unit0, Us); break;
-        default:
-            k_sweep_gen_rp<VW, COUNT, false><<<grid, kBlock, lds, st>>>(adj, d, nullptr, nullptr, nullptr, n, W, in, out,
-                                                                       counts, use_lds, unit0, Us);
+        case 3: ell(k_sweep_ell_rp<3, VW, COUNT, BS>); break;
+        case 4: ell(k_sweep_ell_rp<4, VW, COUNT, BS>); break;
+        case 6: ell(k_sweep_ell_rp<6, VW, COUNT, BS>); break;
+        default: {
+            auto kern = k_sweep_gen_rp<VW, COUNT, false>;
+            const int g = resident_grid(kern, kBlock, lds, n * Us);
+            kern<<<g, kBlock, lds, st>>>(adj, d, nullptr, nullptr, nullptr, n, W, in, out, counts, use_lds, unit0, Us);
             break;
+        }
     }
 }
 
@@ -682,8 +805,12 @@ static int launch_sweep_csr_rp(const int64_t* rp, const int32_t* col, const int3
     int rc = rp_geometry(n, W, Us, &grid, &vw, &use_lds, &lds);
     if (rc) return rc;
     if (!counts) { lds = 0; use_lds = 0; }
-#define MJX_CSR(VWV, C) k_sweep_gen_rp<VWV, C, true><<<grid, kBlock, lds, st>>>(nullptr, 0, rp, col, order, n, W, in, \
-                                                                               out, counts, use_lds, unit0, Us)
+#define MJX_CSR(VWV, C)                                                                                      \
+    do {                                                                                                     \
+        auto kern = k_sweep_gen_rp<VWV, C, true>;                                                            \
+        grid = resident_grid(kern, kBlock, lds, n * Us);                                                     \
+        kern<<<grid, kBlock, lds, st>>>(nullptr, 0, rp, col, order, n, W, in, out, counts, use_lds, unit0, Us); \
+    } while (0)
     if (vw == 2) {
         if (counts) MJX_CSR(2, true); else MJX_CSR(2, false);
     } else {
@@ -845,6 +972,101 @@ extern "C" int mjx_rollout_csr_rp_ordered(const int64_t* row_ptr, const int32_t*
         if (rc) return rc;
     }
     return MJX_OK;
+}
+
+// ---- degree-class ELL ------------------------------------------------------
+
+static int check_classes(const int64_t* classes, int nclasses, int64_t n) {
+    if (nclasses < 0 || (nclasses > 0 && !classes)) return MJX_EINVAL;
+    int64_t covered = 0;
+    for (int c = 0; c < nclasses; ++c) {
+        const int64_t i0 = classes[4 * c], cnt = classes[4 * c + 1], D = classes[4 * c + 2], base = classes[4 * c + 3];
+        if (i0 < 0 || cnt < 0 || i0 + cnt > n || D < 0 || D > 255 || base < 0 || (base & 3)) return MJX_EINVAL;
+        covered += cnt;
+    }
+    return covered == n ? MJX_OK : MJX_EINVAL;
+}
+
+extern "C" int mjx_class_ell_fill(const int64_t* row_ptr, const int32_t* col, const int32_t* order,
+                                  const int64_t* classes, int nclasses, int64_t n, int32_t* cell, void* stream) {
+    if (n < 0 || (n > 0 && (!row_ptr || !order))) return MJX_EINVAL;
+    int rc = check_classes(classes, nclasses, n);
+    if (rc) return rc;
+    hipStream_t st = as_stream(stream);
+    for (int c = 0; c < nclasses; ++c) {
+        const int64_t i0 = classes[4 * c], cnt = classes[4 * c + 1], D = classes[4 * c + 2], base = classes[4 * c + 3];
+        if (cnt * D == 0) continue;
+        if (!col || !cell) return MJX_EINVAL;
+        k_class_ell_fill<<<grid_for(cnt * D), kBlock, 0, st>>>(row_ptr, col, order + i0, cnt, (int)D, cell + base);
+        MJX_LAUNCH_CHECK("class_ell_fill");
+    }
+    return MJX_OK;
+}
+
+template <int VW, bool COUNT>
+static int launch_sweep_cls_rp(const int32_t* order, const int32_t* cell, int64_t cnt, int D, int64_t W,
+                               const u64* in, u64* out, unsigned long long* counts, size_t lds, int use_lds,
+                               int64_t unit0, int64_t Us, hipStream_t st) {
+    auto go = [&](auto kern) {
+        const int g = resident_grid(kern, kBlock, lds, cnt * Us);
+        kern<<<g, kBlock, lds, st>>>(order, cell, cnt, D, W, in, out, counts, use_lds, unit0, Us);
+    };
+    switch (D) {
+        case 0: go(k_sweep_cls_rp<0, VW, COUNT>); break;
+        case 1: go(k_sweep_cls_rp<1, VW, COUNT>); break;
+        case 2: go(k_sweep_cls_rp<2, VW, COUNT>); break;
+        case 3: go(k_sweep_cls_rp<3, VW, COUNT>); break;
+        case 4: go(k_sweep_cls_rp<4, VW, COUNT>); break;
+        case 5: go(k_sweep_cls_rp<5, VW, COUNT>); break;
+        case 6: go(k_sweep_cls_rp<6, VW, COUNT>); break;
+        case 7: go(k_sweep_cls_rp<7, VW, COUNT>); break;
+        case 8: go(k_sweep_cls_rp<8, VW, COUNT>); break;
+        default: go(k_sweep_cls_rp<-1, VW, COUNT>); break;
+    }
+    MJX_LAUNCH_CHECK("sweep_cls_rp");
+    return MJX_OK;
+}
+
+extern "C" int mjx_rollout_class_rp(const int32_t* order, const int32_t* cell, const int64_t* classes,
+                                    int nclasses, int64_t n, int64_t words, const uint64_t* s_in,
+                                    uint64_t* s_out, uint64_t* tmp, int steps, unsigned long long* counts,
+                                    void* stream) {
+    if (n < 0 || words < 1 || (n > 0 && (!order || !s_in || !s_out))) return MJX_EINVAL;
+    if (n > (int64_t)INT32_MAX) return MJX_ERANGE;
+    if (overlaps(s_in, s_out) || overlaps(s_in, tmp) || overlaps(s_out, tmp)) return MJX_EINVAL;
+    int rc = check_classes(classes, nclasses, n);
+    if (rc) return rc;
+    if (n == 0) return MJX_OK;
+    for (int c = 0; c < nclasses; ++c)
+        if (classes[4 * c + 1] * classes[4 * c + 2] > 0 && !cell) return MJX_EINVAL;
+    hipStream_t st = as_stream(stream);
+    if (steps < 0) return MJX_EINVAL;
+    if (steps == 0) {
+        MJX_HIP(hipMemcpyAsync(s_out, s_in, (size_t)n * (size_t)words * 8, hipMemcpyDeviceToDevice, st),
+                "rollout copy");
+        return counts ? mjx_popcount_rp(s_out, n, words, counts, stream) : MJX_OK;
+    }
+    const int64_t Us = units_of(words);
+    int grid, vw, use_lds; size_t lds;
+    rc = rp_geometry(n, words, Us, &grid, &vw, &use_lds, &lds);
+    if (rc) return rc;
+    auto sweep = [&](const u64* a, u64* b, unsigned long long* cn) {
+        for (int c = 0; c < nclasses; ++c) {
+            const int64_t i0 = classes[4 * c], cnt = classes[4 * c + 1], base = classes[4 * c + 3];
+            const int D = (int)classes[4 * c + 2];
+            if (cnt == 0) continue;
+            const int32_t* o = order + i0;
+            const int32_t* cl = cell ? cell + base : nullptr;
+            int r;
+            if (vw == 2) r = cn ? launch_sweep_cls_rp<2, true>(o, cl, cnt, D, words, a, b, cn, lds, use_lds, 0, Us, st)
+                                : launch_sweep_cls_rp<2, false>(o, cl, cnt, D, words, a, b, cn, 0, 0, 0, Us, st);
+            else r = cn ? launch_sweep_cls_rp<1, true>(o, cl, cnt, D, words, a, b, cn, lds, use_lds, 0, Us, st)
+                        : launch_sweep_cls_rp<1, false>(o, cl, cnt, D, words, a, b, cn, 0, 0, 0, Us, st);
+            if (r) return r;
+        }
+        return (int)MJX_OK;
+    };
+    return run_rollout(steps, (const u64*)s_in, (u64*)s_out, (u64*)tmp, counts, sweep);
 }
 
 extern "C" int mjx_rollout_csr_rp(const int64_t* row_ptr, const int32_t* col, int64_t n, int64_t words,

@@ -80,6 +80,12 @@ def rollout(graph, bits, steps, words=None, out=None, tmp=None, counts=None, sli
         if words is None:
             _lib.call("mjx_rollout_csr_np", _device.ptr(graph.row_ptr), _device.ptr(graph.col), graph.n,
                       _device.ptr(bits), _device.ptr(out), tptr, int(steps), cptr, st)
+        elif graph.rp_layout == "class":
+            # degree-class ELL (nb:113-117's own layout), built once per graph
+            order, cell, classes = graph.class_ell()
+            _lib.call("mjx_rollout_class_rp", _device.ptr(order), _device.ptr(cell) if cell.numel() else None,
+                      classes.ctypes.data, classes.shape[0], graph.n, int(words),
+                      _device.ptr(bits), _device.ptr(out), tptr, int(steps), cptr, st)
         else:
             _lib.call("mjx_rollout_csr_rp_ordered", _device.ptr(graph.row_ptr), _device.ptr(graph.col),
                       _device.ptr(graph.order) if graph.order is not None else None, graph.n, int(words),

@@ -281,6 +281,37 @@ class Graph:
         self.kind, self.n, self.d = kind, int(n), d
         self.adj, self.row_ptr, self.col = adj, row_ptr, col
         self.order = order          # CSR: nodes sorted by degree (visiting order of the rp sweep)
+        # CSR replica-packed sweeps: "class" = degree-class ELL (class_ell), "csr" = row_ptr/col
+        self.rp_layout = "class"
+        self._class_ell = None
+
+    def class_ell(self):
+        """Degree-class ELL of a CSR graph, the notebook's ER layout
+        (``nodes_with_d_positions[d]`` / ``N_nodes_pos[d]``, nb:359-361, used by
+        ``onestep_majority`` nb:113-117): ``(order, cell, classes)`` where
+        ``order`` (device int32) lists the nodes by degree, ``classes`` (host
+        int64, rows ``i0, count, D, base``) the runs of one degree, and
+        ``cell`` (device int32) row k of a class at ``base + k*D``.  Built once
+        (mjx_class_ell_fill), cached."""
+        if self._class_ell is None:
+            from . import _lib
+            if self.kind != "csr":
+                raise ValueError("class_ell needs a CSR graph")
+            deg = self.row_ptr[1:] - self.row_ptr[:-1]
+            degs, cnts = torch.unique_consecutive(deg[self.order.long()], return_counts=True)
+            degs, cnts = degs.cpu().numpy().astype(np.int64), cnts.cpu().numpy().astype(np.int64)
+            rows, i0, base = [], 0, 0
+            for D, c in zip(degs, cnts):
+                rows.append((i0, c, D, base))
+                i0 += c
+                base += -(-(c * D) // 4) * 4          # next class at a multiple of 4 (int4 row loads)
+            classes = np.ascontiguousarray(np.array(rows, dtype=np.int64).reshape(-1, 4))
+            cell = torch.empty(max(base, 1), dtype=torch.int32, device=self.row_ptr.device)
+            _lib.call("mjx_class_ell_fill", _device.ptr(self.row_ptr), _device.ptr(self.col) if self.nnz else None,
+                      _device.ptr(self.order), classes.ctypes.data, classes.shape[0], self.n, _device.ptr(cell),
+                      _device.stream_handle())
+            self._class_ell = (self.order, cell, classes)
+        return self._class_ell
 
     @classmethod
     def ell(cls, adj):

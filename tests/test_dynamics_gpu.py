@@ -98,6 +98,50 @@ def test_er_with_isolated_and_high_degree(mjx_mod):
         assert np.array_equal(mjx_mod.s_endstate(g, S0[3], T, 1), want[3])
 
 
+@pytest.mark.parametrize("R", [64, 128, 192, 4096])
+def test_class_ell_equals_csr_layout(mjx_mod, R):
+    """The degree-class ELL sweep (nb:113-117's per-class layout; every class
+    kernel D = 0..8 and the runtime-degree one) against the CSR sweep and the
+    oracle, fused counts included; W odd (R=192) takes the 8-byte units."""
+    n = 2500
+    rng = np.random.default_rng(R)
+    u, v = rng.integers(0, n, 5000), rng.integers(0, n, 5000)
+    hub_u = np.zeros(40, np.int64) + 11
+    hub_v = rng.choice(np.arange(12, n), 40, replace=False)
+    a, b = np.r_[u, hub_u], np.r_[v, hub_v]
+    keep = a != b
+    key = np.unique(np.minimum(a, b)[keep] * n + np.maximum(a, b)[keep])
+    rp, col = mjx_mod.csr_from_edges(n, key // n, key % n)
+    degs = set(np.diff(rp).tolist())
+    assert set(range(9)) <= degs and max(degs) > 8
+    g = mjx_mod.Graph.csr(rp, col)
+    order, cell, classes = g.class_ell()
+    assert classes[:, 1].sum() == n and (classes[:, 3] % 4 == 0).all()
+    o = order.cpu().numpy()
+    c = cell.cpu().numpy()
+    for i0, cnt, D, base in classes:           # rows of the class cells are the CSR rows
+        for k in (0, cnt // 2, cnt - 1):
+            vtx = o[i0 + k]
+            assert D == rp[vtx + 1] - rp[vtx]
+            assert np.array_equal(c[base + k * D: base + k * D + D], col[rp[vtx]:rp[vtx + 1]])
+    W = (R + 63) // 64
+    S0 = 2 * rng.integers(0, 2, size=(R, n)).astype(np.int64) - 1
+    bits = mjx_mod.pack(S0)
+    for T in (1, 2, 3):
+        res = {}
+        for layout in ("class", "csr"):
+            g.rp_layout = layout
+            cnt = torch.zeros(W * 64, dtype=torch.int64, device="cuda")
+            out = mjx_mod.rollout(g, bits, T, words=W, counts=cnt)
+            res[layout] = (out.cpu().numpy(), cnt.cpu().numpy())
+        g.rp_layout = "class"
+        assert np.array_equal(res["class"][0], res["csr"][0]), T
+        assert np.array_equal(res["class"][1], res["csr"][1]), T
+        want = orc.s_endstate_er(rp, col, S0, T, 1)
+        assert np.array_equal(res["class"][1][:R], (want > 0).sum(axis=1)), T
+        assert np.array_equal(mjx_mod.s_endstate(g, S0, T, 1), want), T
+
+
 def test_pack_unpack_roundtrip(mjx_mod):
     rng = np.random.default_rng(1)
     for (R, n) in [(1, 1), (1, 65), (3, 1000), (64, 777), (65, 300), (4096, 50)]:
