@@ -13,6 +13,8 @@
 #include <string.h>
 #include <stdio.h>
 #include <mutex>
+#include <stdlib.h>
+#include <math.h>
 
 namespace mjx {
 
@@ -483,7 +485,7 @@ __global__ void __launch_bounds__(kBlock) k_sweep_gen_rp(const int32_t* __restri
 // parameter, the runtime bit counter (88 -> fewer VGPRs, more waves in
 // flight for a latency-bound gather).  D = -1: runtime degree `dd` (> 8).
 // ---------------------------------------------------------------------------
-template <int D, int VW, bool COUNT>
+template <int D, int VW, bool COUNT, int NK = KC>
 __global__ void __launch_bounds__(kBlock) k_sweep_cls_rp(const int32_t* __restrict__ order,
                                                          const int32_t* __restrict__ cell, int64_t cnt, int dd,
                                                          int64_t W, const u64* __restrict__ s_in,
@@ -495,7 +497,7 @@ __global__ void __launch_bounds__(kBlock) k_sweep_cls_rp(const int32_t* __restri
     const int64_t slots = ((int64_t)gridDim.x * kBlock) / Us;
     const int64_t unit = unit0 + t % Us, slot = t / Us;
     const bool active = slot < slots;
-    VertCounter<VW> vc;
+    VertCounter<VW, NK> vc;
     if constexpr (COUNT) {
         vc.reset();
         lds_count_init<VW>(lds_cnt, Us, use_lds);
@@ -552,11 +554,11 @@ __global__ void __launch_bounds__(kBlock) k_sweep_cls_rp(const int32_t* __restri
             stv<VW>(s_out + v * W + unit * VW, out);
             if constexpr (COUNT) {
                 vc.add(out);
-                if (vc.added == (1 << KC) - 1) flush_to(vc, use_lds, lds_cnt, counts, unit, unit0);
+                if (vc.added == (1 << NK) - 1) flush_to(vc, use_lds, lds_cnt, counts, unit, unit0);
             }
         }
     }
-    count_epilogue<VW, COUNT>(vc, active, unit, unit0, Us, lds_cnt, use_lds, counts);
+    count_epilogue<VW, COUNT, kBlock, NK>(vc, active, unit, unit0, Us, lds_cnt, use_lds, counts);
 }
 
 // Fills the class-ELL cells of one class from CSR: cell[k*D + j] =
@@ -1011,18 +1013,20 @@ static int launch_sweep_cls_rp(const int32_t* order, const int32_t* cell, int64_
         const int g = resident_grid(kern, kBlock, lds, cnt * Us);
         kern<<<g, kBlock, lds, st>>>(order, cell, cnt, D, W, in, out, counts, use_lds, unit0, Us);
     };
+#define MJX_CLS(DD) go(k_sweep_cls_rp<DD, VW, COUNT>)
     switch (D) {
-        case 0: go(k_sweep_cls_rp<0, VW, COUNT>); break;
-        case 1: go(k_sweep_cls_rp<1, VW, COUNT>); break;
-        case 2: go(k_sweep_cls_rp<2, VW, COUNT>); break;
-        case 3: go(k_sweep_cls_rp<3, VW, COUNT>); break;
-        case 4: go(k_sweep_cls_rp<4, VW, COUNT>); break;
-        case 5: go(k_sweep_cls_rp<5, VW, COUNT>); break;
-        case 6: go(k_sweep_cls_rp<6, VW, COUNT>); break;
-        case 7: go(k_sweep_cls_rp<7, VW, COUNT>); break;
-        case 8: go(k_sweep_cls_rp<8, VW, COUNT>); break;
-        default: go(k_sweep_cls_rp<-1, VW, COUNT>); break;
+        case 0: MJX_CLS(0); break;
+        case 1: MJX_CLS(1); break;
+        case 2: MJX_CLS(2); break;
+        case 3: MJX_CLS(3); break;
+        case 4: MJX_CLS(4); break;
+        case 5: MJX_CLS(5); break;
+        case 6: MJX_CLS(6); break;
+        case 7: MJX_CLS(7); break;
+        case 8: MJX_CLS(8); break;
+        default: MJX_CLS(-1); break;
     }
+#undef MJX_CLS
     MJX_LAUNCH_CHECK("sweep_cls_rp");
     return MJX_OK;
 }
