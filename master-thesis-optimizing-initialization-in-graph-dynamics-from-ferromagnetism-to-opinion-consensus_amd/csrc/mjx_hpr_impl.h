@@ -168,20 +168,25 @@ __device__ __forceinline__ S xa_messages(const S* __restrict__ rows, const S* __
     } else {
 #pragma unroll
         for (int x = 0; x < X; ++x) tab[TB::v.xo[x]] = M[0][x];
+        // in place, sources in decreasing index: every target i + xo[x] > i has
+        // already given up its own value, and the all-(-1) trajectory (xo = 0)
+        // rescales the source itself (one table live instead of two: VGPRs)
 #pragma unroll
         for (int j = 1; j < K; ++j) {
-            S nxt[NS];
 #pragma unroll
-            for (int i = 0; i < NS; ++i) nxt[i] = S(0);
-#pragma unroll
-            for (int i = 0; i < NS; ++i) {
+            for (int i = NS - 1; i >= 0; --i) {
                 if (TB::v.maxd[i] <= j) {   // table holds j neighbours: digits <= j
+                    const S t = tab[i];
 #pragma unroll
-                    for (int x = 0; x < X; ++x) nxt[i + TB::v.xo[x]] += tab[i] * M[j][x];
+                    for (int x = 0; x < X; ++x) {
+                        if (TB::v.xo[x] == 0) tab[i] = t * M[j][x];
+                    }
+#pragma unroll
+                    for (int x = 0; x < X; ++x) {
+                        if (TB::v.xo[x] != 0) tab[i + TB::v.xo[x]] += t * M[j][x];
+                    }
                 }
             }
-#pragma unroll
-            for (int i = 0; i < NS; ++i) tab[i] = nxt[i];
         }
     }
     // directional cumulative sums: suffix in dims whose target spin is +1, prefix otherwise
