@@ -561,6 +561,78 @@ __global__ void __launch_bounds__(kBlock) k_sweep_cls_rp(const int32_t* __restri
     count_epilogue<VW, COUNT, kBlock, NK>(vc, active, unit, unit0, Us, lds_cnt, use_lds, counts);
 }
 
+// The classes above D = 8 (few nodes each: Poisson tail) in one launch: a
+// table of consecutive classes, each thread walks its positions in increasing
+// order with a forward class cursor.  One launch (and one count epilogue)
+// instead of one per class.
+constexpr int kMaxGen = 32;
+struct GenTable {
+    int nc;
+    int D[kMaxGen];
+    int64_t i0[kMaxGen + 1];   // positions relative to the first class; i0[nc] = end
+    int64_t base[kMaxGen];
+};
+
+template <int VW, bool COUNT>
+__global__ void __launch_bounds__(kBlock) k_sweep_cls_gen_rp(const int32_t* __restrict__ order,
+                                                             const int32_t* __restrict__ cell, GenTable tab,
+                                                             int64_t W, const u64* __restrict__ s_in,
+                                                             u64* __restrict__ s_out,
+                                                             unsigned long long* __restrict__ counts, int use_lds,
+                                                             int64_t Us) {
+    extern __shared__ unsigned lds_cnt[];
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t slots = ((int64_t)gridDim.x * kBlock) / Us;
+    const int64_t unit = t % Us, slot = t / Us;
+    const bool active = slot < slots;
+    VertCounter<VW> vc;
+    if constexpr (COUNT) {
+        vc.reset();
+        lds_count_init<VW>(lds_cnt, Us, use_lds);
+    }
+    if (active) {
+        int c = 0;
+        for (int64_t i = slot; i < tab.i0[tab.nc]; i += slots) {
+            while (i >= tab.i0[c + 1]) ++c;
+            const int dd = tab.D[c];
+            const int32_t* row = cell + tab.base[c] + (i - tab.i0[c]) * dd;
+            const int64_t v = order[i];
+            BitCounter<8> bc[VW];
+#pragma unroll
+            for (int q = 0; q < VW; ++q) bc[q].reset();
+            int j = 0;
+            for (; j + 4 <= dd; j += 4) {
+                int32_t k[4];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) k[m] = row[j + m];
+                u64 x[4][VW];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) ldv<VW>(s_in + (int64_t)k[m] * W + unit * VW, x[m]);
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+#pragma unroll
+                    for (int q = 0; q < VW; ++q) bc[q].add(x[m][q]);
+            }
+            for (; j < dd; ++j) {
+                u64 x[VW];
+                ldv<VW>(s_in + (int64_t)row[j] * W + unit * VW, x);
+#pragma unroll
+                for (int q = 0; q < VW; ++q) bc[q].add(x[q]);
+            }
+            u64 own[VW], out[VW];
+            ldv<VW>(s_in + v * W + unit * VW, own);
+#pragma unroll
+            for (int q = 0; q < VW; ++q) out[q] = bc[q].majority(dd, own[q]);
+            stv<VW>(s_out + v * W + unit * VW, out);
+            if constexpr (COUNT) {
+                vc.add(out);
+                if (vc.added == (1 << KC) - 1) flush_to(vc, use_lds, lds_cnt, counts, unit, 0);
+            }
+        }
+    }
+    count_epilogue<VW, COUNT>(vc, active, unit, 0, Us, lds_cnt, use_lds, counts);
+}
+
 // Fills the class-ELL cells of one class from CSR: cell[k*D + j] =
 // col[row_ptr[order[k]] + j], k < cnt.
 __global__ void __launch_bounds__(kBlock) k_class_ell_fill(const int64_t* __restrict__ row_ptr,
@@ -1005,12 +1077,33 @@ extern "C" int mjx_class_ell_fill(const int64_t* row_ptr, const int32_t* col, co
     return MJX_OK;
 }
 
+// Counting launches end with Us*VW*64 global count atomics per block (4096
+// at R = 4096, ~100 us for a 2048-block grid): a small class gets at most one
+// block per kClsCountNodes nodes per thread slot.
+constexpr int64_t kClsCountNodes = 16;
+static int64_t cls_count_threads(int64_t cnt, int64_t Us) {
+    const int64_t slots = (cnt + kClsCountNodes - 1) / kClsCountNodes;
+    return (slots < 1 ? 1 : slots) * Us;
+}
+
+template <int VW, bool COUNT>
+static int launch_sweep_cls_gen_rp(const int32_t* order, const int32_t* cell, const GenTable& tab, int64_t W,
+                                   const u64* in, u64* out, unsigned long long* counts, size_t lds, int use_lds,
+                                   int64_t Us, hipStream_t st) {
+    auto kern = k_sweep_cls_gen_rp<VW, COUNT>;
+    const int64_t cnt = tab.i0[tab.nc];
+    const int g = resident_grid(kern, kBlock, lds, COUNT ? cls_count_threads(cnt, Us) : cnt * Us);
+    kern<<<g, kBlock, lds, st>>>(order, cell, tab, W, in, out, counts, use_lds, Us);
+    MJX_LAUNCH_CHECK("sweep_cls_gen_rp");
+    return MJX_OK;
+}
+
 template <int VW, bool COUNT>
 static int launch_sweep_cls_rp(const int32_t* order, const int32_t* cell, int64_t cnt, int D, int64_t W,
                                const u64* in, u64* out, unsigned long long* counts, size_t lds, int use_lds,
                                int64_t unit0, int64_t Us, hipStream_t st) {
     auto go = [&](auto kern) {
-        const int g = resident_grid(kern, kBlock, lds, cnt * Us);
+        const int g = resident_grid(kern, kBlock, lds, COUNT ? cls_count_threads(cnt, Us) : cnt * Us);
         kern<<<g, kBlock, lds, st>>>(order, cell, cnt, D, W, in, out, counts, use_lds, unit0, Us);
     };
 #define MJX_CLS(DD) go(k_sweep_cls_rp<DD, VW, COUNT>)
@@ -1055,10 +1148,36 @@ extern "C" int mjx_rollout_class_rp(const int32_t* order, const int32_t* cell, c
     rc = rp_geometry(n, words, Us, &grid, &vw, &use_lds, &lds);
     if (rc) return rc;
     auto sweep = [&](const u64* a, u64* b, unsigned long long* cn) {
+        // runs of consecutive classes with D > 8 (adjacent in `order`) share one launch
+        GenTable tab{};
+        int64_t g0 = 0;
+        auto flush_gen = [&]() -> int {
+            if (tab.nc == 0) return MJX_OK;
+            const int32_t* o = order + g0;
+            int r;
+            if (vw == 2) r = cn ? launch_sweep_cls_gen_rp<2, true>(o, cell, tab, words, a, b, cn, lds, use_lds, Us, st)
+                                : launch_sweep_cls_gen_rp<2, false>(o, cell, tab, words, a, b, cn, 0, 0, Us, st);
+            else r = cn ? launch_sweep_cls_gen_rp<1, true>(o, cell, tab, words, a, b, cn, lds, use_lds, Us, st)
+                        : launch_sweep_cls_gen_rp<1, false>(o, cell, tab, words, a, b, cn, 0, 0, Us, st);
+            tab.nc = 0;
+            return r;
+        };
         for (int c = 0; c < nclasses; ++c) {
             const int64_t i0 = classes[4 * c], cnt = classes[4 * c + 1], base = classes[4 * c + 3];
             const int D = (int)classes[4 * c + 2];
             if (cnt == 0) continue;
+            if (D > 8) {
+                if (tab.nc > 0 && (tab.nc == kMaxGen || g0 + tab.i0[tab.nc] != i0)) {
+                    int r = flush_gen();
+                    if (r) return r;
+                }
+                if (tab.nc == 0) { g0 = i0; tab.i0[0] = 0; }
+                tab.D[tab.nc] = D;
+                tab.base[tab.nc] = base;
+                tab.i0[tab.nc + 1] = i0 - g0 + cnt;
+                ++tab.nc;
+                continue;
+            }
             const int32_t* o = order + i0;
             const int32_t* cl = cell ? cell + base : nullptr;
             int r;
@@ -1068,7 +1187,7 @@ extern "C" int mjx_rollout_class_rp(const int32_t* order, const int32_t* cell, c
                         : launch_sweep_cls_rp<1, false>(o, cl, cnt, D, words, a, b, cn, 0, 0, 0, Us, st);
             if (r) return r;
         }
-        return (int)MJX_OK;
+        return flush_gen();
     };
     return run_rollout(steps, (const u64*)s_in, (u64*)s_out, (u64*)tmp, counts, sweep);
 }
