@@ -52,6 +52,32 @@ def test_invalid_arguments_return_status_without_gpu(mjx_mod):
     assert lib.mjx_strerror(EINVAL) == b"invalid argument"
 
 
+def test_class_table_validation_without_gpu(mjx_mod):
+    """mjx_rollout_class_rp / mjx_class_ell_fill reject a malformed degree-class
+    table before touching the device (counts must cover n, D <= 255, 16-B
+    aligned bases)."""
+    import ctypes
+    import numpy as np
+    lib = mjx_mod.load_library()
+    EINVAL = 1
+    fake = ctypes.c_void_p(16)      # never dereferenced: validation fails first
+
+    def table(rows):
+        a = np.ascontiguousarray(np.array(rows, dtype=np.int64).reshape(-1, 4))
+        return a, a.ctypes.data
+
+    for rows in ([(0, 5, 3, 0)],                      # covers 5 of 10 nodes
+                 [(0, 4, 3, 0), (4, 6, 300, 12)],     # D > 255
+                 [(0, 4, 3, 0), (4, 6, 2, 13)],       # base not a multiple of 4
+                 [(0, 4, 3, 0), (4, 7, 2, 12)]):      # runs past n
+        a, ptr = table(rows)
+        assert lib.mjx_rollout_class_rp(fake, fake, ptr, a.shape[0], 10, 1, fake, ctypes.c_void_p(32), None, 1,
+                                        None, None) == EINVAL, rows
+        assert lib.mjx_class_ell_fill(fake, fake, fake, ptr, a.shape[0], 10, fake, None) == EINVAL, rows
+    assert lib.mjx_rollout_class_rp(fake, fake, None, 1, 10, 1, fake, ctypes.c_void_p(32), None, 1,
+                                    None, None) == EINVAL
+
+
 def test_product_path_fails_loudly_without_gpu(mjx_mod):
     import numpy as np
     import torch
