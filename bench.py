@@ -218,6 +218,7 @@ def bench_er(args, rank, world, dist, dev):
         "ms_per_step": 1e3 * el / K,
         "node_updates_per_s": world * n * R * T * K / el,
         "algorithmic_GBps_per_gpu": bytes_per_sweep * T * K / el / 1e9,
+        "frac_of_hbm_peak": bytes_per_sweep * T * K / el / 1e9 / HBM_PEAK_GBS,
     }
 
 
@@ -311,6 +312,7 @@ def bench_hpr(args, rank, world, dist, dev):
            "hpr_dp_ms": upd_ms, "marginals_ms": marg_ms,
            "messages_per_s": world * msgs * K / el,
            "hpr_dp_algorithmic_GBps": bytes_per_iter / (upd_ms / 1e3) / 1e9,
+           "hpr_dp_frac_of_hbm_peak": bytes_per_iter / (upd_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
            "hpr_dp_bytes_per_iter": bytes_per_iter}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import hpr as ohpr
