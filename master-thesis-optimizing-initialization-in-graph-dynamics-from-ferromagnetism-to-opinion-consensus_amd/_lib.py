@@ -68,6 +68,7 @@ _RESTYPES = {"mjx_strerror": ctypes.c_char_p, "mjx_last_hip_error": ctypes.c_cha
              "mjx_sa_lightcone_lds": c_i64, "mjx_bdcm_lds_bytes": c_i64,
              "mjx_rrg_partner_host": c_i64, "mjx_er_work_bytes": c_i64}
 
+MJX_OK, MJX_EINVAL, MJX_EHIP, MJX_ERANGE = 0, 1, 2, 3      # status codes (include/mjx.h)
 MJX_I8, MJX_I32, MJX_I64 = 1, 4, 8
 MJX_F32, MJX_F64 = 104, 108
 

@@ -237,16 +237,17 @@ def erdos_renyi_device(n, p, seed=0, drop_isolated=False):
     mean = n * (n - 1) * p                       # E[2 * edges]
     cap = int(mean + 12 * math.sqrt(2 * mean + 1) + 64)
     n_out, nnz = ctypes.c_int64(0), ctypes.c_int64(0)
-    for _ in range(2):
+    rc = 0
+    for attempt in range(2):
         col = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
         rc = _lib.load().mjx_er_generate(n, p, int(seed) & 0xFFFFFFFFFFFFFFFF, int(bool(drop_isolated)),
                                          _device.ptr(row_ptr), _device.ptr(col), cap, ctypes.byref(n_out),
                                          ctypes.byref(nnz), _device.ptr(work), work.numel(), _device.stream_handle())
-        if rc == 3 and nnz.value > cap:          # MJX_ERANGE: a (very) unlikely edge count, retry at its size
-            cap = int(nnz.value)
+        if rc == _lib.MJX_ERANGE and nnz.value > cap and attempt == 0:
+            cap = int(nnz.value)                 # a (very) unlikely edge count: retry once at its size
             continue
-        _lib.check(rc, "mjx_er_generate")
         break
+    _lib.check(rc, "mjx_er_generate")            # never build a Graph from a failed generate
     del work
     g = Graph.csr_device(row_ptr[:n_out.value + 1], col[:nnz.value])
     return (g, n - n_out.value) if drop_isolated else g

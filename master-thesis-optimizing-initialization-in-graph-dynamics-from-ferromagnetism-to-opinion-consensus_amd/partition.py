@@ -193,18 +193,15 @@ class ShardedRRG:
 
     def exchange(self, buf, g=0):
         """All-gather piece g of every rank into the replicated state (in place).
-        Returns the pending RCCL work (or None): the caller waits on it before
-        the state is read again."""
+        Returns the pending collective (or None): the caller waits on it before
+        the state is read again.  One code path for every backend: RCCL on the
+        GPU runs it on its own stream so piece g+1's sweep overlaps it; gloo (the
+        CPU tests) runs the identical in-place call."""
         if self.world == 1:
             return None
         r = self.range
         whole, mine = buf[r.piece_words(g)], buf[r.own_words(g)]
-        if self.backend == "nccl":
-            return self.dist.all_gather_into_tensor(whole, mine, group=self.group, async_op=True)
-        parts = [torch.empty_like(mine) for _ in range(self.world)]
-        self.dist.all_gather(parts, mine.clone(), group=self.group)
-        whole.view(self.world, r.sub).copy_(torch.stack(parts))
-        return None
+        return self.dist.all_gather_into_tensor(whole, mine, group=self.group, async_op=True)
 
     # -- state ------------------------------------------------------------------
     @property

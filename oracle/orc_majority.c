@@ -1,0 +1,191 @@
+/* ORACLE — test infrastructure only (never linked into libmjx.so, never on the
+ * product path).  Plain-C restatement of the reference's majority path, used by
+ * tests/ as a fast checker at the BASELINE configs' sizes (where the numpy
+ * restatement in oracle/majority.py takes minutes per SA replica).
+ *
+ * Follows, function by function (paths relative to the reference repository):
+ *   orc_onestep_ell     code/SA_RRG.py:18-20   (1-|sign S|)*s + sign S
+ *   orc_s_endstate_ell  code/SA_RRG.py:23-26   p+c-1 steps
+ *   orc_onestep_csr     code/ER_BDCM_entropy.ipynb raw lines 113-117  sign(2S+s)
+ *   orc_s_endstate_csr  same notebook, lines 120-123
+ *   orc_sa_loop         code/SA_RRG.py:63-88 (E_delta :32-37, m :39-40), with
+ *                       numpy's legacy global MT19937 stream (np.random.seed,
+ *                       binomial(1,.5), randint(0,n), rand) restated as in
+ *                       oracle/mt19937.py.
+ * It does exactly what the reference does per proposal (three full rollouts:
+ * s_endstate(s), s_endstate(s with s_i flipped), s_endstate(s) after the
+ * step); no light-cone shortcut.  Pinned against the numpy oracle and the
+ * reference-generated fixtures in tests/test_oracle_c.py.
+ *
+ * Build: oracle/build_oracle.py (gcc -O2 -ffp-contract=off -shared).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ---- MT19937 + numpy legacy distributions (oracle/mt19937.py) ------------ */
+typedef struct {
+    uint32_t mt[624];
+    int idx;
+} orc_mt;
+
+static void mt_seed(orc_mt* s, uint32_t seed)
+{
+    s->mt[0] = seed;
+    for (int i = 1; i < 624; ++i)
+        s->mt[i] = 1812433253u * (s->mt[i - 1] ^ (s->mt[i - 1] >> 30)) + (uint32_t)i;
+    s->idx = 624;
+}
+
+static uint32_t mt_u32(orc_mt* s)
+{
+    if (s->idx >= 624) {
+        for (int k = 0; k < 624; ++k) {
+            uint32_t y = (s->mt[k] & 0x80000000u) | (s->mt[(k + 1) % 624] & 0x7FFFFFFFu);
+            s->mt[k] = s->mt[(k + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908B0DFu : 0u);
+        }
+        s->idx = 0;
+    }
+    uint32_t y = s->mt[s->idx++];
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9D2C5680u;
+    y ^= (y << 15) & 0xEFC60000u;
+    y ^= y >> 18;
+    return y;
+}
+
+static double mt_double(orc_mt* s)
+{
+    uint32_t a = mt_u32(s) >> 5, b = mt_u32(s) >> 6;
+    return ((double)a * 67108864.0 + (double)b) / 9007199254740992.0;
+}
+
+static int64_t mt_randint(orc_mt* s, int64_t n)
+{
+    uint32_t rng = (uint32_t)(n - 1);
+    if (rng == 0) return 0;
+    uint32_t mask = rng;
+    mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+    for (;;) {
+        uint32_t v = mt_u32(s) & mask;
+        if (v <= rng) return v;
+    }
+}
+
+/* ---- dynamics -------------------------------------------------------------- */
+void orc_onestep_ell(const int32_t* adj, int64_t n, int d, const int8_t* s, int8_t* out)
+{
+    for (int64_t i = 0; i < n; ++i) {
+        int S = 0;
+        for (int k = 0; k < d; ++k) S += s[adj[i * d + k]];
+        out[i] = S > 0 ? 1 : (S < 0 ? -1 : s[i]);
+    }
+}
+
+/* s_endstate: `steps` sweeps from s0 into out; returns sum(out). */
+int64_t orc_s_endstate_ell(const int32_t* adj, int64_t n, int d, const int8_t* s0, int steps, int8_t* out,
+                           int8_t* tmp)
+{
+    const int8_t* cur = s0;
+    for (int t = 0; t < steps; ++t) {
+        int8_t* dst = ((steps - 1 - t) % 2 == 0) ? out : tmp;
+        orc_onestep_ell(adj, n, d, cur, dst);
+        cur = dst;
+    }
+    if (steps == 0) memcpy(out, s0, (size_t)n);
+    int64_t sum = 0;
+    for (int64_t i = 0; i < n; ++i) sum += out[i];
+    return sum;
+}
+
+void orc_onestep_csr(const int64_t* row_ptr, const int32_t* col, int64_t n, const int8_t* s, int8_t* out)
+{
+    for (int64_t i = 0; i < n; ++i) {
+        int64_t S = 0;
+        for (int64_t k = row_ptr[i]; k < row_ptr[i + 1]; ++k) S += s[col[k]];
+        int64_t x = 2 * S + s[i];
+        out[i] = x > 0 ? 1 : (x < 0 ? -1 : 0);
+    }
+}
+
+int64_t orc_s_endstate_csr(const int64_t* row_ptr, const int32_t* col, int64_t n, const int8_t* s0, int steps,
+                           int8_t* out, int8_t* tmp)
+{
+    const int8_t* cur = s0;
+    for (int t = 0; t < steps; ++t) {
+        int8_t* dst = ((steps - 1 - t) % 2 == 0) ? out : tmp;
+        orc_onestep_csr(row_ptr, col, n, cur, dst);
+        cur = dst;
+    }
+    if (steps == 0) memcpy(out, s0, (size_t)n);
+    int64_t sum = 0;
+    for (int64_t i = 0; i < n; ++i) sum += out[i];
+    return sum;
+}
+
+/* ---- SA loop (code/SA_RRG.py:63-88) ----------------------------------------
+ * One replica on numpy's stream after np.random.seed(seed).  Stops at
+ * consensus, at the t > 2n^3 cap, or after max_steps (< 0: no limit).
+ * Per-step traces (length >= max_steps when given): proposal i, accept,
+ * sum(s_endstate) after the step, delta_H.  conf receives the final s.
+ * Returns the number of steps taken; *done = 1 consensus, 2 cap, 0 stopped. */
+int64_t orc_sa_loop(const int32_t* adj, int64_t n, int d, int p, int c, uint32_t seed, double par_a, double par_b,
+                    int64_t max_steps, int32_t* tr_i, int8_t* tr_acc, int64_t* tr_sum, double* tr_dE, int8_t* conf,
+                    int32_t* done)
+{
+    int T = p + c - 1;
+    int8_t* s = (int8_t*)malloc((size_t)n);
+    int8_t* s2 = (int8_t*)malloc((size_t)n);
+    int8_t* e1 = (int8_t*)malloc((size_t)n);
+    int8_t* tmp = (int8_t*)malloc((size_t)n);
+    orc_mt rs;
+    mt_seed(&rs, seed);
+    for (int64_t i = 0; i < n; ++i) s[i] = mt_double(&rs) > 0.5 ? 1 : -1;      /* :65 */
+    double a = 0.015 * (double)n, b = 0.01 * (double)n;                        /* :67-68 */
+    double a_cap = 4.5 * (double)n, b_cap = 5.0 * (double)n;                   /* :80-81 */
+    /* 2*n**3 (:84) in Python integers; n <= 2^21 keeps it inside int64 */
+    int64_t t_cap = 2 * n * n * n;
+    int64_t t = 0;
+    int64_t sum_end = orc_s_endstate_ell(adj, n, d, s, T, e1, tmp);            /* :71 */
+    *done = 0;
+    while (sum_end < n) {                                                      /* :72, m < 1 */
+        if (max_steps >= 0 && t >= max_steps) break;
+        int64_t i = mt_randint(&rs, n);                                        /* :73 */
+        /* E_delta (:32-37): two rollouts, the flipped one on a copy */
+        int64_t sum1 = orc_s_endstate_ell(adj, n, d, s, T, e1, tmp);
+        memcpy(s2, s, (size_t)n);
+        s2[i] = (int8_t)-s2[i];
+        int64_t sum2 = orc_s_endstate_ell(adj, n, d, s2, T, e1, tmp);
+        volatile double m2a = -2.0 * a;                   /* (-2*a)*s0[i] + b*(diff), then /n */
+        volatile double x1 = m2a * (double)s[i];
+        volatile double x2 = b * (double)(sum1 - sum2);
+        volatile double x3 = x1 + x2;
+        double dH = x3 / (double)n;
+        double prob = exp(-dH);                                                /* :75 min([1, exp]) */
+        if (prob > 1.0) prob = 1.0;
+        double u = mt_double(&rs);                                             /* :76 */
+        int acc = u < prob;
+        if (acc) s[i] = (int8_t)-s[i];                                         /* :77 */
+        if (a < a_cap) a = par_a * a;                                          /* :80 */
+        if (b < b_cap) b = par_b * b;                                          /* :81 */
+        t += 1;                                                                /* :82 */
+        if (t > t_cap) {                                                       /* :84 */
+            *done = 2;
+        } else {
+            sum_end = orc_s_endstate_ell(adj, n, d, s, T, e1, tmp);            /* :85 */
+            if (sum_end >= n) *done = 1;
+        }
+        if (tr_i) {
+            tr_i[t - 1] = (int32_t)i;
+            tr_acc[t - 1] = (int8_t)acc;
+            tr_sum[t - 1] = sum_end;
+            tr_dE[t - 1] = dH;
+        }
+        if (*done == 2) break;
+    }
+    if (sum_end >= n) *done = 1;
+    memcpy(conf, s, (size_t)n);
+    free(s); free(s2); free(e1); free(tmp);
+    return t;
+}

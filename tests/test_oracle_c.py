@@ -1,0 +1,77 @@
+"""Pin the C restatement (oracle/orc_majority.c) against the reference's own
+golden vectors and the numpy oracle.  CPU only."""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from oracle import fast
+from oracle import majority as orc
+
+PC = [(1, 1), (2, 1), (2, 2), (3, 1)]
+
+
+@pytest.mark.parametrize("d", [3, 4, 6])
+@pytest.mark.parametrize("n", [64, 1000])
+def test_c_rrg_rollout_matches_reference(d, n):
+    z = load_golden("rrg_dyn.npz")
+    key = f"d{d}_n{n}"
+    N, S0 = z[f"{key}_N"], z[f"{key}_s0"]
+    for (p, c) in PC:
+        want = z[f"{key}_p{p}c{c}"]
+        got = np.stack([fast.s_endstate(N, s0, p, c) for s0 in S0])
+        assert np.array_equal(got, want), (p, c)
+
+
+def test_c_er_rollout_matches_reference():
+    z = load_golden("er_dyn.npz")
+    keys = sorted(k[:-len("_row_ptr")] for k in z if k.endswith("_row_ptr"))
+    for key in keys:
+        rp, col, S0 = z[f"{key}_row_ptr"], z[f"{key}_col"], z[f"{key}_s0"]
+        for (p, c) in PC:
+            want = z[f"{key}_p{p}c{c}"]
+            got = np.stack([fast.s_endstate_er(rp, col, s0, p, c) for s0 in S0])
+            assert np.array_equal(got, want), (key, p, c)
+
+
+@pytest.mark.parametrize("name", ["sa_d4_n200_p3c1.npz", "sa_d3_n300_p2c1.npz", "sa_d4_n200_p1c1.npz",
+                                  "sa_d4_n1000_p2c2.npz"])
+def test_c_sa_matches_reference_trace(name):
+    z = load_golden(name)
+    N, p, c = z["N"], int(z["p"]), int(z["c"])
+    for sd in [int(s) for s in z["seeds"]]:
+        steps = int(z[f"seed{sd}_num_steps"])
+        L = len(z[f"seed{sd}_i"])
+        r = fast.sa_loop(N, p, c, sd, max_steps=L, trace=True)
+        tr = r["trace"]
+        assert np.array_equal(tr["i"], z[f"seed{sd}_i"])
+        assert np.array_equal(tr["accept"], z[f"seed{sd}_accept"])
+        assert np.array_equal(tr["sum_end"], z[f"seed{sd}_sum_end"])
+        assert np.array_equal(tr["dE"], z[f"seed{sd}_dE"])        # bit-exact float64
+        if L == steps and int(z[f"seed{sd}_converged"]):
+            assert r["done"] == 1 and r["num_steps"] == steps
+            assert np.array_equal(r["conf"], z[f"seed{sd}_conf"])
+            assert r["mag_reached"] == z[f"seed{sd}_mag_reached"]
+
+
+def test_c_sa_full_script():
+    full = load_golden("sa_fullscript.npz")
+    for key, p, c in (("n200_d4_p3", 3, 1), ("n300_d3_p2", 2, 1)):
+        N = full[f"{key}_graphs"][0]
+        seed = 0 if key.startswith("n200") else 5
+        r = fast.sa_loop(N, p, c, seed)
+        assert r["done"] == 1
+        assert float(r["num_steps"]) == float(full[f"{key}_num_steps"][0])
+        assert np.array_equal(r["conf"], full[f"{key}_conf"][0])
+        assert r["mag_reached"] == full[f"{key}_mag_reached"][0]
+
+
+def test_c_sa_matches_numpy_oracle_on_c1_sizes():
+    """C1's graph size (d=4, N=1e4, p=c=1): 300 steps of two seeds, C vs numpy."""
+    from mjx import random_regular_graph
+    adj = random_regular_graph(4, 10_000, seed=1000)
+    for seed in (0, 63):
+        a = fast.sa_loop(adj, 1, 1, seed, max_steps=300, trace=True)
+        b = orc.sa_loop(adj, 1, 1, seed, max_steps=300, trace=True)
+        for k in ("i", "accept", "sum_end", "dE"):
+            assert np.array_equal(a["trace"][k], b["trace"][k]), k
+        assert np.array_equal(a["conf"], b["conf"])
