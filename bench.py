@@ -303,8 +303,13 @@ def bench_hpr(args, rank, world, dist, dev):
     upd_ms = e[0].elapsed_time(e[1]) / K
     marg_ms = e[1].elapsed_time(e[2]) / K
     msgs = 2 * plan.E
-    # per message update: d-1 incoming rows + its own row (damping) read, one row written
-    bytes_per_iter = msgs * (d + 1) * nc * 4
+    # bytes k_hpr_update moves per message: its incoming row once (each row is
+    # incoming to exactly one node's tile and staged there once), its own old
+    # row (damping), the new row written, plus the in_row/out_row/nbr indices
+    # and the source's two biases (HPR)
+    bytes_per_iter = msgs * (3 * nc * 4 + 3 * 4 + 2 * 4)
+    # marginals: every row read once (+ the Z pairs and the (n, 2) marginals written)
+    marg_bytes = msgs * nc * 4 + msgs * 2 * 4 + n * 2 * 4
     res = {"config": f"configs[2]: HPR d={d} RRG N={n}, p={p} c={c} ({nc} columns), fp32 messages, "
                      "one iteration = HPr_dp + marginals_comp",
            "scaling": "weak", "ranks": world, "messages": msgs,
@@ -313,7 +318,9 @@ def bench_hpr(args, rank, world, dist, dev):
            "messages_per_s": world * msgs * K / el,
            "hpr_dp_algorithmic_GBps": bytes_per_iter / (upd_ms / 1e3) / 1e9,
            "hpr_dp_frac_of_hbm_peak": bytes_per_iter / (upd_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
-           "hpr_dp_bytes_per_iter": bytes_per_iter}
+           "hpr_dp_bytes_per_iter": bytes_per_iter,
+           "marginals_algorithmic_GBps": marg_bytes / (marg_ms / 1e3) / 1e9,
+           "marginals_bytes_per_iter": marg_bytes}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import hpr as ohpr
         inr, src = ohpr.incoming_rows(plan.edges, plan.nbrs_host)

@@ -167,6 +167,16 @@ int mjx_sa_init(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R,
                 uint64_t* s, uint64_t* tmp1, uint64_t* tmp2,
                 mjx_sa_state* st, void* stream);
 
+/* As mjx_sa_init, but replica r continues a given MT19937 stream instead of
+ * seeding one: mt_in [R*624] words and idx_in [R] next-word indices (device),
+ * e.g. the state another replica ended in.  This is how the reference's
+ * N_stat replicas share numpy's ONE global stream back to back
+ * (code/SA_RRG.py:58-65: replica k+1's s0 draws follow replica k's last rand()). */
+int mjx_sa_init_mt(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R,
+                   const uint32_t* mt_in, const int32_t* idx_in, double a0, double b0,
+                   uint64_t* s, uint64_t* tmp1, uint64_t* tmp2,
+                   mjx_sa_state* st, void* stream);
+
 /* Advance every running replica by `nsteps` proposals (code/SA_RRG.py:72-85),
  * full rollout of each proposal.  par_a/par_b: annealing factors (:49-50);
  * a_cap = 4.5*n, b_cap = 5*n (:80-81); t_cap = 2*n**3 (:84). */

@@ -52,7 +52,7 @@ def build(force=False, verbose=True):
     objdir = os.path.join(PKG_DIR, "build")
     os.makedirs(objdir, exist_ok=True)
     base = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
-            "-Wno-unused-function", "-I", INCLUDE]
+            "-Wno-unused-function", "-I", INCLUDE] + os.environ.get("MJX_EXTRA_CFLAGS", "").split()
     objs, cmds = [], []
     # a unit is recompiled when its object is older than its source, any csrc
     # header, include/mjx.h or this script (or always, with force)

@@ -38,6 +38,8 @@ SIGNATURES = {
     "mjx_popcount_rp": [c_vp, c_i64, c_i64, c_vp, c_vp],
     "mjx_sa_init": [c_vp, c_i64, c_int, c_int, c_int, c_i64, c_vp, c_dbl, c_dbl,
                     c_vp, c_vp, c_vp, c_vp, c_vp],
+    "mjx_sa_init_mt": [c_vp, c_i64, c_int, c_int, c_int, c_i64, c_vp, c_vp, c_dbl, c_dbl,
+                       c_vp, c_vp, c_vp, c_vp, c_vp],
     "mjx_sa_steps": [c_vp, c_i64, c_int, c_int, c_int, c_i64, c_vp, c_vp, c_vp, c_vp,
                      c_i64, c_dbl, c_dbl, c_dbl, c_dbl, c_i64, c_vp],
     "mjx_sa_lightcone_lds": [c_int, c_int, c_int],

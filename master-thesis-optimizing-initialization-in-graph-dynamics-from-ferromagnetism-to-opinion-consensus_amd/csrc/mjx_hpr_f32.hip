@@ -9,3 +9,16 @@ int update_f32(const void* ci, void* co, const void* b, const int32_t* nb, const
 }
 }  // namespace hpr
 }  // namespace mjx
+
+#ifdef MJX_HPR_PROF
+// profiling build only (-DMJX_HPR_PROF): per-phase cycle sums of k_hpr_update
+extern "C" int mjx_hpr_prof_read(unsigned long long* host8, int reset) {
+    if (hipMemcpyFromSymbol(host8, HIP_SYMBOL(mjx::hpr::mjx_hpr_prof), 8 * sizeof(unsigned long long)) != hipSuccess)
+        return MJX_EHIP;
+    if (reset) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(mjx::hpr::mjx_hpr_prof), z, sizeof(z)) != hipSuccess) return MJX_EHIP;
+    }
+    return MJX_OK;
+}
+#endif

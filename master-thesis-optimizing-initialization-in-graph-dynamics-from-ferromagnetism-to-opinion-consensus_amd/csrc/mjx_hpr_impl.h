@@ -220,6 +220,13 @@ __device__ __forceinline__ S xa_messages(const S* __restrict__ rows, const S* __
     return rs;
 }
 
+#ifdef MJX_HPR_PROF
+__device__ unsigned long long mjx_hpr_prof[8];
+#define MJX_PROF_MARK(k) do { const unsigned long long _c = clock64(); if ((threadIdx.x & 63) == 0) atomicAdd(&mjx_hpr_prof[k], _c - _t0); _t0 = _c; } while (0)
+#else
+#define MJX_PROF_MARK(k) do {} while (0)
+#endif
+
 template <typename S, int T, int P, int D>
 __global__ void __launch_bounds__((64 * Cfg<S, T, P, D>::NW))
 k_hpr_update(const S* __restrict__ chi_in, S* __restrict__ chi_out, const S* __restrict__ biases,
@@ -234,28 +241,53 @@ k_hpr_update(const S* __restrict__ chi_in, S* __restrict__ chi_out, const S* __r
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
     const int64_t a0 = (int64_t)blockIdx.x * NT;
+#ifdef MJX_HPR_PROF
+    unsigned long long _t0 = clock64();
+#endif
     const int nt = (int)((n - a0) < NT ? (n - a0) : NT);   // nodes in this tile
     const int nl = nt * D;
-    // ---- stage the incoming rows of the tile's nodes and their sources' biases
+    // ---- stage the incoming rows of the tile's nodes and their sources' biases.
+    // Three phases so that one tile pays two memory round trips, not one per
+    // row: every row index, then every 16-B row piece in flight at once (a
+    // wave instruction reads a whole 1 KB row at T=4 fp32), then the LDS image.
     {
         using V = typename Vec16<S>::T;
         constexpr int VN = Vec16<S>::N;
         constexpr int VPR = NC / VN;                 // 16-B vectors per row
-        for (int q = tid; q < nl * VPR; q += 64 * NW) {
-            const int slot = q / VPR, v = q % VPR;
-            const int64_t r = in_row[a0 * D + slot];
-            const V x = reinterpret_cast<const V*>(chi_in + r * NC)[v];
-            const S* xs = reinterpret_cast<const S*>(&x);
+        constexpr int IT = (NL * VPR + 64 * NW - 1) / (64 * NW);
+        // branch-free loads (indices clamped into the tile): a load under a
+        // per-lane branch is followed by its own vmcnt(0) wait
+        const int qmax = nl * VPR - 1;
+        int64_t src[IT];
 #pragma unroll
-            for (int k = 0; k < VN; ++k) rows[slot * C::STRIDE + v * VN + k] = xs[k];
+        for (int k = 0; k < IT; ++k) {
+            int q = tid + k * 64 * NW;
+            q = q < qmax ? q : qmax;
+            src[k] = (int64_t)in_row[a0 * D + q / VPR] * NC + (q % VPR) * VN;
         }
-        for (int q = tid; q < nl; q += 64 * NW) {
-            const int64_t k = nbr[a0 * D + q];
-            bias[2 * q] = biases[2 * k];
-            bias[2 * q + 1] = biases[2 * k + 1];
+        const int bq = tid < nl ? tid : nl - 1;
+        const int64_t bsrc = nbr[a0 * D + bq];
+        V buf[IT];
+#pragma unroll
+        for (int k = 0; k < IT; ++k) buf[k] = *reinterpret_cast<const V*>(chi_in + src[k]);
+        const S bp = biases[2 * bsrc], bm = biases[2 * bsrc + 1];
+#pragma unroll
+        for (int k = 0; k < IT; ++k) {
+            const int q = tid + k * 64 * NW;
+            if (q <= qmax) {
+                const int slot = q / VPR, v = q % VPR;
+                const S* xs = reinterpret_cast<const S*>(&buf[k]);
+#pragma unroll
+                for (int e = 0; e < VN; ++e) rows[slot * C::STRIDE + v * VN + e] = xs[e];
+            }
+        }
+        if (tid < nl) {
+            bias[2 * tid] = bp;
+            bias[2 * tid + 1] = bm;
         }
     }
     __syncthreads();
+    MJX_PROF_MARK(0);
     const bool active = lane < nl;
     const int a_local = lane / D, m = lane % D;
     S out[XPW][X];
@@ -276,8 +308,10 @@ k_hpr_update(const S* __restrict__ chi_in, S* __restrict__ chi_out, const S* __r
             });
         });
     }
+    MJX_PROF_MARK(1);
     red[wave * 64 + lane] = rs;
     __syncthreads();
+    MJX_PROF_MARK(2);
     if (!active) return;
     S tot = S(0);
 #pragma unroll
@@ -299,47 +333,82 @@ k_hpr_update(const S* __restrict__ chi_in, S* __restrict__ chi_out, const S* __r
             dst[ci + xb] = keep * old[ci + xb];
         }
     }
+#ifdef MJX_HPR_PROF
+    __builtin_amdgcn_s_waitcnt(0);
+#endif
+    MJX_PROF_MARK(3);
 }
 
 // ---- marginals (code/HPR_pytorch_RRG.py:147-167) ---------------------------
-// One group of LPE lanes per undirected edge r: Z sums of chi^{u->v}(x_u,x_v) chi^{v->u}(x_v,x_u)
-// by x_u[0] (row r) and by x_v[0] (row r+E), clamped at eps, normalised.
+// A group of G lanes per undirected edge r: Z sums of chi^{u->v}(x_u,x_v) chi^{v->u}(x_v,x_u)
+// by x_u[0] (row r) and by x_v[0] (row r+E), clamped at eps, normalised.  The
+// forward row is read in 16-B pieces (a whole 1 KB row per wave instruction at
+// T=4 fp32); the reverse row's transposed elements by 4-line gathers; U edge
+// groups per lane are in flight at once (the kernel is a stream over chi).
 template <typename S, int T>
 __global__ void __launch_bounds__(256) k_hpr_edge_z(const S* __restrict__ chi, int64_t E, S eps,
                                                      S* __restrict__ zp, S* __restrict__ zm) {
     constexpr int X = 1 << T, NC = X * X;
-    constexpr int LPE = NC < 64 ? NC : 64;
-    constexpr int EPW = 64 / LPE;
+    using V = typename Vec16<S>::T;
+    constexpr int VN = Vec16<S>::N;
+    constexpr int G = NC / VN < 64 ? NC / VN : 64;   // lanes per edge
+    constexpr int NV = NC / (VN * G);                // 16-B pieces per lane per row
+    constexpr int EPW = 64 / G;                      // edges per wave instruction
+    constexpr int U = NV >= 4 ? 1 : 4 / NV;          // edge groups in flight per lane
     const int lane = threadIdx.x & 63;
-    const int g = lane / LPE, l = lane % LPE;
+    const int g = lane / G, l = lane % G;
     const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * 256) >> 6;
-    for (int64_t base = wave * EPW; base < E; base += nwaves * EPW) {
-        const int64_t r = base + g;
-        S fp = 0, fm = 0, bp = 0, bm = 0;
-        if (r < E) {
-            const S* f = chi + r * NC;
-            const S* b = chi + (r + E) * NC;
-            for (int j = l; j < NC; j += LPE) {
-                const int xa = j / X, xb = j % X;
-                const S z = f[j] * b[xb * X + xa];
-                if (xa < X / 2) fp += z; else fm += z;
-                if (xb < X / 2) bp += z; else bm += z;
+    for (int64_t base = wave * EPW * U; base < E; base += nwaves * EPW * U) {
+        S f[U][NV][VN], b[U][NV][VN];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t r = base + u * EPW + g;
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                const int j0 = (v * G + l) * VN;
+                if (r < E) {
+                    const V x = *reinterpret_cast<const V*>(chi + r * NC + j0);
+                    const S* xs = reinterpret_cast<const S*>(&x);
+#pragma unroll
+                    for (int e = 0; e < VN; ++e) {
+                        f[u][v][e] = xs[e];
+                        const int xa = (j0 + e) / X, xb = (j0 + e) % X;
+                        b[u][v][e] = chi[(r + E) * NC + xb * X + xa];
+                    }
+                }
             }
         }
 #pragma unroll
-        for (int off = LPE / 2; off > 0; off >>= 1) {
-            fp += __shfl_xor(fp, off, 64);
-            fm += __shfl_xor(fm, off, 64);
-            bp += __shfl_xor(bp, off, 64);
-            bm += __shfl_xor(bm, off, 64);
-        }
-        if (l == 0 && r < E) {
-            fp = fp > eps ? fp : eps; fm = fm > eps ? fm : eps;
-            bp = bp > eps ? bp : eps; bm = bm > eps ? bm : eps;
-            const S sf = fp + fm, sb = bp + bm;
-            zp[r] = fp / sf; zm[r] = fm / sf;
-            zp[r + E] = bp / sb; zm[r + E] = bm / sb;
+        for (int u = 0; u < U; ++u) {
+            const int64_t r = base + u * EPW + g;
+            S fp = 0, fm = 0, bp = 0, bm = 0;
+            if (r < E) {
+#pragma unroll
+                for (int v = 0; v < NV; ++v)
+#pragma unroll
+                    for (int e = 0; e < VN; ++e) {
+                        const int j = (v * G + l) * VN + e;
+                        const int xa = j / X, xb = j % X;
+                        const S z = f[u][v][e] * b[u][v][e];
+                        if (xa < X / 2) fp += z; else fm += z;
+                        if (xb < X / 2) bp += z; else bm += z;
+                    }
+            }
+#pragma unroll
+            for (int off = G / 2; off > 0; off >>= 1) {
+                fp += __shfl_xor(fp, off, 64);
+                fm += __shfl_xor(fm, off, 64);
+                bp += __shfl_xor(bp, off, 64);
+                bm += __shfl_xor(bm, off, 64);
+            }
+            if (l == 0 && r < E) {
+                fp = fp > eps ? fp : eps; fm = fm > eps ? fm : eps;
+                bp = bp > eps ? bp : eps; bm = bm > eps ? bm : eps;
+                const S sf = fp + fm, sb = bp + bm;
+                zp[r] = fp / sf; zm[r] = fm / sf;
+                zp[r + E] = bp / sb; zm[r + E] = bm / sb;
+            }
         }
     }
 }

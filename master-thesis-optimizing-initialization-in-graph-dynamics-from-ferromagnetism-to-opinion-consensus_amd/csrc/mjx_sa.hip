@@ -59,18 +59,25 @@ __device__ __forceinline__ double mt_double(uint32_t w1, uint32_t w2) {
 __global__ void __launch_bounds__(64) k_sa_init_draw(int64_t n, int64_t R, int64_t W,
                                                      const uint32_t* __restrict__ seeds,
                                                      u64* __restrict__ s, uint32_t* __restrict__ mt_out,
-                                                     int32_t* __restrict__ idx_out) {
+                                                     int32_t* __restrict__ idx_out,
+                                                     const uint32_t* __restrict__ mt_in = nullptr,
+                                                     const int32_t* __restrict__ idx_in = nullptr) {
     __shared__ uint32_t st[MT_N * 64];
     const int lane = threadIdx.x;
     const int64_t w = blockIdx.x;
     const int64_t r = w * 64 + lane;
     const bool live = r < R;
-    uint32_t x = live ? seeds[r] : 0u;
-    for (int k = 0; k < MT_N; ++k) {       // init_genrand / numpy mt19937_seed
-        st[k * 64 + lane] = x;
-        x = 1812433253u * (x ^ (x >> 30)) + (uint32_t)(k + 1);
-    }
     int idx = MT_N;
+    if (mt_in) {                           // continue a given stream (numpy's global state)
+        for (int k = 0; k < MT_N; ++k) st[k * 64 + lane] = live ? mt_in[r * MT_N + k] : 0u;
+        idx = live ? idx_in[r] : MT_N;
+    } else {
+        uint32_t x = live ? seeds[r] : 0u;
+        for (int k = 0; k < MT_N; ++k) {   // init_genrand / numpy mt19937_seed
+            st[k * 64 + lane] = x;
+            x = 1812433253u * (x ^ (x >> 30)) + (uint32_t)(k + 1);
+        }
+    }
     auto next = [&]() -> uint32_t {
         if (idx >= MT_N) {
             for (int k = 0; k < MT_N - MT_M; ++k)
@@ -1087,6 +1094,40 @@ static bool lc_mlp_degree(int d) { return d == 3 || d == 4 || d == 6; }
 
 using namespace mjx;
 
+static int sa_init_finish(const int32_t* adj, int64_t n, int d, int T, int64_t R, int64_t W, double a0, double b0,
+                          uint64_t* s, uint64_t* tmp1, uint64_t* tmp2, const mjx_sa_state& st, void* stream) {
+    hipStream_t hs = as_stream(stream);
+    MJX_HIP(hipMemsetAsync(st.cnt, 0, (size_t)R * sizeof(unsigned long long), hs), "sa_init memset");
+    int rc = mjx_rollout_ell_rp(adj, n, d, W, s, tmp1, tmp2, T, st.cnt, stream);
+    if (rc) return rc;
+    k_sa_init_state<<<(unsigned)((R + 255) / 256), 256, 0, hs>>>(n, R, a0, b0, st.cnt, st);
+    MJX_LAUNCH_CHECK("k_sa_init_state");
+    return MJX_OK;
+}
+
+static bool sa_state_complete(const mjx_sa_state& st) {
+    return st.mt && st.mt_idx && st.a && st.b && st.t && st.sum_end && st.done && st.prop_i && st.prop_s &&
+           st.prop_u && st.cnt;
+}
+
+extern "C" int mjx_sa_init_mt(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R, const uint32_t* mt_in,
+                              const int32_t* idx_in, double a0, double b0, uint64_t* s, uint64_t* tmp1, uint64_t* tmp2,
+                              mjx_sa_state* stp, void* stream) {
+    if (!stp || n < 2 || R < 1 || d < 1 || p < 0 || c < 0 || p + c < 1 || !adj || !mt_in || !idx_in || !s || !tmp1)
+        return MJX_EINVAL;
+    if (n > (int64_t)INT32_MAX) return MJX_ERANGE;
+    mjx_sa_state st = *stp;
+    if (!sa_state_complete(st)) return MJX_EINVAL;
+    const int64_t W = (R + 63) / 64;
+    const int T = p + c - 1;
+    if (T >= 2 && !tmp2) return MJX_EINVAL;
+    // lane per replica: each lane continues its own stream from its own index
+    k_sa_init_draw<<<(unsigned)W, 64, 0, as_stream(stream)>>>(n, R, W, nullptr, (u64*)s, st.mt, st.mt_idx, mt_in,
+                                                               idx_in);
+    MJX_LAUNCH_CHECK("k_sa_init_draw");
+    return sa_init_finish(adj, n, d, T, R, W, a0, b0, s, tmp1, tmp2, st, stream);
+}
+
 extern "C" int mjx_sa_init(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R, const uint32_t* seeds,
                            double a0, double b0, uint64_t* s, uint64_t* tmp1, uint64_t* tmp2, mjx_sa_state* stp,
                            void* stream) {
@@ -1118,12 +1159,7 @@ extern "C" int mjx_sa_init(const int32_t* adj, int64_t n, int d, int p, int c, i
             MJX_LAUNCH_CHECK("k_np_to_rp");
         }
     }
-    MJX_HIP(hipMemsetAsync(st.cnt, 0, (size_t)R * sizeof(unsigned long long), hs), "sa_init memset");
-    int rc = mjx_rollout_ell_rp(adj, n, d, W, s, tmp1, tmp2, T, st.cnt, stream);
-    if (rc) return rc;
-    k_sa_init_state<<<(unsigned)((R + 255) / 256), 256, 0, hs>>>(n, R, a0, b0, st.cnt, st);
-    MJX_LAUNCH_CHECK("k_sa_init_state");
-    return MJX_OK;
+    return sa_init_finish(adj, n, d, T, R, W, a0, b0, s, tmp1, tmp2, st, stream);
 }
 
 extern "C" int mjx_sa_steps(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R, uint64_t* s,

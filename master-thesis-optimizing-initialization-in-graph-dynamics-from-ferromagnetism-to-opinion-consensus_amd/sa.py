@@ -46,7 +46,11 @@ def schedule_constants(n):
 class SAReplicas:
     """R bit-packed SA replicas on one random regular graph (device resident)."""
 
-    def __init__(self, N, p, c, seeds, par_a=PAR_A, par_b=PAR_B, a0=None, b0=None, mode="auto", tape=1024):
+    def __init__(self, N, p, c, seeds, par_a=PAR_A, par_b=PAR_B, a0=None, b0=None, mode="auto", tape=1024,
+                 mt_state=None):
+        """``mt_state`` = (mt uint32 (R, 624), idx int32 (R,)): continue these
+        MT19937 streams instead of seeding (``seeds`` then only fixes R); see
+        ``mt_state()`` and ``sa_run(stream="global")``."""
         self.graph = as_graph(N)
         if self.graph.kind != "ell":
             raise ValueError("SA runs on random regular graphs (ELL adjacency), code/SA_RRG.py:59-61")
@@ -88,10 +92,23 @@ class SAReplicas:
             setattr(self._state, f, getattr(self, f).data_ptr())
         self._state.tr_tie = self.ties.data_ptr()
         T = self.p + self.c - 1
-        _lib.call("mjx_sa_init", _device.ptr(self.graph.adj), n, self.graph.d, self.p, self.c, R,
-                  _device.ptr(self.seeds), self.a0, self.b0, _device.ptr(self.s), _device.ptr(self.tmp1),
-                  _device.ptr(self.tmp2) if T >= 2 else None, _lib.ctypes.byref(self._state),
-                  _device.stream_handle())
+        if mt_state is None:
+            _lib.call("mjx_sa_init", _device.ptr(self.graph.adj), n, self.graph.d, self.p, self.c, R,
+                      _device.ptr(self.seeds), self.a0, self.b0, _device.ptr(self.s), _device.ptr(self.tmp1),
+                      _device.ptr(self.tmp2) if T >= 2 else None, _lib.ctypes.byref(self._state),
+                      _device.stream_handle())
+        else:
+            mt_in = np.ascontiguousarray(np.asarray(mt_state[0], dtype=np.uint32).reshape(R, 624))
+            idx_in = np.ascontiguousarray(np.asarray(mt_state[1], dtype=np.int32).reshape(R))
+            if idx_in.min() < 0 or idx_in.max() > 624:
+                raise ValueError("MT19937 word index must be in [0, 624]")
+            mt_d = torch.from_numpy(mt_in.view(np.int32)).to(dev)
+            idx_d = torch.from_numpy(idx_in).to(dev)
+            _lib.call("mjx_sa_init_mt", _device.ptr(self.graph.adj), n, self.graph.d, self.p, self.c, R,
+                      _device.ptr(mt_d), _device.ptr(idx_d), self.a0, self.b0, _device.ptr(self.s),
+                      _device.ptr(self.tmp1), _device.ptr(self.tmp2) if T >= 2 else None,
+                      _lib.ctypes.byref(self._state), _device.stream_handle())
+            torch.cuda.current_stream().synchronize()       # mt_d / idx_d are freed on return
         lds = _lib.load().mjx_sa_lightcone_lds(self.graph.d, self.p, self.c)
         fits = T >= 1 and 0 < lds <= 150 * 1024
         if mode == "auto":
@@ -152,6 +169,16 @@ class SAReplicas:
     def all_done(self):
         return bool((self.done != 0).all().item())
 
+    def mt_state(self):
+        """Host copy (mt uint32 (R, 624), idx int32 (R,)) of every replica's
+        MT19937 stream: exactly where numpy's stream would be after the same
+        draws when the proposals are drawn in the step (``tape=0`` or the
+        rollout mode); a proposal tape draws ahead of the stop."""
+        if self.mode == "lightcone" and getattr(self, "tape_cap", 0):
+            raise ValueError("the proposal tape draws ahead: use tape=0 (or mode='rollout') for an exact stream")
+        mt = self.mt.cpu().numpy().view(np.uint32).reshape(self.R, 624).copy()
+        return mt, self.mt_idx.cpu().numpy().copy()
+
     def run(self, max_steps=None, chunk=256):
         """Step until every replica has reached consensus or the t cap
         (``while(m_final<1)``, code/SA_RRG.py:72), or ``max_steps``."""
@@ -210,23 +237,79 @@ def E_delta(N, s0, a, b, p, c, i):
     return (-2 * a * si + b * (sum1 - sum2)) / g.n
 
 
+def _graph_list(d, n, N_stat, N, graphs, graph_seed):
+    """One (n, d) neighbour array per replica (code/SA_RRG.py:58-61 draws a
+    fresh random regular graph per replica)."""
+    from .graph import random_regular_graph
+    if graphs is not None:
+        gl = [np.asarray(g) for g in graphs]
+        if len(gl) != N_stat:
+            raise ValueError(f"graphs: one neighbour array per replica ({N_stat}), got {len(gl)}")
+        return gl
+    if N is not None:                       # one given graph for every replica
+        return [np.asarray(N)] * N_stat
+    base = 0 if graph_seed is None else int(graph_seed)
+    return [random_regular_graph(d, n, seed=base + k) for k in range(N_stat)]
+
+
 def sa_run(d, n, p, c, par_a=PAR_A, par_b=PAR_B, N_stat=5, seed=0, seeds=None, N=None, graph_seed=None,
-           max_steps=None):
+           max_steps=None, graphs=None, stream="independent", mode="auto"):
     """Drop-in for the SA_RRG.py experiment (code/SA_RRG.py:44-92).
 
     Returns the reference's output arrays ``mag_reached, num_steps, conf,
-    graphs`` (the np.savez keys of code/SA_RRG.py:92).  All N_stat replicas
-    share one graph (``N`` if given, else a random d-regular graph) and replica
-    k uses numpy seed ``seeds[k]`` (default seed + k).
+    graphs`` (the np.savez keys of code/SA_RRG.py:92), row k = replica k.
+
+    Graphs: ``graphs`` (one (n, d) neighbour array per replica), else ``N``
+    for every replica, else a fresh random d-regular graph per replica
+    (``graph_seed + k``), as the reference draws one per replica (:59).
+
+    Randomness:
+      * ``stream="global"`` — the reference's own semantics: ONE numpy stream
+        seeded once (``np.random.seed(seed)``) and consumed by the replicas
+        back to back, so replica k+1's s0 draws continue where replica k's
+        last rand() left the stream (:58-88).  Replicas run one after the
+        other (mjx_sa_init_mt hands the stream over); bit-identical to the
+        script with the same graphs.
+      * ``stream="independent"`` — replica k owns ``np.random.seed(seeds[k])``
+        (default seed + k); replicas sharing a graph run together, bit-packed.
     """
-    from .graph import random_regular_graph
-    if N is None:
-        N = random_regular_graph(d, n, seed=graph_seed)
-    N = np.asarray(N)
-    if seeds is None:
-        seeds = [seed + k for k in range(N_stat)]
-    sa = SAReplicas(N, p, c, seeds, par_a=par_a, par_b=par_b)
-    sa.run(max_steps=max_steps)
-    res = sa.results()
-    res["graphs"] = np.broadcast_to(N.astype(int), (len(seeds),) + N.shape).copy()
+    gl = _graph_list(d, n, N_stat, N, graphs, graph_seed)
+    R = len(gl)
+    res = {"mag_reached": np.zeros(R), "num_steps": np.zeros(R), "conf": np.zeros((R, n)),
+           "done": np.zeros(R, dtype=np.int32), "near_ties": np.zeros(R, dtype=np.int32)}
+
+    def store(k, out, j):
+        for key in res:
+            res[key][k] = out[key][j]
+
+    if stream == "global":
+        state = None
+        m = "rollout" if mode == "rollout" else "lightcone"
+        for k, g in enumerate(gl):
+            sa = SAReplicas(g, p, c, [int(seed) & 0xFFFFFFFF], par_a=par_a, par_b=par_b, mode=m, tape=0,
+                            mt_state=state)
+            sa.run(max_steps=max_steps)
+            store(k, sa.results(), 0)
+            state = sa.mt_state()
+            del sa
+    elif stream == "independent":
+        if seeds is None:
+            seeds = [seed + k for k in range(R)]
+        seeds = list(seeds)
+        if len(seeds) != R:
+            raise ValueError(f"seeds: one per replica ({R}), got {len(seeds)}")
+        # replicas that share a graph run together (bit-packed)
+        groups = {}
+        for k, g in enumerate(gl):
+            groups.setdefault(id(g), []).append(k)
+        for ks in groups.values():
+            sa = SAReplicas(gl[ks[0]], p, c, [seeds[k] for k in ks], par_a=par_a, par_b=par_b, mode=mode)
+            sa.run(max_steps=max_steps)
+            out = sa.results()
+            for j, k in enumerate(ks):
+                store(k, out, j)
+            del sa
+    else:
+        raise ValueError(f"stream must be 'global' or 'independent', got {stream!r}")
+    res["graphs"] = np.stack([g.astype(int) for g in gl])
     return res

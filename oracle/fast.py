@@ -30,7 +30,7 @@ def _lib():
         lib.orc_s_endstate_csr.argtypes = [_P, _P, _I64, _P, ctypes.c_int, _P, _P]
         lib.orc_s_endstate_csr.restype = _I64
         lib.orc_sa_loop.argtypes = [_P, _I64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint32,
-                                    ctypes.c_double, ctypes.c_double, _I64, _P, _P, _P, _P, _P, _P]
+                                    ctypes.c_double, ctypes.c_double, _I64, _P, _P, _P, _P, _P, _P, _P, _P]
         lib.orc_sa_loop.restype = _I64
         _LIB = lib
     return _LIB
@@ -63,7 +63,9 @@ def s_endstate_er(row_ptr, col, s0, p, c):
     return out.astype(np.int64)
 
 
-def sa_loop(N, p, c, seed, par_a=1.0005, par_b=1.0005, max_steps=None, trace=False):
+def sa_loop(N, p, c, seed, par_a=1.0005, par_b=1.0005, max_steps=None, trace=False, mt_state=None):
+    """``mt_state`` = (mt uint32 (624,), idx): continue that stream instead of
+    seeding; the returned dict then holds the stream's final "mt_state"."""
     N = np.ascontiguousarray(N, dtype=np.int32)
     n, d = N.shape
     if max_steps is None and trace:
@@ -76,12 +78,19 @@ def sa_loop(N, p, c, seed, par_a=1.0005, par_b=1.0005, max_steps=None, trace=Fal
               "dE": np.zeros(L, np.float64)}
     conf = np.empty(n, np.int8)
     done = ctypes.c_int32(0)
+    mt = idx = None
+    if mt_state is not None:
+        mt = np.ascontiguousarray(np.asarray(mt_state[0], dtype=np.uint32).reshape(624)).copy()
+        idx = ctypes.c_int32(int(mt_state[1]))
     t = _lib().orc_sa_loop(_ptr(N), n, d, int(p), int(c), int(seed) & 0xFFFFFFFF, float(par_a), float(par_b), cap,
                            _ptr(tr["i"]) if tr else None, _ptr(tr["accept"]) if tr else None,
                            _ptr(tr["sum_end"]) if tr else None, _ptr(tr["dE"]) if tr else None, _ptr(conf),
-                           ctypes.byref(done))
+                           ctypes.byref(done), _ptr(mt) if mt is not None else None,
+                           ctypes.byref(idx) if idx is not None else None)
     conf = conf.astype(np.int64)
     out = {"conf": conf, "num_steps": int(t), "mag_reached": np.sum(conf) / n, "done": int(done.value)}
+    if mt is not None:
+        out["mt_state"] = (mt, int(idx.value))
     if trace:
         out["trace"] = {"i": tr["i"][:t].astype(np.int64), "accept": tr["accept"][:t],
                         "sum_end": tr["sum_end"][:t], "dE": tr["dE"][:t]}

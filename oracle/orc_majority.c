@@ -129,10 +129,12 @@ int64_t orc_s_endstate_csr(const int64_t* row_ptr, const int32_t* col, int64_t n
  * consensus, at the t > 2n^3 cap, or after max_steps (< 0: no limit).
  * Per-step traces (length >= max_steps when given): proposal i, accept,
  * sum(s_endstate) after the step, delta_H.  conf receives the final s.
- * Returns the number of steps taken; *done = 1 consensus, 2 cap, 0 stopped. */
+ * Returns the number of steps taken; *done = 1 consensus, 2 cap, 0 stopped.
+ * mt_io/idx_io (optional): the stream to continue instead of seeding, and
+ * where the stream stands on return. */
 int64_t orc_sa_loop(const int32_t* adj, int64_t n, int d, int p, int c, uint32_t seed, double par_a, double par_b,
                     int64_t max_steps, int32_t* tr_i, int8_t* tr_acc, int64_t* tr_sum, double* tr_dE, int8_t* conf,
-                    int32_t* done)
+                    int32_t* done, uint32_t* mt_io, int32_t* idx_io)
 {
     int T = p + c - 1;
     int8_t* s = (int8_t*)malloc((size_t)n);
@@ -140,7 +142,12 @@ int64_t orc_sa_loop(const int32_t* adj, int64_t n, int d, int p, int c, uint32_t
     int8_t* e1 = (int8_t*)malloc((size_t)n);
     int8_t* tmp = (int8_t*)malloc((size_t)n);
     orc_mt rs;
-    mt_seed(&rs, seed);
+    if (mt_io) {            /* continue the given stream (numpy's ONE global stream, :58-65) */
+        memcpy(rs.mt, mt_io, sizeof(rs.mt));
+        rs.idx = *idx_io;
+    } else {
+        mt_seed(&rs, seed);
+    }
     for (int64_t i = 0; i < n; ++i) s[i] = mt_double(&rs) > 0.5 ? 1 : -1;      /* :65 */
     double a = 0.015 * (double)n, b = 0.01 * (double)n;                        /* :67-68 */
     double a_cap = 4.5 * (double)n, b_cap = 5.0 * (double)n;                   /* :80-81 */
@@ -186,6 +193,10 @@ int64_t orc_sa_loop(const int32_t* adj, int64_t n, int d, int p, int c, uint32_t
     }
     if (sum_end >= n) *done = 1;
     memcpy(conf, s, (size_t)n);
+    if (mt_io) {
+        memcpy(mt_io, rs.mt, sizeof(rs.mt));
+        *idx_io = rs.idx;
+    }
     free(s); free(s2); free(e1); free(tmp);
     return t;
 }

@@ -193,11 +193,13 @@ def gen_sa_full():
     with open(SA_PATH) as f:
         src = f.read()
     runs = {}
-    for (n, d, p, gseed, nseed) in ((200, 4, 3, 1, 0), (300, 3, 2, 2, 5)):
+    # (n, d, p, graph seed, numpy seed, N_stat): N_stat = 2 pins the back-to-back
+    # use of ONE numpy stream by consecutive replicas, each on its own graph
+    for (n, d, p, gseed, nseed, nstat) in ((200, 4, 3, 1, 0, 1), (300, 3, 2, 2, 5, 1), (200, 4, 3, 3, 11, 2)):
         tmp = tempfile.mktemp(suffix=".npz")
         s = src
         for old, new in (("n=10000", f"n={n}"), ("d=4", f"d={d}"), ("p=3", f"p={p}"), ("c=1 ", "c=1 "),
-                         ("N_stat=5", "N_stat=1")):
+                         ("N_stat=5", f"N_stat={nstat}")):
             assert old in s, old
             s = s.replace(old, new, 1)
         if p == 2:
@@ -211,7 +213,7 @@ def gen_sa_full():
         g = {"__name__": "ref_sa_full"}
         exec(compile(s, SA_PATH, "exec"), g)
         z = np.load(tmp)
-        runs[f"n{n}_d{d}_p{p}"] = {k: z[k] for k in z.files}
+        runs[f"n{n}_d{d}_p{p}" + (f"_nstat{nstat}" if nstat > 1 else "")] = {k: z[k] for k in z.files}
         os.unlink(tmp)
         print("full script", n, d, p, "steps", z["num_steps"])
     out = {}

@@ -75,3 +75,21 @@ def test_c_sa_matches_numpy_oracle_on_c1_sizes():
         for k in ("i", "accept", "sum_end", "dE"):
             assert np.array_equal(a["trace"][k], b["trace"][k]), k
         assert np.array_equal(a["conf"], b["conf"])
+
+
+def test_c_sa_global_stream_two_replicas():
+    """The reference script with N_stat = 2 (one numpy stream, seeded once,
+    consumed by replica 0 then replica 1, each on its own graph)."""
+    from oracle.mt19937 import MT19937
+    full = load_golden("sa_fullscript.npz")
+    key = "n200_d4_p3_nstat2"
+    graphs = full[f"{key}_graphs"]
+    m = MT19937(11)                                     # np.random.seed(11) before the replica loop
+    state = (np.array(m.mt, dtype=np.uint32), m.idx)
+    for k in range(2):
+        r = fast.sa_loop(graphs[k], 3, 1, 0, mt_state=state)
+        state = r["mt_state"]
+        assert r["done"] == 1
+        assert float(r["num_steps"]) == float(full[f"{key}_num_steps"][k])
+        assert np.array_equal(r["conf"], full[f"{key}_conf"][k])
+        assert r["mag_reached"] == full[f"{key}_mag_reached"][k]

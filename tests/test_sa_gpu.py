@@ -154,3 +154,49 @@ def test_sa_lightcone_wave_split_is_bit_exact(mjx_mod, split, monkeypatch):
         L = len(o["i"])
         assert np.array_equal(tr["accept"][:L, r], o["accept"])
         assert np.array_equal(tr["sum_end"][:L, r], o["sum_end"])
+
+
+def _ref_sa_arrays(full, key):
+    return {k: full[f"{key}_{k}"] for k in ("mag_reached", "num_steps", "conf", "graphs")}
+
+
+@pytest.mark.parametrize("mode", ["lightcone", "rollout"])
+def test_sa_run_global_stream_two_replicas_to_npz(mjx_mod, mode, tmp_path):
+    """SA_RRG.py with N_stat = 2 end to end: one numpy stream seeded once and
+    consumed by the replicas back to back, a graph per replica (:58-65), and
+    the np.savez file (:92) equal to the one the reference script wrote
+    (keys, dtypes, values)."""
+    full = load_golden("sa_fullscript.npz")
+    ref = _ref_sa_arrays(full, "n200_d4_p3_nstat2")
+    res = mjx_mod.sa_run(4, 200, 3, 1, N_stat=2, seed=11, graphs=list(ref["graphs"]), stream="global", mode=mode)
+    assert list(res["done"]) == [1, 1]
+    path = tmp_path / "MCMC_p3_d4.npz"
+    mjx_mod.save_sa_npz(path, res)
+    with np.load(path) as z:
+        assert sorted(z.files) == sorted(ref)
+        for k in ref:
+            assert z[k].dtype == ref[k].dtype, k
+            assert np.array_equal(z[k], ref[k]), k
+
+
+def test_sa_run_single_replica_to_npz(mjx_mod, tmp_path):
+    full = load_golden("sa_fullscript.npz")
+    ref = _ref_sa_arrays(full, "n200_d4_p3")
+    res = mjx_mod.sa_run(4, 200, 3, 1, N_stat=1, seed=0, graphs=list(ref["graphs"]), stream="global")
+    path = tmp_path / "sa.npz"
+    mjx_mod.save_sa_npz(path, res)
+    with np.load(path) as z:
+        for k in ref:
+            assert z[k].dtype == ref[k].dtype and np.array_equal(z[k], ref[k]), k
+
+
+def test_sa_run_independent_per_replica_graphs(mjx_mod):
+    """Independent streams, a fresh graph per replica: replica k equals the
+    oracle run on its own graph with seed k (first 400 steps)."""
+    res = mjx_mod.sa_run(3, 300, 2, 1, N_stat=3, seed=40, graph_seed=7, max_steps=400)
+    g = res["graphs"]
+    assert g.shape == (3, 300, 3) and not np.array_equal(g[0], g[1])
+    for k in range(3):
+        o = orc.sa_loop(g[k], 2, 1, 40 + k, max_steps=400)
+        assert np.array_equal(res["conf"][k], o["conf"]), k
+        assert res["num_steps"][k] == o["num_steps"], k

@@ -6,7 +6,7 @@ import torch
 import mjx
 
 n, d, p, c = int(os.environ.get("N", 100000)), 4, 2, 2
-for dtype in (torch.float32, torch.float64):
+for dtype in ((torch.float32,) if os.environ.get("ONLY_F32") else (torch.float32, torch.float64)):
     edges = mjx.random_regular_edges(d, n, seed=3)
     plan = mjx.HPRPlan(edges, n, d)
     nc = 4 ** (p + c)
