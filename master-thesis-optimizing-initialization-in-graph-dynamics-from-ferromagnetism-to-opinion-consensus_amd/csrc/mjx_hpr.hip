@@ -26,14 +26,19 @@ static int marginals_impl(const void* chi, const int32_t* out_row, int64_t n, in
     const int64_t E = n * (int64_t)d / 2;
     S* zp = (S*)zwork;
     S* zm = zp + 2 * E;
-    const int grid = grid_for(E * 64 / 4);
+    // one grid-stride round of resident waves (a larger grid runs a partly empty second round)
+#define MJX_EDGE_Z(TT)                                                                                   \
+    case TT: {                                                                                           \
+        auto k = k_hpr_edge_z<S, TT>;                                                                    \
+        const int64_t lanes = E * (1 << TT) / 2;           /* U = 2 edge groups per lane */             \
+        k<<<resident_grid(k, 256, 0, lanes), 256, 0, st>>>((const S*)chi, E, (S)eps, zp, zm);            \
+        break;                                                                                           \
+    }
     switch (T) {
-        case 2: k_hpr_edge_z<S, 2><<<grid, 256, 0, st>>>((const S*)chi, E, (S)eps, zp, zm); break;
-        case 3: k_hpr_edge_z<S, 3><<<grid, 256, 0, st>>>((const S*)chi, E, (S)eps, zp, zm); break;
-        case 4: k_hpr_edge_z<S, 4><<<grid, 256, 0, st>>>((const S*)chi, E, (S)eps, zp, zm); break;
-        case 5: k_hpr_edge_z<S, 5><<<grid, 256, 0, st>>>((const S*)chi, E, (S)eps, zp, zm); break;
+        MJX_EDGE_Z(2) MJX_EDGE_Z(3) MJX_EDGE_Z(4) MJX_EDGE_Z(5)
         default: return MJX_ERANGE;
     }
+#undef MJX_EDGE_Z
     MJX_LAUNCH_CHECK("k_hpr_edge_z");
     k_hpr_node_marg<S><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(zp, zm, out_row, n, d, (S*)marg);
     MJX_LAUNCH_CHECK("k_hpr_node_marg");

@@ -32,6 +32,7 @@
 // with a +1 pad per row (conflict-free strided reads).
 #pragma once
 #include "mjx_common.h"
+#include <stdlib.h>
 #include <type_traits>
 #include <utility>
 
@@ -143,22 +144,29 @@ struct Tabs {
 };
 
 // out[XB] for one compile-time x_a; returns the partial row sum.
-template <typename S, int T, int P, int D, int XA>
+template <int D>
+__device__ __forceinline__ int a_local_of(int lane) { return lane / D; }
+
+// HALF: the buffer holds only the valid-x_a half of each incoming row,
+// element x_k * 2^(T-1) + (x_a >> 1)
+template <typename S, int T, int P, int D, int XA, int RS = Cfg<S, T, P, D>::STRIDE, bool HALF = false>
 __device__ __forceinline__ S xa_messages(const S* __restrict__ rows, const S* __restrict__ bias, int a_local, int m,
                                          S w, S (&out)[1 << T]) {
     using C = Cfg<S, T, P, D>;
     using TB = Tabs<T, P, D, XA>;
     constexpr int X = C::X, K = C::K, BASE = C::BASE, NS = C::NS;
-    // M_j(x) for the d-1 incoming neighbours other than the receiver (slot m)
-    S M[D - 1][X];
-#pragma unroll
-    for (int j = 0; j < D - 1; ++j) {
+    // M_j(x) = bias_{k_j}(x[0]) chi^{k_j -> a}(x, x_a) for the d-1 incoming
+    // neighbours other than the receiver (slot m), read from LDS when needed:
+    // the first straight into the table, the middle ones by the convolution,
+    // the last one after the cumulative sums (short live ranges: VGPRs)
+    auto loadM = [&](int j, S (&Mj)[X]) {
         const int slot = a_local * D + (j < m ? j : j + 1);
         const S bp = bias[2 * slot], bm = bias[2 * slot + 1];
-        const S* r = rows + slot * C::STRIDE + XA;
+        constexpr int CS = HALF ? X / 2 : X;          // stride between x_k
+        const S* r = rows + slot * RS + (HALF ? (XA >> 1) : XA);
 #pragma unroll
-        for (int x = 0; x < X; ++x) M[j][x] = (x < X / 2 ? bp : bm) * r[x * X];
-    }
+        for (int x = 0; x < X; ++x) Mj[x] = (x < X / 2 ? bp : bm) * r[x * CS];
+    };
     // count table of the first K neighbours
     S tab[NS];
 #pragma unroll
@@ -166,24 +174,30 @@ __device__ __forceinline__ S xa_messages(const S* __restrict__ rows, const S* __
     if constexpr (K == 0) {
         tab[0] = S(1);
     } else {
+        {
+            S M0[X];
+            loadM(0, M0);
 #pragma unroll
-        for (int x = 0; x < X; ++x) tab[TB::v.xo[x]] = M[0][x];
+            for (int x = 0; x < X; ++x) tab[TB::v.xo[x]] = M0[x];
+        }
         // in place, sources in decreasing index: every target i + xo[x] > i has
         // already given up its own value, and the all-(-1) trajectory (xo = 0)
         // rescales the source itself (one table live instead of two: VGPRs)
 #pragma unroll
         for (int j = 1; j < K; ++j) {
+            S Mj[X];
+            loadM(j, Mj);
 #pragma unroll
             for (int i = NS - 1; i >= 0; --i) {
                 if (TB::v.maxd[i] <= j) {   // table holds j neighbours: digits <= j
                     const S t = tab[i];
 #pragma unroll
                     for (int x = 0; x < X; ++x) {
-                        if (TB::v.xo[x] == 0) tab[i] = t * M[j][x];
+                        if (TB::v.xo[x] == 0) tab[i] = t * Mj[x];
                     }
 #pragma unroll
                     for (int x = 0; x < X; ++x) {
-                        if (TB::v.xo[x] != 0) tab[i + TB::v.xo[x]] += t * M[j][x];
+                        if (TB::v.xo[x] != 0) tab[i + TB::v.xo[x]] += t * Mj[x];
                     }
                 }
             }
@@ -204,6 +218,9 @@ __device__ __forceinline__ S xa_messages(const S* __restrict__ rows, const S* __
         }
     }
     // fold in the last neighbour
+    S Ml[X];
+    __builtin_amdgcn_sched_barrier(0);
+    loadM(D - 2, Ml);
     S rs = S(0);
 #pragma unroll
     for (int xb = 0; xb < X; ++xb) {
@@ -211,7 +228,7 @@ __device__ __forceinline__ S xa_messages(const S* __restrict__ rows, const S* __
 #pragma unroll
         for (int x = 0; x < X; ++x) {
             const int cn = TB::v.cn[x][xb];
-            if (cn >= 0) acc += M[D - 2][x] * tab[cn];
+            if (cn >= 0) acc += Ml[x] * tab[cn];
         }
         acc *= w;
         out[xb] = acc;
@@ -339,22 +356,238 @@ k_hpr_update(const S* __restrict__ chi_in, S* __restrict__ chi_out, const S* __r
     MJX_PROF_MARK(3);
 }
 
+// ---- software-pipelined form (fp32, T = 4: 1 KB message rows) ---------------
+// One persistent 512-thread workgroup per CU walks tiles t = blockIdx.x,
+// + gridDim.x, ...; wave w owns the valid x_a 2w(+1) (XPW = 1).  Everything a
+// tile reads from HBM arrives by LDS-DMA (no VGPRs) while the previous work
+// computes:
+//   * the incoming rows of tile i+1, only their valid-x_a half (the update
+//     reads chi^{k->a}(x_k, x_a) for x_a[T-1] = attr only: 128 of 256
+//     columns), one float per lane (global_load_lds_dword), into buffer
+//     (i+1)&1 with a 129-float row stride (conflict-free M reads);
+//   * the old rows of tile i (damping), whole (global_load_lds_dwordx4, one
+//     row per wave instruction), at a 260-float stride (conflict-free
+//     16-B epilogue reads).
+// Row indices (wave-uniform, scalar loads) and biases are fetched one tile ahead.
+constexpr int PIPE_HRS = 129;       // half-row stride (floats) of the incoming-row buffers
+constexpr int PIPE_ORS = 260;       // old-row stride (floats): 1040 B, 16-B aligned DMA bases
+
+template <int T, int P, int D>
+struct PipeCfg {
+    using C = Cfg<float, T, P, D>;
+    static constexpr int NW = 8, NL = C::NL, NT = C::NT;
+    static constexpr int RPW = (NL + NW - 1) / NW;            // rows per wave per tile
+    static constexpr size_t BUF = (size_t)NL * PIPE_HRS;       // floats per incoming buffer
+    static constexpr size_t OLD = (size_t)NL * PIPE_ORS;       // floats of the old-row buffer
+    static constexpr size_t LDS = (2 * BUF + OLD + 2 * (size_t)NL * 2 + (size_t)NW * 64) * sizeof(float);
+};
+
+__device__ __forceinline__ void glds16(const float* gsrc, uint32_t lds_byte_addr) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_byte_addr)
+                 : "memory");
+}
+
+__device__ __forceinline__ void glds4(const float* gsrc, uint32_t lds_byte_addr) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_byte_addr)
+                 : "memory");
+}
+
+template <int T, int P, int D>
+__global__ void __launch_bounds__(512) k_hpr_update_pipe(const float* __restrict__ chi_in, float* __restrict__ chi_out,
+                                                          const float* __restrict__ biases,
+                                                          const int32_t* __restrict__ nbr,
+                                                          const int32_t* __restrict__ in_row,
+                                                          const int32_t* __restrict__ out_row, int64_t n,
+                                                          int attr_plus, float w_plus, float w_minus, float damp) {
+    using PC = PipeCfg<T, P, D>;
+    constexpr int X = 1 << T, NC = X * X, NT = PC::NT, NL = PC::NL, NW = PC::NW, RPW = PC::RPW;
+    static_assert(NC == 256, "pipelined HPR update: 1 KB rows (T = 4, fp32)");
+    static_assert(Cfg<float, T, P, D>::NVALID == NW, "one valid x_a per wave");
+    extern __shared__ __align__(16) unsigned char smem[];
+    float* rows = reinterpret_cast<float*>(smem);                 // [2][NL][PIPE_HRS] valid halves
+    float* oldb = rows + 2 * PC::BUF;                             // [NL][PIPE_ORS] old rows
+    float* bias = oldb + PC::OLD;                                 // [2][NL][2]
+    float* red = bias + 2 * NL * 2;                               // [NW][64]
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int64_t ntiles = (n + NT - 1) / NT;
+    const uint32_t rows_lds = (uint32_t)(uintptr_t)rows;
+    const uint32_t old_lds = (uint32_t)(uintptr_t)oldb;
+    const float keep = 1.0f - damp;
+    const int q = wave;                                           // valid x_a index
+    const int cv = (attr_plus ? 2 * q : 2 * q + 1) * X;           // valid block of every row
+    const int ci = (attr_plus ? 2 * q + 1 : 2 * q) * X;           // x_a[T-1] != attr: chi_new = 0
+    // column of half-row element h = x_k * 8 + (x_a >> 1)
+    const int hcol0 = (lane >> 3) * X + 2 * (lane & 7) + (attr_plus ? 0 : 1);
+
+    auto tile_nl = [&](int64_t t) -> int {
+        const int64_t a0 = t * NT;
+        return (int)((n - a0) < NT ? (n - a0) : NT) * D;
+    };
+    // wave-uniform row indices of this wave's slots wave*RPW + k of tile t (-1: none)
+    auto load_idx = [&](const int32_t* __restrict__ arr, int64_t t, int32_t (&ri)[RPW]) {
+        const int nl = t < ntiles ? tile_nl(t) : 0;
+#pragma unroll
+        for (int k = 0; k < RPW; ++k) {
+            const int slot = wave * RPW + k;
+            ri[k] = slot < nl ? __builtin_amdgcn_readfirstlane(arr[t * NT * D + slot]) : -1;
+        }
+    };
+    auto dma_in = [&](const int32_t (&ri)[RPW], int b) {           // valid halves -> buffer b
+#pragma unroll
+        for (int k = 0; k < RPW; ++k) {
+            if (ri[k] >= 0) {
+                const int slot = wave * RPW + k;
+                const float* src = chi_in + (int64_t)ri[k] * NC + hcol0;
+                const uint32_t dst = rows_lds + (uint32_t)((b * PC::BUF + (size_t)slot * PIPE_HRS) * sizeof(float));
+                glds4(src, dst);                                   // x_k 0..7
+                glds4(src + 8 * X, dst + 64 * sizeof(float));     // x_k 8..15
+            }
+        }
+    };
+    auto dma_old = [&](const int32_t (&ro)[RPW]) {                // whole old rows
+#pragma unroll
+        for (int k = 0; k < RPW; ++k) {
+            if (ro[k] >= 0) {
+                const int slot = wave * RPW + k;
+                glds16(chi_in + (int64_t)ro[k] * NC + lane * 4,
+                       old_lds + (uint32_t)((size_t)slot * PIPE_ORS * sizeof(float)));
+            }
+        }
+    };
+    // per-lane: source node of slot `lane` (its biases), own out row (the store)
+    auto load_lane = [&](const int32_t* __restrict__ arr, int64_t t) -> int32_t {
+        const int nl = t < ntiles ? tile_nl(t) : 0;
+        return lane < nl ? arr[t * NT * D + lane] : -1;
+    };
+
+    int64_t t = blockIdx.x;
+    if (t >= ntiles) return;
+    const int64_t G = gridDim.x;
+    // ---- prologue: tile t's rows and biases staged, the next tile's indices in hand
+    int32_t ri[RPW], ro[RPW];
+    load_idx(in_row, t, ri);
+    dma_in(ri, 0);
+    load_idx(in_row, t + G, ri);
+    load_idx(out_row, t, ro);
+    {
+        const int32_t nb = load_lane(nbr, t);
+        float bp = 0.f, bm = 0.f;
+        if (nb >= 0) {
+            bp = biases[2 * (int64_t)nb];
+            bm = biases[2 * (int64_t)nb + 1];
+        }
+        if (wave == 0 && lane < NL) {
+            bias[2 * lane] = bp;
+            bias[2 * lane + 1] = bm;
+        }
+    }
+    int32_t nb_next = load_lane(nbr, t + G);
+    int32_t orow = load_lane(out_row, t);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+
+    for (int it = 0; t < ntiles; ++it, t += G) {
+        const int b = it & 1;
+        const int nl = tile_nl(t);
+        const bool active = lane < nl;
+        // ---- stage 1 (all DMA): next tile's valid halves, this tile's old rows;
+        // next indices and biases into registers
+        dma_in(ri, 1 - b);
+        dma_old(ro);
+        load_idx(in_row, t + 2 * G, ri);
+        load_idx(out_row, t + G, ro);
+        float nbp = 0.f, nbm = 0.f;
+        if (nb_next >= 0) {
+            nbp = biases[2 * (int64_t)nb_next];
+            nbm = biases[2 * (int64_t)nb_next + 1];
+        }
+        nb_next = load_lane(nbr, t + 2 * G);
+        const int32_t orow_next = load_lane(out_row, t + G);
+        // ---- stage 2: compute from buffer b
+        const float* rb = rows + b * PC::BUF;
+        const float* bb = bias + b * NL * 2;
+        float out[X];
+        float rs = 0.f;
+        if (active) {
+            static_for<0, NW>([&](auto ww) {
+                constexpr int wv = decltype(ww)::value;
+                if (wave == wv) {
+                    constexpr int XP = 2 * wv, XM = 2 * wv + 1;
+                    const float wgt0 = (XP < X / 2) ? w_plus : w_minus;
+                    if (attr_plus) rs = xa_messages<float, T, P, D, XP, PIPE_HRS, true>(rb, bb, a_local_of<D>(lane),
+                                                                                         lane % D, wgt0, out);
+                    else rs = xa_messages<float, T, P, D, XM, PIPE_HRS, true>(rb, bb, a_local_of<D>(lane), lane % D,
+                                                                               wgt0, out);
+                }
+            });
+        }
+        red[wave * 64 + lane] = rs;
+        // every DMA of this wave landed (next halves, old rows), LDS writes done
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        // ---- stage 3: normalise, damp, store (code/HPR_pytorch_RRG.py:215)
+        if (active) {
+            float tot = 0.f;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) tot += red[w * 64 + lane];
+            const float inv = 1.0f / tot;
+            const float* ol = oldb + lane * PIPE_ORS;
+            float* dst = chi_out + (int64_t)orow * NC;
+#pragma unroll
+            for (int k = 0; k < X / 4; ++k) {
+                const float4 ov = *reinterpret_cast<const float4*>(ol + cv + 4 * k);
+                const float4 oi = *reinterpret_cast<const float4*>(ol + ci + 4 * k);
+                float4 v, z;
+                v.x = damp * (out[4 * k] * inv) + keep * ov.x;
+                v.y = damp * (out[4 * k + 1] * inv) + keep * ov.y;
+                v.z = damp * (out[4 * k + 2] * inv) + keep * ov.z;
+                v.w = damp * (out[4 * k + 3] * inv) + keep * ov.w;
+                z.x = keep * oi.x;
+                z.y = keep * oi.y;
+                z.z = keep * oi.z;
+                z.w = keep * oi.w;
+                *reinterpret_cast<float4*>(dst + cv + 4 * k) = v;
+                *reinterpret_cast<float4*>(dst + ci + 4 * k) = z;
+            }
+        }
+        if (wave == 0 && lane < NL) {              // next tile's biases (buffer 1-b)
+            bias[(1 - b) * NL * 2 + 2 * lane] = nbp;
+            bias[(1 - b) * NL * 2 + 2 * lane + 1] = nbm;
+        }
+        orow = orow_next;
+        // old-row buffer and buffer b free, next biases written
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    }
+}
+
 // ---- marginals (code/HPR_pytorch_RRG.py:147-167) ---------------------------
-// A group of G lanes per undirected edge r: Z sums of chi^{u->v}(x_u,x_v) chi^{v->u}(x_v,x_u)
-// by x_u[0] (row r) and by x_v[0] (row r+E), clamped at eps, normalised.  The
-// forward row is read in 16-B pieces (a whole 1 KB row per wave instruction at
-// T=4 fp32); the reverse row's transposed elements by 4-line gathers; U edge
-// groups per lane are in flight at once (the kernel is a stream over chi).
+// Z sums of chi^{u->v}(x_u,x_v) chi^{v->u}(x_v,x_u) by x_u[0] (row r) and by
+// x_v[0] (row r+E), clamped at eps, normalised.  A group of G = X lanes per
+// undirected edge: lane l reads 16-B pieces l, l+G, ... of row r (a group
+// instruction reads 16*G contiguous bytes) and, for each element, the
+// transposed element of row r+E by scalar loads (at T=4 fp32 a group
+// instruction reads 4 whole 64-B lines); the sums need log2(G) shuffle steps.  U edge groups per lane are in flight at once (the kernel is
+// a stream over chi).
 template <typename S, int T>
 __global__ void __launch_bounds__(256) k_hpr_edge_z(const S* __restrict__ chi, int64_t E, S eps,
                                                      S* __restrict__ zp, S* __restrict__ zm) {
     constexpr int X = 1 << T, NC = X * X;
     using V = typename Vec16<S>::T;
     constexpr int VN = Vec16<S>::N;
-    constexpr int G = NC / VN < 64 ? NC / VN : 64;   // lanes per edge
+    constexpr int G = X < 64 ? X : 64;               // lanes per edge
     constexpr int NV = NC / (VN * G);                // 16-B pieces per lane per row
     constexpr int EPW = 64 / G;                      // edges per wave instruction
-    constexpr int U = NV >= 4 ? 1 : 4 / NV;          // edge groups in flight per lane
+    constexpr int U = 2;                             // edge groups in flight per lane
     const int lane = threadIdx.x & 63;
     const int g = lane / G, l = lane % G;
     const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
@@ -364,46 +597,43 @@ __global__ void __launch_bounds__(256) k_hpr_edge_z(const S* __restrict__ chi, i
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int64_t r = base + u * EPW + g;
+            const int64_t rr = r < E ? r : E - 1;            // branch-free loads
 #pragma unroll
             for (int v = 0; v < NV; ++v) {
                 const int j0 = (v * G + l) * VN;
-                if (r < E) {
-                    const V x = *reinterpret_cast<const V*>(chi + r * NC + j0);
-                    const S* xs = reinterpret_cast<const S*>(&x);
+                const V x = *reinterpret_cast<const V*>(chi + rr * NC + j0);
+                const S* xs = reinterpret_cast<const S*>(&x);
 #pragma unroll
-                    for (int e = 0; e < VN; ++e) {
-                        f[u][v][e] = xs[e];
-                        const int xa = (j0 + e) / X, xb = (j0 + e) % X;
-                        b[u][v][e] = chi[(r + E) * NC + xb * X + xa];
-                    }
+                for (int e = 0; e < VN; ++e) {
+                    f[u][v][e] = xs[e];
+                    const int xu = (j0 + e) / X, xv = (j0 + e) % X;
+                    b[u][v][e] = chi[(rr + E) * NC + xv * X + xu];
                 }
             }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int64_t r = base + u * EPW + g;
-            S fp = 0, fm = 0, bp = 0, bm = 0;
-            if (r < E) {
+            S sp = 0, sm = 0, bp = 0, bm = 0;            // by x_u[0], by x_v[0]
 #pragma unroll
-                for (int v = 0; v < NV; ++v)
+            for (int v = 0; v < NV; ++v)
 #pragma unroll
-                    for (int e = 0; e < VN; ++e) {
-                        const int j = (v * G + l) * VN + e;
-                        const int xa = j / X, xb = j % X;
-                        const S z = f[u][v][e] * b[u][v][e];
-                        if (xa < X / 2) fp += z; else fm += z;
-                        if (xb < X / 2) bp += z; else bm += z;
-                    }
-            }
+                for (int e = 0; e < VN; ++e) {
+                    const int j = (v * G + l) * VN + e;
+                    const int xu = j / X, xv = j % X;
+                    const S z = f[u][v][e] * b[u][v][e];
+                    if (xu < X / 2) sp += z; else sm += z;
+                    if (xv < X / 2) bp += z; else bm += z;
+                }
 #pragma unroll
             for (int off = G / 2; off > 0; off >>= 1) {
-                fp += __shfl_xor(fp, off, 64);
-                fm += __shfl_xor(fm, off, 64);
+                sp += __shfl_xor(sp, off, 64);
+                sm += __shfl_xor(sm, off, 64);
                 bp += __shfl_xor(bp, off, 64);
                 bm += __shfl_xor(bm, off, 64);
             }
             if (l == 0 && r < E) {
-                fp = fp > eps ? fp : eps; fm = fm > eps ? fm : eps;
+                S fp = sp > eps ? sp : eps, fm = sm > eps ? sm : eps;
                 bp = bp > eps ? bp : eps; bm = bm > eps ? bm : eps;
                 const S sf = fp + fm, sb = bp + bm;
                 zp[r] = fp / sf; zm[r] = fm / sf;
@@ -459,6 +689,31 @@ static int launch_update(const void* chi_in, void* chi_out, const void* biases, 
     } else {
         const int64_t tiles = (n + C::NT - 1) / C::NT;
         if (tiles > INT32_MAX) return MJX_ERANGE;
+        if constexpr (std::is_same<S, float>::value && T == 4) {
+            // 1 KB rows: the software-pipelined persistent form (MJX_HPR_PIPE=0 selects the other)
+            static const bool pipe = [] {
+                const char* e = getenv("MJX_HPR_PIPE");
+                return !(e && e[0] == '0');
+            }();
+            if (pipe) {
+                using PC = PipeCfg<T, P, D>;
+                auto pk = k_hpr_update_pipe<T, P, D>;
+                static bool pattr = false;
+                if (!pattr) {
+                    MJX_HIP(hipFuncSetAttribute((const void*)pk, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                (int)PC::LDS), "hpr pipe set lds");
+                    pattr = true;
+                }
+                const int per = resident_blocks_per_cu((const void*)pk, 512, PC::LDS);
+                int64_t grid = (int64_t)kCUs * (per > 0 ? per : 1);
+                if (grid > tiles) grid = tiles;
+                pk<<<(unsigned)grid, 512, PC::LDS, st>>>((const float*)chi_in, (float*)chi_out, (const float*)biases,
+                                                         nbr, in_row, out_row, n, attr_plus, (float)w_plus,
+                                                         (float)w_minus, (float)damp);
+                MJX_LAUNCH_CHECK("k_hpr_update_pipe");
+                return MJX_OK;
+            }
+        }
         auto kern = k_hpr_update<S, T, P, D>;
         static bool attr_set = false;   // per instantiation: opt in to > 64 KiB dynamic LDS once
         if (!attr_set) {
