@@ -99,7 +99,8 @@ def load(build_if_missing=False):
     global _LIB
     if _LIB is not None:
         return _LIB
-    path = _build.LIB
+    # MJX_LIB: an alternative build of the same library (profiling variants)
+    path = os.environ.get("MJX_LIB") or _build.LIB
     if not os.path.exists(path):
         if build_if_missing:
             _build.build()

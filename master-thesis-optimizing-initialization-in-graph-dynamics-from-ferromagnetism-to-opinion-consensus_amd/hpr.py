@@ -199,51 +199,94 @@ class HPRState:
         HPr_dp(self.chi, self.biases, self.plan, self.p, self.c, self.attr_value, self.lmbd_in, self.damppar,
                out=self.chi_b)
         self.chi, self.chi_b = self.chi_b, self.chi
+        self._graph = None                   # a captured batch holds the old buffer roles
         marginals_comp(self.chi, self.plan, self.p, self.c, zwork=self.zwork, out=self.marg)
         new_biases_i(self.biases, self.pie, self.gamma, self.marg, self.t, u=u, generator=generator, s_out=self.s)
         self.t += 1
         return self.sum_end()
 
-    def steps_batched(self, k, generator):
-        """k iterations of the main loop (code/HPR_pytorch_RRG.py:345-356) with no
-        host read in between: the k uniform vectors are drawn up front from the
-        CPU generator in the reference's order (one torch.rand(n) per iteration,
-        :142), every iteration's trial configuration and sum(s_endstate(s)) are
-        kept on the device, and one read returns them all.
-        Returns (sums[k] int64 numpy, s_hist (k, n) int32 device tensor)."""
-        n = self.plan.n
-        dev = self.s.device
-        u = torch.stack([torch.rand(n, dtype=torch.float64, generator=generator) for _ in range(k)]).to(dev)
-        s_hist = torch.empty((k, n), dtype=torch.int32, device=dev)
-        cnt = torch.zeros(k, dtype=torch.int64, device=dev)
-        bits = torch.empty((n + 63) // 64, dtype=torch.int64, device=dev)
-        T = self.p + self.c - 1
+    # -- batches of the main loop on the device ----------------------------------
+    def _batch_buffers(self, k):
+        if getattr(self, "_bk", None) != k:
+            n, dev = self.plan.n, self.s.device
+            self._bk = k
+            self._u = torch.empty((k, n), dtype=torch.float64, device=dev)
+            self._s_hist = torch.empty((k, n), dtype=torch.int32, device=dev)
+            self._cnt = torch.zeros(k, dtype=torch.int64, device=dev)
+            self._bits = torch.empty((n + 63) // 64, dtype=torch.int64, device=dev)
+            self._rtmp = (torch.empty_like(self._bits), torch.empty_like(self._bits))
+            self._graph = None
+
+    def _batch_launches(self, k):
+        """The launches of k iterations (code/HPR_pytorch_RRG.py:345-356) on the
+        current stream, every argument fixed: iteration j reads the messages from
+        buffer j % 2 and writes the other (k even: the batch ends where it
+        started); its uniforms are row j of self._u (already compared with the
+        reinforcement threshold, see steps_batched), its trial configuration goes
+        to row j of self._s_hist and sum(s_endstate(s)) to self._cnt[j]."""
+        n, T, st = self.plan.n, self.p + self.c - 1, _device.stream_handle()
+        self._cnt.zero_()
         for j in range(k):
-            HPr_dp(self.chi, self.biases, self.plan, self.p, self.c, self.attr_value, self.lmbd_in, self.damppar,
-                   out=self.chi_b)
-            self.chi, self.chi_b = self.chi_b, self.chi
-            marginals_comp(self.chi, self.plan, self.p, self.c, zwork=self.zwork, out=self.marg)
-            new_biases_i(self.biases, self.pie, self.gamma, self.marg, self.t + j, u=u[j], s_out=s_hist[j])
-            _lib.call("mjx_pack_np", _device.ptr(s_hist[j]), _lib.MJX_I32, n, _device.ptr(bits),
-                      _device.stream_handle())
+            src, dst = (self.chi, self.chi_b) if j % 2 == 0 else (self.chi_b, self.chi)
+            HPr_dp(src, self.biases, self.plan, self.p, self.c, self.attr_value, self.lmbd_in, self.damppar, out=dst)
+            marginals_comp(dst, self.plan, self.p, self.c, zwork=self.zwork, out=self.marg)
+            _lib.call("mjx_hpr_new_biases", _code(self.dtype), _device.ptr(self.biases), _device.ptr(self.marg),
+                      _device.ptr(self._u[j]), 0.5, self.pie, n, _device.ptr(self._s_hist[j]), st)
+            _lib.call("mjx_pack_np", _device.ptr(self._s_hist[j]), _lib.MJX_I32, n, _device.ptr(self._bits), st)
             if T:
-                rollout(self.plan.graph, bits, T, counts=cnt[j:j + 1])
+                rollout(self.plan.graph, self._bits, T, out=self._rtmp[0], tmp=self._rtmp[1],
+                        counts=self._cnt[j:j + 1])
             else:
-                _lib.call("mjx_popcount_np", _device.ptr(bits), n, _device.ptr(cnt[j:j + 1]),
-                          _device.stream_handle())
+                _lib.call("mjx_popcount_np", _device.ptr(self._bits), n, _device.ptr(self._cnt[j:j + 1]), st)
+
+    def steps_batched(self, k, generator, graph=True):
+        """k iterations of the main loop (code/HPR_pytorch_RRG.py:345-356) with no
+        host read in between; one read returns every iteration's
+        sum(s_endstate(s)).  The k uniform vectors are drawn up front from the
+        CPU generator in the reference's order (one torch.rand(n) per iteration,
+        :142) and compared on the host with that iteration's threshold
+        1-(1+t)^-gamma (the same float64 comparison the reference makes), so
+        the device batch has no per-iteration argument: after one eager batch
+        it is captured once as a hipGraph and replayed (``graph``).
+        Returns (sums[k] int64 numpy, s_hist (k, n) int32 device tensor,
+        generator state before the draws)."""
+        if k % 2:
+            raise ValueError("batch size must be even (the message buffers alternate)")
+        self._batch_buffers(k)
+        n = self.plan.n
+        g_state = generator.get_state()
+        sel = torch.empty((k, n), dtype=torch.float64)
+        for j in range(k):
+            u = torch.rand(n, dtype=torch.float64, generator=generator)
+            thresh = 1 - (1 + (self.t + j)) ** (-self.gamma)            # code/HPR_pytorch_RRG.py:142
+            sel[j] = torch.where(u < thresh, 0.0, 1.0)                  # kernel: refresh iff sel < 0.5
+        self._u.copy_(sel)
+        if graph and self._graph is not None:
+            self._graph.replay()
+        elif graph and getattr(self, "_warm", False):
+            self._graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self._graph):
+                self._batch_launches(k)
+            self._graph.replay()
+        else:
+            self._batch_launches(k)
+            self._warm = True
         self.t += k
-        self.s.copy_(s_hist[k - 1])
-        return 2 * cnt.cpu().numpy() - n, s_hist
+        self.s.copy_(self._s_hist[k - 1])
+        return 2 * self._cnt.cpu().numpy() - n, self._s_hist, g_state
 
 
 def hpr_run(d, n, p, c, damppar=0.4, attr_value=1, lmbd_in=None, pie=0.3, gamma=0.1, TT=10000, edges=None,
-            nbrs=None, seed=0, dtype=torch.float32, chi0=None, biases0=None, generator=None, batch=16):
+            nbrs=None, seed=0, dtype=torch.float32, chi0=None, biases0=None, generator=None, batch=16, graph=True):
     """The HPR experiment of code/HPR_pytorch_RRG.py:224-377 for one graph.
 
     Randomness follows the reference: with ``generator`` a torch CPU generator
     (default: seeded with ``seed``), chi0 = rand(2E, 4^T) row-normalised,
     biases0 = rand(n, 2) row-normalised (:329-335) and one rand(n) per
-    iteration (:142), all float64 like the reference's default dtype.
+    iteration (:142), all float64 like the reference's default dtype.  The
+    loop runs in device batches of ``batch`` iterations (one host read each,
+    replayed as a hipGraph with ``graph``); on return the generator has made
+    exactly the draws the reference makes up to its stop iteration.
     Returns the np.savez keys of :377 (mag_reached, conf, num_steps, graphs).
     """
     from .graph import random_regular_edges
@@ -270,8 +313,8 @@ def hpr_run(d, n, p, c, damppar=0.4, attr_value=1, lmbd_in=None, pie=0.3, gamma=
             # `batch` iterations per host read; the run stops at the first
             # iteration the reference would stop at (t > TT, or consensus)
             t0 = st.t
-            sums, s_hist = st.steps_batched(batch, generator)
-            for j in range(batch):
+            sums, s_hist, g_state = st.steps_batched(batch + batch % 2, generator, graph=graph)
+            for j in range(batch + batch % 2):
                 t = t0 + j + 1
                 if t > TT:
                     m_final = 2
@@ -280,6 +323,10 @@ def hpr_run(d, n, p, c, damppar=0.4, attr_value=1, lmbd_in=None, pie=0.3, gamma=
                 if m_final >= 1:
                     st.t = t
                     s_dev = s_hist[j]
+                    # leave the generator where the reference's would be: j+1 draws
+                    generator.set_state(g_state)
+                    for _ in range(j + 1):
+                        torch.rand(n, dtype=torch.float64, generator=generator)
                     break
             else:
                 s_dev = st.s

@@ -126,3 +126,47 @@ def test_hpr_c3_size_against_sampled_oracle_rows(mjx_mod):
     marg = mjx_mod.marginals_comp(new, plan, p, c)
     m = marg.cpu().numpy()
     assert np.all(np.isfinite(m)) and np.max(np.abs(m.sum(1) - 1)) < 1e-5
+
+
+@pytest.mark.parametrize("n,p,c", [(4102, 2, 2), (3000, 1, 3), (2050, 3, 1)])
+def test_hpr_t4_pipelined_update_partial_tiles(mjx_mod, n, p, c):
+    """T = 4 fp32 runs the software-pipelined kernel: sizes whose last tile is
+    partial and that give several tiles per workgroup, every P, against the
+    float64 oracle on sampled rows (1e-5 row-normalised)."""
+    d = 4
+    edges = mjx_mod.random_regular_edges(d, n, seed=n)
+    plan = mjx_mod.HPRPlan(edges, n, d)
+    g = torch.Generator().manual_seed(n)
+    nc = 4 ** (p + c)
+    chi0 = torch.rand((2 * plan.E, nc), dtype=torch.float64, generator=g)
+    chi0 /= chi0.sum(1, keepdim=True)
+    b0 = torch.rand((n, 2), dtype=torch.float64, generator=g)
+    b0 /= b0.sum(1, keepdim=True)
+    chi = chi0.to(torch.float32).cuda()
+    b = b0.to(torch.float32).cuda()
+    inr, src = orc.incoming_rows(edges, plan.nbrs_host)
+    rows = np.concatenate([np.arange(64), np.arange(2 * plan.E - 64, 2 * plan.E),
+                           np.random.default_rng(1).choice(2 * plan.E, 200, replace=False)])
+    for attr in (1, -1):
+        new = mjx_mod.HPr_dp(chi, b, plan, p, c, attr, 25 * n, 0.4)
+        want = orc.HPr_dp(chi.cpu().double().numpy(), b.cpu().double().numpy(), inr, src, n, d, p, c, attr, 25 * n,
+                          0.4, rows=rows)
+        assert rownorm_err(new[torch.from_numpy(rows).cuda()].cpu().numpy(), want) <= 1e-5, attr
+
+
+def test_hpr_run_graph_batches_equal_eager_loop(mjx_mod):
+    """hpr_run in hipGraph-replayed device batches (one host read per batch)
+    equals the per-iteration eager loop: same stop, same conf, and the CPU
+    generator left exactly where the reference's would be."""
+    n, d, p, c = 200, 3, 2, 1
+    edges = mjx_mod.random_regular_edges(d, n, seed=5)
+    out = {}
+    for mode in ("eager", "batch", "graph"):
+        g = torch.Generator().manual_seed(11)
+        kw = dict(batch=0) if mode == "eager" else dict(batch=8, graph=(mode == "graph"))
+        res = mjx_mod.hpr_run(d, n, p, c, TT=150, edges=edges, seed=11, dtype=torch.float64, generator=g, **kw)
+        out[mode] = (res, torch.rand(4, dtype=torch.float64, generator=g))
+    for mode in ("batch", "graph"):
+        assert out[mode][0]["num_steps"][0] == out["eager"][0]["num_steps"][0]
+        assert np.array_equal(out[mode][0]["conf"], out["eager"][0]["conf"])
+        assert torch.equal(out[mode][1], out["eager"][1])
