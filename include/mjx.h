@@ -235,6 +235,33 @@ int mjx_hpr_marginals(int dtype, const void* chi, const int32_t* out_row, int64_
  * place and writes s[n] = +-1 (int32, nullable). */
 int mjx_hpr_new_biases(int dtype, void* biases, const void* marg, const double* u, double thresh,
                        double pie, int64_t n, int32_t* s, void* stream);
+/* The edge half of marginals_comp (code/HPR_pytorch_RRG.py:150-161) alone:
+ * zwork[4E] = per-row normalised (Z+ [2E], Z- [2E]) of every directed row. */
+int mjx_hpr_edge_z(int dtype, const void* chi, int64_t E, int p, int c, double eps, void* zwork,
+                   void* stream);
+
+/* ---- HPR on Erdos-Renyi graphs (the "general (ER)" HPR of code/README.md:1) -
+ * HPr_dp with the degree taken per message: rows of degree class D (the
+ * message a->b with deg(a) = D+1, rows[m] of them) read their D incoming rows
+ * inc[m*D + j] (messages k_j -> a, k_j != b) whose senders are inc_src[m*D + j],
+ * with the reinforced messages bias_k(x_k[0]) chi^{k->a} and the trajectory
+ * factor of d-1 = D (code/HPR_pytorch_RRG.py:14-39,128-133,183-218); same row,
+ * column and bias layouts as mjx_hpr_update.  Jacobi: every class reads chi_in
+ * and writes its rows of chi_out.  w_plus/w_minus = exp(-lmbd*x_a[0]/n);
+ * 2 <= p+c <= 4, any D <= 255.  A class whose count table (2^(T-1)*(D+1)^T
+ * elements per message) does not fit the 160 KiB LDS keeps it in `scratch`:
+ * mjx_hpr_er_scratch_bytes(dtype, D, p, c) per message in flight (0: LDS
+ * suffices, -1: unsupported); the call then runs ceil(m / (scratch_bytes /
+ * that)) launches (MJX_ERANGE if scratch holds not even one table). */
+int64_t mjx_hpr_er_scratch_bytes(int dtype, int D, int p, int c);
+int mjx_hpr_er_update_class(int dtype, const void* chi_in, void* chi_out, const void* biases,
+                            const int32_t* rows, const int32_t* inc, const int32_t* inc_src, int64_t m,
+                            int D, int p, int c, int attr_value, double w_plus, double w_minus,
+                            double damp, void* scratch, int64_t scratch_bytes, void* stream);
+/* node marginals over CSR out-rows (row of i->k for every neighbour k of i):
+ * marg[i] = normalised (prod Z+, prod Z-) of zwork from mjx_hpr_edge_z. */
+int mjx_hpr_node_marg_csr(int dtype, const void* zwork, int64_t E, const int64_t* out_ptr,
+                          const int32_t* out_rows, int64_t n, void* marg, void* stream);
 
 /* ---- one giant graph partitioned by node range -- */
 /* One synchronous sweep of the rows [row_lo, row_hi) of a node-packed state.
@@ -308,9 +335,14 @@ int mjx_graph_check_ell(const int32_t* adj, int64_t n, int d, unsigned long long
  * T = p + c <= 4.  An "edge class" is the set of messages a -> b with
  * deg(a) - 1 = D (nb:312-318): rows[m] are their chi rows, inc[m*D + k] the
  * rows of the D incoming messages k -> a (the notebook's N_edges_pos_dm1).
- * mjx_bdcm_lds_bytes(D, p, c) must be <= 160 KiB (else MJX_ERANGE).
+ * Any D <= 255: the count table of an item (2^(T-1)*(D+1)^T doubles) lives in
+ * LDS when mjx_bdcm_lds_bytes(D, p, c) <= 160 KiB, else in the caller's
+ * `scratch` slab, mjx_bdcm_scratch_bytes(D, p, c) per item in flight (0: LDS
+ * suffices, -1: unsupported); the call then runs ceil(m / (scratch_bytes /
+ * that)) launches (MJX_ERANGE if the slab holds not even one table).
  */
 int64_t mjx_bdcm_lds_bytes(int D, int p, int c);
+int64_t mjx_bdcm_scratch_bytes(int D, int p, int c);
 /* One class of BDCM_ER (nb:150-196): new rows = damp*normalize(max(chi2, eps))
  * + (1-damp)*old, written to upd[m*4^T] and then committed into chi (the class
  * reads chi before any of its own rows change: Jacobi within a class,
@@ -319,11 +351,12 @@ int64_t mjx_bdcm_lds_bytes(int D, int p, int c);
  * delta_bits (nullable): atomic max of |new - old| as IEEE bits (a NaN wins). */
 int mjx_bdcm_update_class(double* chi, const int32_t* rows, const int32_t* inc, int64_t m, int D, int p, int c,
                           int attr_value, double lmbd, double damp, double eps, double* upd,
-                          unsigned long long* delta_bits, void* stream);
+                          unsigned long long* delta_bits, void* scratch, int64_t scratch_bytes, void* stream);
 /* Zi_ER for the m nodes of degree D (nb:211-276): zi[nodes[k]] = max(Zi, eps);
  * inc[k*D + j] = row of the message from the j-th neighbour into the node. */
 int mjx_bdcm_node_z(const double* chi, const int32_t* nodes, const int32_t* inc, int64_t m, int D, int p, int c,
-                    int attr_value, double lmbd, double eps, double* zi, void* stream);
+                    int attr_value, double lmbd, double eps, double* zi, void* scratch, int64_t scratch_bytes,
+                    void* stream);
 /* Zij (nb:200-209) and the per-edge term of avg_m_init (nb:379-392);
  * edges[2E] = G.edges (u, v) pairs, deg[n] node degrees; m_term nullable. */
 int mjx_bdcm_edge_obs(const double* chi, const int32_t* edges, const int32_t* deg, int64_t E, int p, int c,

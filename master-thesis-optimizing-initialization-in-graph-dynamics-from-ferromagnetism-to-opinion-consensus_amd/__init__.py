@@ -15,6 +15,7 @@ from .npz import save_sa_npz, save_hpr_npz, save_bdcm_npz, sa_arrays, hpr_arrays
 from .dynamics import onestep_majority, s_endstate, m, pack, unpack, rollout, popcount, as_graph
 from .sa import SAReplicas, E_delta, sa_run, schedule_constants
 from .hpr import HPRPlan, HPRState, HPr_dp, marginals_comp, new_biases_i, hpr_run
+from .hpr_er import HPRERPlan, HPr_dp_er, marginals_comp_er, hpr_er_plan, hpr_er_run
 from .bdcm import (BDCMPlan, bdcm_er_plan, BDCM_ER, bdcm_leaf_reset, Zij, Zi_ER, phi_BP_GENERAL_ER,
                    avg_m_init_GENERAL_ER, BDCM_entropy_procedure_GENERAL_ER, bdcm_er_run)
 
@@ -24,6 +25,7 @@ __all__ = [
     "onestep_majority", "s_endstate", "m", "pack", "unpack", "rollout", "popcount", "as_graph",
     "SAReplicas", "E_delta", "sa_run", "schedule_constants",
     "HPRPlan", "HPRState", "HPr_dp", "marginals_comp", "new_biases_i", "hpr_run",
+    "HPRERPlan", "HPr_dp_er", "marginals_comp_er", "hpr_er_plan", "hpr_er_run",
     "BDCMPlan", "bdcm_er_plan", "BDCM_ER", "bdcm_leaf_reset", "Zij", "Zi_ER", "phi_BP_GENERAL_ER",
     "avg_m_init_GENERAL_ER", "BDCM_entropy_procedure_GENERAL_ER", "bdcm_er_run",
 ]

@@ -22,6 +22,7 @@ UNITS = [
     ("mjx_hpr.hip", []),
     ("mjx_hpr_f32.hip", []),
     ("mjx_hpr_f64.hip", []),
+    ("mjx_hpr_er.hip", []),
     ("mjx_bdcm.hip", ["-ffp-contract=off"]),
     ("mjx_graph.hip", []),
 ]

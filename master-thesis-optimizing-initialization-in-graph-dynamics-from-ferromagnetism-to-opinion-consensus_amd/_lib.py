@@ -50,6 +50,11 @@ SIGNATURES = {
                        c_dbl, c_dbl, c_dbl, c_vp],
     "mjx_hpr_marginals": [c_int, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_dbl, c_vp, c_vp, c_vp],
     "mjx_hpr_new_biases": [c_int, c_vp, c_vp, c_vp, c_dbl, c_dbl, c_i64, c_vp, c_vp],
+    "mjx_hpr_edge_z": [c_int, c_vp, c_i64, c_int, c_int, c_dbl, c_vp, c_vp],
+    "mjx_hpr_er_scratch_bytes": [c_int, c_int, c_int, c_int],
+    "mjx_hpr_er_update_class": [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_int,
+                                c_dbl, c_dbl, c_dbl, c_vp, c_i64, c_vp],
+    "mjx_hpr_node_marg_csr": [c_int, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp],
     "mjx_sweep_ell_np_range": [c_vp, c_i64, c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp],
     "mjx_rrg_generate": [c_i64, c_int, c_u64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp],
     "mjx_rrg_partner_host": [c_i64, c_int, c_u64, c_i64],
@@ -60,15 +65,17 @@ SIGNATURES = {
     "mjx_binned_build": [c_vp, c_i64, c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp],
     "mjx_sweep_binned": [c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp],
     "mjx_bdcm_lds_bytes": [c_int, c_int, c_int],
+    "mjx_bdcm_scratch_bytes": [c_int, c_int, c_int],
     "mjx_bdcm_update_class": [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_int, c_dbl, c_dbl, c_dbl, c_vp,
-                              c_vp, c_vp],
-    "mjx_bdcm_node_z": [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_int, c_dbl, c_dbl, c_vp, c_vp],
+                              c_vp, c_vp, c_i64, c_vp],
+    "mjx_bdcm_node_z": [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_int, c_dbl, c_dbl, c_vp, c_vp, c_i64,
+                        c_vp],
     "mjx_bdcm_edge_obs": [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_dbl, c_vp, c_vp, c_vp],
     "mjx_sum_f64": [c_vp, c_i64, c_int, c_vp, c_vp, c_vp],
 }
 _RESTYPES = {"mjx_strerror": ctypes.c_char_p, "mjx_last_hip_error": ctypes.c_char_p,
-             "mjx_sa_lightcone_lds": c_i64, "mjx_bdcm_lds_bytes": c_i64,
-             "mjx_rrg_partner_host": c_i64, "mjx_er_work_bytes": c_i64}
+             "mjx_sa_lightcone_lds": c_i64, "mjx_bdcm_lds_bytes": c_i64, "mjx_bdcm_scratch_bytes": c_i64,
+             "mjx_rrg_partner_host": c_i64, "mjx_er_work_bytes": c_i64, "mjx_hpr_er_scratch_bytes": c_i64}
 
 MJX_OK, MJX_EINVAL, MJX_EHIP, MJX_ERANGE = 0, 1, 2, 3      # status codes (include/mjx.h)
 MJX_I8, MJX_I32, MJX_I64 = 1, 4, 8

@@ -104,13 +104,28 @@ class BDCMPlan:
     def classes(self):
         return [D for D, _, _, _ in self.edge_classes]
 
-    def check_sizes(self, p, c):
-        """Raise MjxError if some class exceeds the kernels' LDS budget."""
+    SCRATCH_CAP = 256 << 20          # bytes of count tables in flight for the high-degree classes
+
+    def scratch(self, p, c):
+        """Global slab for the count tables of the classes beyond the LDS budget
+        (None if every class fits); raises MjxError if a class is unsupported."""
         lib = _lib.load()
-        for D in set(self.classes) | {D for D, _, _, _ in self.node_classes}:
-            b = lib.mjx_bdcm_lds_bytes(D, int(p), int(c))
-            if b < 0 or b > 160 * 1024:
-                raise _lib.MjxError(f"BDCM class D={D} at p+c={p + c} needs {b} B of LDS (> 160 KiB)")
+        need = 0
+        for D, _, _, m in list(self.edge_classes) + list(self.node_classes):
+            b = lib.mjx_bdcm_scratch_bytes(D, int(p), int(c))
+            if b < 0:
+                raise _lib.MjxError(f"BDCM class D={D} at p+c={p + c} is unsupported")
+            need = max(need, min(b * m, max(b, self.SCRATCH_CAP)))
+        key = (int(p), int(c))
+        if need and getattr(self, "_scratch_key", None) != key:
+            self._scratch = torch.empty(need, dtype=torch.uint8, device=self.device)
+            self._scratch_key = key
+        return self._scratch if need else None
+
+    def check_sizes(self, p, c):
+        """Raise MjxError if some class is unsupported (tables beyond the LDS
+        budget run from a global scratch slab)."""
+        self.scratch(p, c)
 
     def upd(self, nc):
         need = max((m for _, _, _, m in self.edge_classes), default=0) * nc
@@ -150,11 +165,16 @@ def _chi2d(chi, plan, p, c):
     return chi.view(2 * plan.E, nc)
 
 
+def _scratch_args(plan, p, c):
+    sc = plan.scratch(p, c)
+    return (_device.ptr(sc), sc.numel()) if sc is not None else (None, 0)
+
+
 def _update(ch, plan, D, rows, inc, m, p, c, attr_value, lmbd, damp, eps, delta):
     _lib.call("mjx_bdcm_update_class", _device.ptr(ch), _device.ptr(rows), _device.ptr(inc) if D else None, m, D,
               int(p), int(c), int(attr_value), float(lmbd), float(damp), float(eps),
               _device.ptr(plan.upd(ch.shape[1])), _device.ptr(delta) if delta is not None else None,
-              _device.stream_handle())
+              *_scratch_args(plan, p, c), _device.stream_handle())
 
 
 def BDCM_ER(chi, plan, p, c, attr_value, lmbd_in, damppar, epsilon=0.0, delta=None):
@@ -195,7 +215,8 @@ def Zi_ER(chi, plan, p, c, attr_value, lmbd_in, epsilon=0.0):
     zi = torch.empty(plan.n_core, dtype=torch.float64, device=ch.device)
     for (D, nodes, inc, m) in plan.node_classes:
         _lib.call("mjx_bdcm_node_z", _device.ptr(ch), _device.ptr(nodes), _device.ptr(inc), m, D, int(p), int(c),
-                  int(attr_value), float(lmbd_in), float(epsilon), _device.ptr(zi), _device.stream_handle())
+                  int(attr_value), float(lmbd_in), float(epsilon), _device.ptr(zi), *_scratch_args(plan, p, c),
+                  _device.stream_handle())
     return zi
 
 

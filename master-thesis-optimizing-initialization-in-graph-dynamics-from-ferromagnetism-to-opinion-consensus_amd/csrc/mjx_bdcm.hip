@@ -65,9 +65,9 @@ static bool make_geo(int D, int p, int c, int attr_value, Geo* g) {
     return true;
 }
 
-static size_t lds_bytes(const Geo& g) {
-    return ((size_t)g.XV * g.S + (size_t)g.D * g.XV * g.XV) * sizeof(double);
-}
+static size_t tab_bytes(const Geo& g) { return (size_t)g.XV * g.S * sizeof(double); }
+static size_t m_bytes(const Geo& g) { return (size_t)g.D * g.XV * g.XV * sizeof(double); }
+static size_t lds_bytes(const Geo& g) { return tab_bytes(g) + m_bytes(g); }
 
 // the spin the condition on rho_t must produce, and the spin a tie keeps
 // (traj_condition for t < T-1, atr_condition for t = T-1; nb:66-83)
@@ -193,14 +193,17 @@ __device__ void build_table(const Geo& g, const double* __restrict__ chi, const 
 
 // BDCM_ER for one edge class (nb:150-196), new rows into upd[m][NC].
 // damp >= 1 assigns normalize(chi2) (the leaf reset of nb:404-417 is class D = 0).
+// The count table lives in LDS, or (a class whose table exceeds the LDS budget)
+// in the global slab gtab, one table per workgroup of the launch; item e0 + blockIdx.x.
 __global__ void __launch_bounds__(64) k_bdcm_edge(const double* __restrict__ chi, const int32_t* __restrict__ rows,
                                                   const int32_t* __restrict__ inc, Geo g, double w_plus,
-                                                  double w_minus, double eps, double damp, double* __restrict__ upd) {
+                                                  double w_minus, double eps, double damp, double* __restrict__ upd,
+                                                  int64_t e0, double* __restrict__ gtab) {
     extern __shared__ __align__(16) double sm[];
-    double* tab = sm;
-    double* M = sm + (size_t)g.XV * g.S;
+    double* M = sm;
+    double* tab = gtab ? gtab + (size_t)blockIdx.x * g.XV * g.S : sm + (size_t)g.D * g.XV * g.XV;
     const int lane = threadIdx.x;
-    const int64_t e = blockIdx.x;
+    const int64_t e = e0 + blockIdx.x;
     build_table(g, chi, inc, e, tab, M, lane);
     const int X = g.X, NC = X * X;
     double v[4];
@@ -260,12 +263,13 @@ __global__ void __launch_bounds__(256) k_bdcm_commit(double* __restrict__ chi, c
 // Zi_ER for one node-degree class (nb:211-276): zi[node] = max(sum_xa w Ai LL, eps)
 __global__ void __launch_bounds__(64) k_bdcm_node(const double* __restrict__ chi, const int32_t* __restrict__ nodes,
                                                   const int32_t* __restrict__ inc, Geo g, double w_plus,
-                                                  double w_minus, double eps, double* __restrict__ zi) {
+                                                  double w_minus, double eps, double* __restrict__ zi, int64_t e0,
+                                                  double* __restrict__ gtab) {
     extern __shared__ __align__(16) double sm[];
-    double* tab = sm;
-    double* M = sm + (size_t)g.XV * g.S;
+    double* M = sm;
+    double* tab = gtab ? gtab + (size_t)blockIdx.x * g.XV * g.S : sm + (size_t)g.D * g.XV * g.XV;
     const int lane = threadIdx.x;
-    const int64_t e = blockIdx.x;
+    const int64_t e = e0 + blockIdx.x;
     build_table(g, chi, inc, e, tab, M, lane);
     double z = 0.0;
     if (lane < g.XV) {
@@ -336,12 +340,24 @@ __global__ void __launch_bounds__(256) k_sum_final(const double* __restrict__ pa
 }
 
 template <typename K>
-static int set_lds(K kern, size_t lds) {
-    if (lds > 64 * 1024) {
-        MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+static int set_lds(K kern) {
+    static bool done = false;                  // opt in to the whole LDS once per kernel
+    if (!done) {
+        MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds),
                 "bdcm set lds");
+        done = true;
     }
     return MJX_OK;
+}
+
+// items per launch and dynamic LDS: everything in LDS when the table fits,
+// else as many tables as the scratch slab holds (0: unsupported)
+static int64_t plan_launch(const Geo& g, int64_t m, void* scratch, int64_t scratch_bytes, size_t* lds, bool* in_lds) {
+    *in_lds = lds_bytes(g) <= kMaxLds;
+    *lds = *in_lds ? lds_bytes(g) : m_bytes(g);
+    if (!*in_lds && m_bytes(g) > kMaxLds) return 0;
+    if (*in_lds) return m;
+    return scratch ? scratch_bytes / (int64_t)tab_bytes(g) : 0;
 }
 
 }  // namespace bdcm
@@ -356,22 +372,38 @@ extern "C" int64_t mjx_bdcm_lds_bytes(int D, int p, int c) {
     return (int64_t)lds_bytes(g);
 }
 
+extern "C" int64_t mjx_bdcm_scratch_bytes(int D, int p, int c) {
+    Geo g;
+    if (!make_geo(D, p, c, 1, &g)) return -1;
+    if (lds_bytes(g) <= kMaxLds) return 0;
+    if (m_bytes(g) > kMaxLds) return -1;
+    return (int64_t)tab_bytes(g);
+}
+
 extern "C" int mjx_bdcm_update_class(double* chi, const int32_t* rows, const int32_t* inc, int64_t m, int D, int p,
                                      int c, int attr_value, double lmbd, double damp, double eps, double* upd,
-                                     unsigned long long* delta_bits, void* stream) {
+                                     unsigned long long* delta_bits, void* scratch, int64_t scratch_bytes,
+                                     void* stream) {
     if (m < 0 || !chi) return MJX_EINVAL;
     if (m == 0) return MJX_OK;
     if (!rows || !upd || (D > 0 && !inc) || !(damp > 0.0)) return MJX_EINVAL;
     Geo g;
     if (!make_geo(D, p, c, attr_value, &g)) return MJX_ERANGE;
-    const size_t lds = lds_bytes(g);
-    if (lds > kMaxLds || m > (int64_t)INT32_MAX) return MJX_ERANGE;
+    size_t lds;
+    bool in_lds;
+    const int64_t per = plan_launch(g, m, scratch, scratch_bytes, &lds, &in_lds);
+    if (per < 1) return MJX_ERANGE;
     hipStream_t st = as_stream(stream);
-    int rc = set_lds(k_bdcm_edge, lds);
+    int rc = set_lds(k_bdcm_edge);
     if (rc) return rc;
     // exp(-lmbd*(2 x_a[0] - 1)) for x_a[0] = +1 / -1 (nb:191)
-    k_bdcm_edge<<<(unsigned)m, 64, lds, st>>>(chi, rows, inc, g, exp(-lmbd), exp(lmbd), eps, damp, upd);
-    MJX_LAUNCH_CHECK("k_bdcm_edge");
+    for (int64_t e0 = 0; e0 < m; e0 += per) {
+        const int64_t cnt = (m - e0 < per) ? m - e0 : per;
+        if (cnt > (int64_t)INT32_MAX) return MJX_ERANGE;
+        k_bdcm_edge<<<(unsigned)cnt, 64, lds, st>>>(chi, rows, inc, g, exp(-lmbd), exp(lmbd), eps, damp, upd, e0,
+                                                    in_lds ? nullptr : (double*)scratch);
+        MJX_LAUNCH_CHECK("k_bdcm_edge");
+    }
     const int NC = g.X * g.X;
     k_bdcm_commit<<<grid_for(m * NC), 256, 0, st>>>(chi, rows, m, NC, upd, delta_bits);
     MJX_LAUNCH_CHECK("k_bdcm_commit");
@@ -379,19 +411,27 @@ extern "C" int mjx_bdcm_update_class(double* chi, const int32_t* rows, const int
 }
 
 extern "C" int mjx_bdcm_node_z(const double* chi, const int32_t* nodes, const int32_t* inc, int64_t m, int D, int p,
-                               int c, int attr_value, double lmbd, double eps, double* zi, void* stream) {
+                               int c, int attr_value, double lmbd, double eps, double* zi, void* scratch,
+                               int64_t scratch_bytes, void* stream) {
     if (m < 0 || !chi || !zi) return MJX_EINVAL;
     if (m == 0) return MJX_OK;
     if (!nodes || (D > 0 && !inc)) return MJX_EINVAL;
     Geo g;
     if (!make_geo(D, p, c, attr_value, &g)) return MJX_ERANGE;
-    const size_t lds = lds_bytes(g);
-    if (lds > kMaxLds || m > (int64_t)INT32_MAX) return MJX_ERANGE;
+    size_t lds;
+    bool in_lds;
+    const int64_t per = plan_launch(g, m, scratch, scratch_bytes, &lds, &in_lds);
+    if (per < 1) return MJX_ERANGE;
     hipStream_t st = as_stream(stream);
-    int rc = set_lds(k_bdcm_node, lds);
+    int rc = set_lds(k_bdcm_node);
     if (rc) return rc;
-    k_bdcm_node<<<(unsigned)m, 64, lds, st>>>(chi, nodes, inc, g, exp(-lmbd), exp(lmbd), eps, zi);
-    MJX_LAUNCH_CHECK("k_bdcm_node");
+    for (int64_t e0 = 0; e0 < m; e0 += per) {
+        const int64_t cnt = (m - e0 < per) ? m - e0 : per;
+        if (cnt > (int64_t)INT32_MAX) return MJX_ERANGE;
+        k_bdcm_node<<<(unsigned)cnt, 64, lds, st>>>(chi, nodes, inc, g, exp(-lmbd), exp(lmbd), eps, zi, e0,
+                                                    in_lds ? nullptr : (double*)scratch);
+        MJX_LAUNCH_CHECK("k_bdcm_node");
+    }
     return MJX_OK;
 }
 

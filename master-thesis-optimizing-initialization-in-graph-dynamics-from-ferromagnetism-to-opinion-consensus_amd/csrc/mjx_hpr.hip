@@ -21,9 +21,7 @@ extern "C" int mjx_hpr_update(int dtype, const void* chi_in, void* chi_out, cons
 }
 
 template <typename S>
-static int marginals_impl(const void* chi, const int32_t* out_row, int64_t n, int d, int T, double eps, void* zwork,
-                          void* marg, hipStream_t st) {
-    const int64_t E = n * (int64_t)d / 2;
+static int edge_z_impl(const void* chi, int64_t E, int T, double eps, void* zwork, hipStream_t st) {
     S* zp = (S*)zwork;
     S* zm = zp + 2 * E;
     // one grid-stride round of resident waves (a larger grid runs a partly empty second round)
@@ -40,7 +38,17 @@ static int marginals_impl(const void* chi, const int32_t* out_row, int64_t n, in
     }
 #undef MJX_EDGE_Z
     MJX_LAUNCH_CHECK("k_hpr_edge_z");
-    k_hpr_node_marg<S><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(zp, zm, out_row, n, d, (S*)marg);
+    return MJX_OK;
+}
+
+template <typename S>
+static int marginals_impl(const void* chi, const int32_t* out_row, int64_t n, int d, int T, double eps, void* zwork,
+                          void* marg, hipStream_t st) {
+    const int64_t E = n * (int64_t)d / 2;
+    const int rc = edge_z_impl<S>(chi, E, T, eps, zwork, st);
+    if (rc) return rc;
+    const S* zp = (const S*)zwork;
+    k_hpr_node_marg<S><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(zp, zp + 2 * E, out_row, n, d, (S*)marg);
     MJX_LAUNCH_CHECK("k_hpr_node_marg");
     return MJX_OK;
 }
@@ -52,6 +60,15 @@ extern "C" int mjx_hpr_marginals(int dtype, const void* chi, const int32_t* out_
     hipStream_t st = as_stream(stream);
     if (dtype == MJX_F32) return marginals_impl<float>(chi, out_row, n, d, p + c, eps, zwork, marg, st);
     if (dtype == MJX_F64) return marginals_impl<double>(chi, out_row, n, d, p + c, eps, zwork, marg, st);
+    return MJX_EINVAL;
+}
+
+extern "C" int mjx_hpr_edge_z(int dtype, const void* chi, int64_t E, int p, int c, double eps, void* zwork,
+                              void* stream) {
+    if (E < 1 || p < 1 || c < 1 || !chi || !zwork) return MJX_EINVAL;
+    hipStream_t st = as_stream(stream);
+    if (dtype == MJX_F32) return edge_z_impl<float>(chi, E, p + c, eps, zwork, st);
+    if (dtype == MJX_F64) return edge_z_impl<double>(chi, E, p + c, eps, zwork, st);
     return MJX_EINVAL;
 }
 

@@ -98,6 +98,15 @@ class HPRPlan:
         return cls(np.array(list(G.edges), dtype=np.int64), n, d, nbrs)
 
     @property
+    def er_plan(self):
+        """The same graph as a one-class HPRERPlan (the general kernel's form)."""
+        if getattr(self, "_er_plan", None) is None:
+            from .hpr_er import HPRERPlan
+            rp = np.arange(self.n + 1, dtype=np.int64) * self.d
+            self._er_plan = HPRERPlan(self.edges, rp, self.nbrs_host.reshape(-1))
+        return self._er_plan
+
+    @property
     def graph(self):
         """ELL graph for the majority-dynamics check (the reference's N_nodes)."""
         if self._graph is None:
@@ -123,9 +132,16 @@ def HPr_dp(chi_mat, biases_i, plan, p, c, attr_value, lmbd_in, damppar, out=None
     b = _device.to_device(biases_i, dtype=dt)
     out = torch.empty_like(chi) if out is None else out
     wp, wm = _weights(lmbd_in, plan.n)
-    _lib.call("mjx_hpr_update", _code(dt), _device.ptr(chi), _device.ptr(out), _device.ptr(b),
-              _device.ptr(plan.nbr), _device.ptr(plan.in_row), _device.ptr(plan.out_row), plan.n, plan.d,
-              int(p), int(c), int(attr_value), wp, wm, float(damppar), _device.stream_handle())
+    rc = _lib.load().mjx_hpr_update(_code(dt), _device.ptr(chi), _device.ptr(out), _device.ptr(b),
+                                    _device.ptr(plan.nbr), _device.ptr(plan.in_row), _device.ptr(plan.out_row),
+                                    plan.n, plan.d, int(p), int(c), int(attr_value), wp, wm, float(damppar),
+                                    _device.stream_handle())
+    if rc == _lib.MJX_ERANGE:
+        # beyond the register kernels (d > 6, or (d-1)^T count tables above 128
+        # entries): the per-degree-class kernel, one class D = d-1
+        from .hpr_er import HPr_dp_er
+        return HPr_dp_er(chi, b, plan.er_plan, p, c, attr_value, lmbd_in, damppar, out=out)
+    _lib.check(rc, "mjx_hpr_update")
     return out
 
 

@@ -56,6 +56,20 @@ def allowed(xi, y, rho2, p, c):
     return 0
 
 
+def _allowed_vec(xi, Y, rho2, p, c):
+    """allowed() for one trajectory xi, every receiver row of Y (B, T) and every
+    field row of rho2 (Q, T) at once: (B, Q) 0/1 (the same conditions, nb:66-83)."""
+    T = p + c
+    F = rho2[None, :, :] + Y[:, None, :]                      # (B, Q, T) field per time
+    ok = np.ones(F.shape[:2], dtype=bool)
+    for t in range(T - 1):
+        f = F[:, :, t]
+        ok &= (xi[t + 1] == np.sign(f)) | ((f == 0) & (xi[t + 1] == xi[t]))
+    f = F[:, :, T - 1]
+    ok &= (xi[p] == np.sign(f)) | ((f == 0) & (xi[p] == xi[T - 1]))
+    return ok.astype(np.float64)
+
+
 def factor_A(D, p, c, attr_value):
     """A[xi, xj, rho] for D incoming messages (nb:330-336, lambda = 0), 0/1."""
     T = p + c
@@ -66,9 +80,7 @@ def factor_A(D, p, c, attr_value):
     for a in range(X):
         if tr[a][T - 1] != attr_value:                       # attr_fix (nb:103-105)
             continue
-        for b in range(X):
-            for q, rho in enumerate(rhos):
-                A[a, b, q] = allowed(tr[a], tr[b], 2 * rho - D, p, c)
+        A[a] = _allowed_vec(tr[a], tr, 2 * rhos - D, p, c)
     return A
 
 
@@ -79,12 +91,11 @@ def factor_Ai(D, p, c, attr_value):
     tr = 2 * traj01(T) - 1
     rhos = np.array(list(itertools.product(range(D + 1), repeat=T)), dtype=np.int64)
     A = np.zeros((X, rhos.shape[0]))
-    zero = np.zeros(T, dtype=np.int64)
+    zero = np.zeros((1, T), dtype=np.int64)
     for a in range(X):
         if tr[a][T - 1] != attr_value:
             continue
-        for q, rho in enumerate(rhos):
-            A[a, q] = allowed(tr[a], zero, 2 * rho - D, p, c)
+        A[a] = _allowed_vec(tr[a], zero, 2 * rhos - D, p, c)[0]
     return A
 
 

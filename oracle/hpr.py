@@ -13,6 +13,10 @@ Follows (paths relative to the reference repository):
   HPr_dp                     code/HPR_pytorch_RRG.py:183-218
   marginals_comp             code/HPR_pytorch_RRG.py:147-167
   new_biases_i               code/HPR_pytorch_RRG.py:137-145
+  HPr_dp_er, er_classes,     the same update on an Erdos-Renyi graph with the degree taken
+  marginals_comp_csr         per message (the "general (ER)" HPR of code/README.md:1, which
+                             the repository does not ship): pinned by equality with HPr_dp on
+                             d-regular graphs (tests/test_hpr_oracle.py)
 The DP is the reference's: per (edge, x_a), a table over count vectors rho
 (number of +1 among the incoming neighbours at each time) built one neighbour
 at a time, then contracted with A.  Vectorised over edges.
@@ -72,42 +76,27 @@ def A_factor(T, p, c, d, attr_value):
         xi = tr[ia]
         if xi[p + c - 1] != attr_value:                      # attr_fix (:34-36)
             continue
-        for ib in range(X):
-            xj = tr[ib]
-            for q, rho in enumerate(rhos):
-                sig = (2 * rho - d + 1) + xj                  # rho passed as 2*rho-d+1 (:212)
-                ok = True
-                for t in range(p + c - 1):                    # traj_condition (:19-29)
-                    if xi[t + 1] == np.sign(sig[t]):
-                        continue
-                    if sig[t] == 0 and xi[t + 1] == xi[t]:
-                        continue
-                    ok = False
-                    break
-                if ok:                                        # atr_condition (:14-17)
-                    s = sig[p + c - 1]
-                    ok = (xi[p] == np.sign(s)) or (s == 0 and xi[p] == xi[p + c - 1])
-                A[ia, ib, q] = 1.0 if ok else 0.0
+        sig = (2 * rhos - d + 1)[None, :, :] + tr[:, None, :]   # (xb, rho, t): rho passed as 2*rho-d+1 (:212)
+        ok = np.ones(sig.shape[:2], dtype=bool)
+        for t in range(p + c - 1):                           # traj_condition (:19-29)
+            f = sig[:, :, t]
+            ok &= (xi[t + 1] == np.sign(f)) | ((f == 0) & (xi[t + 1] == xi[t]))
+        f = sig[:, :, p + c - 1]                             # atr_condition (:14-17)
+        ok &= (xi[p] == np.sign(f)) | ((f == 0) & (xi[p] == xi[p + c - 1]))
+        A[ia] = ok
     return A
 
 
-def HPr_dp(chi, biases, in_rows, src, n, d, p, c, attr_value, lmbd_in, damppar, rows=None):
-    """One HPR message update (code/HPR_pytorch_RRG.py:183-218), float64.
-
-    chi (2E, 4^T); biases (n, 2) with column 0 = bias of +1; in_rows (2E, d-1)
-    incoming row indices; src (2E,) source node of each row.  ``rows``: compute
-    only these output rows (returns len(rows) rows)."""
+def _chi_new(chi, biases, inr, src, n, d, p, c, attr_value, lmbd_in):
+    """Unnormalised chi_new of the rows whose incoming rows are inr (R, d-1):
+    the DP over count vectors and the contraction with A (:186-212)."""
     T = p + c
     X = 2 ** T
-    chi = np.asarray(chi, dtype=np.float64)
-    biases = np.asarray(biases, dtype=np.float64)
-    rows = np.arange(chi.shape[0]) if rows is None else np.asarray(rows)
-    R = rows.size
+    R = inr.shape[0]
     tr = traj_table(T)
     plus0 = tr[:, 0] == 1
     # M[e, m, xk, xa] = bias_{k}(xk[0]) * chi[k->a][xk*X + xa]
     cm = chi.reshape(-1, X, X)
-    inr = np.asarray(in_rows)[rows]
     M = cm[inr]                                                # (R, d-1, X(xk), X(xa))
     bs = np.where(plus0[None, :], biases[src][:, 0:1], biases[src][:, 1:2])     # (2E, X)
     M = M * bs[inr][..., None]
@@ -116,8 +105,11 @@ def HPr_dp(chi, biases, in_rows, src, n, d, p, c, attr_value, lmbd_in, damppar, 
     pw = d ** np.arange(T - 1, -1, -1)
     x01 = (tr == 1).astype(np.int64)                           # +1 -> 1
     LL = np.zeros((R, X, nb), dtype=np.float64)
-    for ik in range(X):
-        LL[:, :, int(x01[ik] @ pw)] += M[:, 0, ik, :]
+    if d == 1:                                                 # no incoming message: rho = 0
+        LL[:, :, 0] = 1.0
+    else:
+        for ik in range(X):
+            LL[:, :, int(x01[ik] @ pw)] += M[:, 0, ik, :]
     for m in range(1, d - 1):
         L = np.zeros_like(LL)
         for ik in range(X):
@@ -130,8 +122,86 @@ def HPr_dp(chi, biases, in_rows, src, n, d, p, c, attr_value, lmbd_in, damppar, 
     A = A_factor(T, p, c, d, attr_value)
     w = np.exp(-lmbd_in * tr[:, 0] / n)                        # exp(-lmbd*xi[0]/n)
     new = np.einsum("raq,abq->rab", LL, A) * w[None, :, None]
-    new = new.reshape(R, X * X)
+    return new.reshape(R, X * X)
+
+
+def HPr_dp(chi, biases, in_rows, src, n, d, p, c, attr_value, lmbd_in, damppar, rows=None):
+    """One HPR message update (code/HPR_pytorch_RRG.py:183-218), float64.
+
+    chi (2E, 4^T); biases (n, 2) with column 0 = bias of +1; in_rows (2E, d-1)
+    incoming row indices; src (2E,) source node of each row.  ``rows``: compute
+    only these output rows (returns len(rows) rows)."""
+    chi = np.asarray(chi, dtype=np.float64)
+    biases = np.asarray(biases, dtype=np.float64)
+    rows = np.arange(chi.shape[0]) if rows is None else np.asarray(rows)
+    new = _chi_new(chi, biases, np.asarray(in_rows)[rows], src, n, d, p, c, attr_value, lmbd_in)
     return damppar * new / np.sum(new, axis=1, keepdims=True) + (1 - damppar) * chi[rows]
+
+
+# ---- the ER ("general") HPR: the same update with a per-message degree --------
+def er_classes(edges, row_ptr, col):
+    """Messages of an ER graph (no isolated nodes) grouped by D = deg(a) - 1
+    for a -> b: list of (D, rows (m,), inc (m, D) rows of k -> a, k != b), the
+    source node of every row (2E,), and the CSR out-rows (row of i -> col[j]).
+    Row layout of code/HPR_pytorch_RRG.py:277-285."""
+    edges = np.asarray(edges, dtype=np.int64)
+    rp = np.asarray(row_ptr, dtype=np.int64)
+    col = np.asarray(col, dtype=np.int64)
+    E = edges.shape[0]
+    row = {}
+    for r, (u, v) in enumerate(edges.tolist()):
+        row[(u, v)] = r
+        row[(v, u)] = r + E
+    src = np.concatenate([edges[:, 0], edges[:, 1]])
+    dst = np.concatenate([edges[:, 1], edges[:, 0]])
+    deg = np.diff(rp)
+    D_of = deg[src] - 1
+    classes = []
+    for D in sorted(set(D_of.tolist())):
+        rows = np.flatnonzero(D_of == D)
+        inc = np.array([[row[(k, a)] for k in col[rp[a]:rp[a + 1]].tolist() if k != b]
+                        for a, b in zip(src[rows].tolist(), dst[rows].tolist())], dtype=np.int64).reshape(rows.size, D)
+        classes.append((int(D), rows, inc))
+    n = rp.size - 1
+    out_rows = np.array([row[(i, k)] for i in range(n) for k in col[rp[i]:rp[i + 1]].tolist()], dtype=np.int64)
+    return classes, src, out_rows
+
+
+def HPr_dp_er(chi, biases, classes, src, n, p, c, attr_value, lmbd_in, damppar):
+    """HPr_dp on an ER graph: every degree class D with the factor of d-1 = D
+    incoming messages, all from the old chi (Jacobi), float64."""
+    chi = np.asarray(chi, dtype=np.float64)
+    biases = np.asarray(biases, dtype=np.float64)
+    out = np.empty_like(chi)
+    for D, rows, inc in classes:
+        new = _chi_new(chi, biases, inc, src, n, D + 1, p, c, attr_value, lmbd_in)
+        out[rows] = damppar * new / np.sum(new, axis=1, keepdims=True) + (1 - damppar) * chi[rows]
+    return out
+
+
+def marginals_comp_csr(chi, row_ptr, out_rows, p, c, epsilon=1e-15):
+    """marginals_comp (code/HPR_pytorch_RRG.py:147-167) with a per-node degree:
+    products over the CSR out-rows of every node."""
+    T = p + c
+    X = 2 ** T
+    chi = np.asarray(chi, dtype=np.float64)
+    E = chi.shape[0] // 2
+    fw = chi[:E].reshape(E, X, X)
+    bw = chi[E:].reshape(E, X, X).transpose(0, 2, 1)
+    ZZ = fw * bw
+    half = X // 2
+    zp = np.concatenate([ZZ[:, :half, :].sum(axis=(1, 2)), ZZ[:, :, :half].sum(axis=(1, 2))])
+    zm = np.concatenate([ZZ[:, half:, :].sum(axis=(1, 2)), ZZ[:, :, half:].sum(axis=(1, 2))])
+    zp = np.maximum(zp, epsilon)
+    zm = np.maximum(zm, epsilon)
+    s = zp + zm
+    zp, zm = zp / s, zm / s
+    rp = np.asarray(row_ptr, dtype=np.int64)
+    n = rp.size - 1
+    mp = np.array([np.prod(zp[out_rows[rp[i]:rp[i + 1]]]) for i in range(n)])
+    mm = np.array([np.prod(zm[out_rows[rp[i]:rp[i + 1]]]) for i in range(n)])
+    marg = np.stack([mp, mm], axis=1)
+    return marg / (marg[:, 0] + marg[:, 1])[:, None]
 
 
 def marginals_comp(chi, edges_pos, p, c, epsilon=1e-15):

@@ -170,3 +170,26 @@ def test_hpr_run_graph_batches_equal_eager_loop(mjx_mod):
         assert out[mode][0]["num_steps"][0] == out["eager"][0]["num_steps"][0]
         assert np.array_equal(out[mode][0]["conf"], out["eager"][0]["conf"])
         assert torch.equal(out[mode][1], out["eager"][1])
+
+
+@pytest.mark.parametrize("d,p,c", [(5, 2, 2), (6, 1, 3), (7, 1, 1), (8, 2, 1)])
+def test_hpr_any_degree_through_the_class_kernel(mjx_mod, d, p, c):
+    """Degrees and trajectory lengths beyond the register kernels (count
+    tables above 128 entries, d > 6) run through the per-degree-class kernel:
+    sampled rows against the float64 oracle, fp64 1e-12 and fp32 1e-5."""
+    n = 60 if d * (p + c) > 16 else 120
+    edges = mjx_mod.random_regular_edges(d, n, seed=d + 10 * p)
+    plan = mjx_mod.HPRPlan(edges, n, d)
+    rng = np.random.default_rng(d)
+    nc = 4 ** (p + c)
+    chi = rng.random((2 * plan.E, nc))
+    chi /= chi.sum(1, keepdims=True)
+    b = rng.random((n, 2))
+    b /= b.sum(1, keepdims=True)
+    inr, src = orc.incoming_rows(edges, plan.nbrs_host)
+    rows = np.random.default_rng(2).choice(2 * plan.E, 24, replace=False)
+    want = orc.HPr_dp(chi, b, inr, src, n, d, p, c, 1, 25 * n, 0.4, rows=rows)
+    for dtype in (torch.float64, torch.float32):
+        got = mjx_mod.HPr_dp(torch.tensor(chi, dtype=dtype, device="cuda"), torch.tensor(b, dtype=dtype, device="cuda"),
+                             plan, p, c, 1, 25 * n, 0.4)
+        assert rownorm_err(got[torch.from_numpy(rows).cuda()].cpu().numpy(), want) <= TOL[dtype], dtype

@@ -39,3 +39,53 @@ def test_hpr_oracle_matches_reference(name):
         b2, s = hpr.new_biases_i(b, float(z["pie"]), float(z["gamma"]), z[f"it{k}_marg"], k, z[f"it{k}_u"])
         assert np.array_equal(b2, z[f"it{k}_biases"]) and np.array_equal(s, z[f"it{k}_s"])
         chi, b = ref, b2
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_er_hpr_oracle_equals_reference_on_regular_graphs(name):
+    """The ER restatement (per-message degree) on the reference's own d-regular
+    fixtures: the same messages and marginals as the reference's HPr_dp /
+    marginals_comp (the ER variant has no reference implementation; on a
+    d-regular graph it must be HPR itself)."""
+    z = load_golden(name)
+    n, d, p, c = (int(z[k]) for k in ("n", "d", "p", "c"))
+    e = z["edges"]
+    nb = z["N_nodes"].astype(np.int64)
+    rp = np.arange(n + 1, dtype=np.int64) * d
+    classes, src, out_rows = hpr.er_classes(e, rp, nb.reshape(-1))
+    assert [D for D, _, _ in classes] == [d - 1]
+    assert np.array_equal(out_rows.reshape(n, d), z["N_edges_pos"])
+    new = hpr.HPr_dp_er(z["chi0"], z["biases0"], classes, src, n, p, c, int(z["attr_value"]), int(z["lmbd_in"]),
+                        float(z["damppar"]))
+    ref = z["it0_chi"]
+    assert np.max(np.abs(new - ref) / np.max(np.abs(ref), axis=1, keepdims=True)) < 1e-12
+    marg = hpr.marginals_comp_csr(ref, rp, out_rows, p, c)
+    assert np.max(np.abs(marg - z["it0_marg"])) < 1e-12
+
+
+def test_er_hpr_oracle_on_mixed_degrees_is_normalised():
+    """Leaves (D = 0) and several degree classes: rows stay normalised and the
+    damping keeps the invalid x_a[T-1] blocks at (1 - damp) * old."""
+    rng = np.random.default_rng(0)
+    # a small graph: a path 0-1-2 plus a triangle 2-3-4 and a pendant 4-5
+    e = np.array([[0, 1], [1, 2], [2, 3], [3, 4], [2, 4], [4, 5]])
+    n = 6
+    src = np.concatenate([e[:, 0], e[:, 1]])
+    dst = np.concatenate([e[:, 1], e[:, 0]])
+    order = np.lexsort((dst, src))
+    rp = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(np.bincount(src, minlength=n), out=rp[1:])
+    classes, srcs, out_rows = hpr.er_classes(e, rp, dst[order])
+    assert sorted(D for D, _, _ in classes) == [0, 1, 2]
+    p, c = 1, 2
+    nc = 4 ** (p + c)
+    chi = rng.random((2 * len(e), nc))
+    chi /= chi.sum(1, keepdims=True)
+    b = rng.random((n, 2))
+    b /= b.sum(1, keepdims=True)
+    new = hpr.HPr_dp_er(chi, b, classes, srcs, n, p, c, 1, 25 * n, 0.4)
+    assert np.allclose(new.sum(1), 1.0)
+    X = 2 ** (p + c)
+    inval = [xa for xa in range(X) if hpr.traj_table(p + c)[xa][-1] != 1]
+    blk = np.concatenate([np.arange(xa * X, xa * X + X) for xa in inval])
+    assert np.allclose(new[:, blk], 0.6 * chi[:, blk])
