@@ -19,7 +19,12 @@ Secondary line items in the same JSON object:
     (oracle/majority.py, same numpy ops as code/SA_RRG.py:18-20) on the same
     graph, one process per core, bounded sample, rank 0 at N=1 only,
   * sa: SA proposals/s and sweeps/s on configs[1] (d=3, N=1e6, p=2, c=1,
-    4096 replicas, full rollout per proposal).
+    4096 replicas; light-cone and full-rollout modes), timed after a warm-in
+    of --sa-warmin proposals per replica,
+  * sa_c1: configs[0] literally (SA_RRG.py's case: d=4, N=1e4, p=c=1, 64
+    replicas) beside the numpy restatement of the reference's SA loop,
+  * hpr / bdcm / er / giant legs, the HPR
+    leg with the torch-CPU restatement on all host cores beside it.
 """
 import argparse
 import json
@@ -50,6 +55,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sa-steps", type=int, default=2000)
     ap.add_argument("--sa-rollout-steps", type=int, default=10)
+    ap.add_argument("--sa-warmin", type=int, default=10000,
+                    help="proposals every SA replica makes before the timed region (steady state, not t=0)")
+    ap.add_argument("--c1-steps", type=int, default=10000)
     ap.add_argument("--no-sa", action="store_true")
     ap.add_argument("--giant-n", type=int, default=1_000_000_000)
     ap.add_argument("--giant-d", type=int, default=6)
@@ -156,6 +164,7 @@ def bench_sa(args, rank, world, dist, dev):
         sa.steps(2)
         torch.cuda.synchronize()
         t_init = time.perf_counter() - t_init
+        sa.steps(args.sa_warmin)                      # steady state: past the all-accept start
         el = _timed(lambda: sa.steps(steps), dist, dev)
         props = world * sa_R * steps / el
         out[mode] = {
@@ -164,10 +173,44 @@ def bench_sa(args, rank, world, dist, dev):
             "ms_per_step": 1e3 * el / steps,
             "reference_equivalent_node_updates_per_s": props * 3 * (sa_p + sa_c - 1) * sa_n,
             "init_s": t_init,
+            "warmin_proposals_per_replica": args.sa_warmin,
             "steps": steps,
         }
         del sa
     return out
+
+
+def bench_sa_c1(args, rank, world, dist, dev):
+    """configs[0] literally: SA_RRG.py's own case, d=4 RRG, N=1e4, p=c=1,
+    64 replicas (numpy seeds), light-cone SA on the GPU after a warm-in, timed
+    beside the numpy restatement of the reference's SA step (oracle/majority.py
+    sa_loop: three full rollouts per proposal, code/SA_RRG.py:63-88) on one
+    host core, on the same graph and seed."""
+    import torch
+    import mjx
+    n, d, p, c, R = 10_000, 4, 1, 1, 64
+    adj = mjx.random_regular_graph(d, n, seed=args.seed + 1000 + rank)
+    seeds = list(range(rank * R, (rank + 1) * R))
+    sa = mjx.SAReplicas(adj, p, c, seeds)
+    sa.steps(args.sa_warmin)
+    K = args.c1_steps
+    el = _timed(lambda: sa.steps(K), dist, dev)
+    props = world * R * K / el
+    res = {"config": "configs[0]: SA_RRG.py case, d=4 RRG N=1e4, p=c=1, 64 replicas per GPU (numpy seeds), "
+                     f"{K} proposals per replica after {args.sa_warmin} warm-in proposals",
+           "mode": sa.mode, "proposals_per_s": props, "sweeps_per_s": props / n, "ms_per_step": 1e3 * el / K}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import majority as orc
+        t0 = time.perf_counter()
+        o = orc.sa_loop(adj, p, c, seeds[0], max_steps=2000)
+        cpu_s = time.perf_counter() - t0
+        res["cpu_baseline"] = {"proposals_per_s": o["num_steps"] / cpu_s, "cores": 1, "kind": "port",
+                               "sample": f"oracle/majority.py sa_loop (numpy, code/SA_RRG.py:63-88, three rollouts "
+                                         f"per proposal) on the same graph, seed {seeds[0]}, {o['num_steps']} "
+                                         f"proposals in {cpu_s:.1f} s, one core (the reference runs its replicas "
+                                         f"one after another on one core)"}
+        res["speedup_vs_cpu"] = props / res["cpu_baseline"]["proposals_per_s"]
+    return res
 
 
 def bench_er(args, rank, world, dist, dev):
@@ -322,22 +365,35 @@ def bench_hpr(args, rank, world, dist, dev):
            "marginals_algorithmic_GBps": marg_bytes / (marg_ms / 1e3) / 1e9,
            "marginals_bytes_per_iter": marg_bytes}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # the reference runs HPr_dp as torch ops; on the host that is torch's CPU
+        # backend with every core: oracle/hpr_torch.py, the same DP in torch ops
         from oracle import hpr as ohpr
+        from oracle import hpr_torch
         inr, src = ohpr.incoming_rows(plan.edges, plan.nbrs_host)
-        chi_h = chi.double().cpu().numpy()
-        b_h = b.double().cpu().numpy()
-        rows = np.random.default_rng(0).choice(msgs, size=256, replace=False)
+        chi_h = chi.double().cpu()
+        b_h = b.double().cpu()
+        rows = np.random.default_rng(0).choice(msgs, size=2048, replace=False)
+        try:
+            avail = len(os.sched_getaffinity(0))
+        except AttributeError:
+            avail = os.cpu_count() or 1
+        cores = max(1, min(16, avail))
+        old_threads = torch.get_num_threads()
+        torch.set_num_threads(cores)
+        hpr_torch.HPr_dp(chi_h, b_h, inr, src, n, d, p, c, 1, lmbd, 0.4, rows[:64])      # warm-up
         t0 = time.perf_counter()
         done = 0
-        while time.perf_counter() - t0 < 4.0:
-            ohpr.HPr_dp(chi_h, b_h, inr, src, n, d, p, c, 1, lmbd, 0.4, rows=rows)
+        while time.perf_counter() - t0 < 5.0:
+            hpr_torch.HPr_dp(chi_h, b_h, inr, src, n, d, p, c, 1, lmbd, 0.4, rows)
             done += rows.size
         cpu_s = time.perf_counter() - t0
-        res["cpu_baseline"] = {"messages_per_s": done / cpu_s, "cores": 1, "kind": "port",
-                               "sample": f"oracle/hpr.py HPr_dp (numpy float64, code/HPR_pytorch_RRG.py:183-218) "
-                                         f"on {rows.size} sampled output rows of the same graph, repeated "
-                                         f"for {cpu_s:.1f} s",
+        torch.set_num_threads(old_threads)
+        res["cpu_baseline"] = {"messages_per_s": done / cpu_s, "cores": cores, "kind": "port",
+                               "sample": f"oracle/hpr_torch.py HPr_dp (torch CPU ops, float64, "
+                                         f"code/HPR_pytorch_RRG.py:183-218) on {rows.size} sampled output rows of "
+                                         f"the same graph, repeated for {cpu_s:.1f} s, torch threads = {cores}",
                                "ms_per_iter_equiv": 1e3 * msgs / (done / cpu_s)}
+        res["speedup_vs_cpu"] = res["messages_per_s"] / res["cpu_baseline"]["messages_per_s"]
     return res
 
 
@@ -476,6 +532,9 @@ def main():
     sa_res = None
     if not args.no_sa and args.sa_steps > 0:
         sa_res = bench_sa(args, rank, world, dist, dev)
+    c1 = None
+    if not args.no_sa and args.c1_steps > 0:
+        c1 = bench_sa_c1(args, rank, world, dist, dev)
 
     del s0, out, tmp, counts, chk, o2
     torch.cuda.empty_cache()
@@ -527,6 +586,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "sa": sa_res,
+            "sa_c1": c1,
             "er": er,
             "hpr": hpr,
             "bdcm": bdcm,

@@ -108,10 +108,34 @@ def popcount(bits, n, words=None, counts=None):
 # ---------------------------------------------------------------------------
 # reference-shaped layer
 # ---------------------------------------------------------------------------
+_GRAPHS = {}        # id(array) -> (weakref to it, strided sample of it, device Graph)
+
+
 def as_graph(N):
+    """Device graph of a neighbour array.  A numpy ``N`` (the reference's
+    (n, d) array, code/SA_RRG.py:9-16) is uploaded once and the device copy
+    reused while the same array object is passed again (SA_RRG.py calls the
+    dynamics three times per proposal with one N); a strided sample of the
+    entries is re-checked on every call, so a replaced array is re-uploaded.
+    The reference never modifies N in place; a caller that does should pass a
+    new array (or a ``Graph``)."""
     if isinstance(N, Graph):
         return N
-    return Graph.ell(N)
+    if not isinstance(N, np.ndarray) or N.ndim != 2:
+        return Graph.ell(N)
+    import weakref
+    step = max(1, N.size // 1024)
+    sample = N.reshape(-1)[::step].copy()
+    hit = _GRAPHS.get(id(N))
+    if hit is not None and hit[0]() is N and hit[1].shape == sample.shape and np.array_equal(hit[1], sample):
+        return hit[2]
+    g = Graph.ell(N)
+    try:
+        ref = weakref.ref(N, lambda _, k=id(N): _GRAPHS.pop(k, None))
+    except TypeError:
+        return g
+    _GRAPHS[id(N)] = (ref, sample, g)
+    return g
 
 
 def _return_like(x, like):

@@ -214,3 +214,20 @@ def test_full_size_properties_d4(mjx_mod):
     # oracle on a sample replica (numpy, ~1 s)
     want = orc.s_endstate(adj, S[5].cpu().numpy(), 2, 1)
     assert np.array_equal(outS[5].cpu().numpy(), want)
+
+
+def test_numpy_neighbour_array_uploaded_once(mjx_mod):
+    """The drop-in onestep_majority(N, s) with the reference's numpy N reuses
+    the device adjacency across calls on the same array; a different array
+    (or new contents) is uploaded again and still gives the oracle's result."""
+    from oracle import majority as orc
+    N = mjx_mod.random_regular_graph(4, 1000, seed=3).astype(np.int64)
+    g1 = mjx_mod.as_graph(N)
+    assert mjx_mod.as_graph(N) is g1
+    s = 2 * np.random.default_rng(0).integers(0, 2, 1000).astype(np.int64) - 1
+    for _ in range(3):
+        assert np.array_equal(mjx_mod.onestep_majority(N, s), orc.onestep_majority(N, s))
+    assert mjx_mod.as_graph(N) is g1
+    N2 = mjx_mod.random_regular_graph(4, 1000, seed=4).astype(np.int64)
+    assert mjx_mod.as_graph(N2) is not g1
+    assert np.array_equal(mjx_mod.s_endstate(N2, s, 2, 1), orc.s_endstate(N2, s, 2, 1))

@@ -89,3 +89,18 @@ def test_er_hpr_oracle_on_mixed_degrees_is_normalised():
     inval = [xa for xa in range(X) if hpr.traj_table(p + c)[xa][-1] != 1]
     blk = np.concatenate([np.arange(xa * X, xa * X + X) for xa in inval])
     assert np.allclose(new[:, blk], 0.6 * chi[:, blk])
+
+
+def test_torch_cpu_restatement_equals_numpy_oracle():
+    """bench.py's CPU baseline (oracle/hpr_torch.py) computes the same rows as
+    the pinned numpy oracle."""
+    import torch
+    from oracle import hpr_torch
+    z = load_golden("hpr_d4_n64_p2c2.npz")
+    n, d, p, c = (int(z[k]) for k in ("n", "d", "p", "c"))
+    inr, src = hpr.incoming_rows(z["edges"], z["N_nodes"])
+    rows = np.array([0, 5, 77, 2 * z["edges"].shape[0] - 1])
+    want = hpr.HPr_dp(z["chi0"], z["biases0"], inr, src, n, d, p, c, 1, 25 * n, 0.4, rows=rows)
+    got = hpr_torch.HPr_dp(torch.from_numpy(z["chi0"]), torch.from_numpy(z["biases0"]), inr, src, n, d, p, c, 1,
+                           25 * n, 0.4, rows)
+    assert np.max(np.abs(got.numpy() - want)) < 1e-13
