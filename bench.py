@@ -363,7 +363,9 @@ def bench_hpr(args, rank, world, dist, dev):
            "hpr_dp_frac_of_hbm_peak": bytes_per_iter / (upd_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
            "hpr_dp_bytes_per_iter": bytes_per_iter,
            "marginals_algorithmic_GBps": marg_bytes / (marg_ms / 1e3) / 1e9,
-           "marginals_bytes_per_iter": marg_bytes}
+           "marginals_bytes_per_iter": marg_bytes,
+           "hpr_dp_traffic_bytes": rocprof_traffic("k_hpr_update_pipe"),
+           "marginals_edge_z_traffic_bytes": rocprof_traffic("k_hpr_edge_z")}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # the reference runs HPr_dp as torch ops; on the host that is torch's CPU
         # backend with every core: oracle/hpr_torch.py, the same DP in torch ops
@@ -442,7 +444,8 @@ def bench_giant(args, rank, world, dist, dev):
 
 def rocprof_traffic(kernel_prefix="k_sweep_ell_rp"):
     """HBM bytes per launch from a committed rocprofv3 PMC summary, if any
-    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py)."""
+    (profiles/pmc_traffic.json, written by tools/pmc_parse.py from
+    rocprofv3 --pmc passes over tools/pmc_run.py)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:

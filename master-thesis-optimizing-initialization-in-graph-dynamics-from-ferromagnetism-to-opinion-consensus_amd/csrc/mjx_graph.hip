@@ -311,11 +311,13 @@ extern "C" int mjx_graph_check_ell(const int32_t* adj, int64_t n, int d, unsigne
 //   phase 1 (k_bin_msg, workgroups per source block): stage the block's state
 //     bits in LDS, stream the block's source offsets (phase-1 order: b-major,
 //     t inside) and write one message bit per slot;
-//   phase 2 (k_bin_apply, one workgroup per destination tile): for every
-//     segment (b, t) stream its 16-bit destination offsets (phase-2 order:
-//     t-major) and its message bits, count +1 neighbours in LDS, then apply the
-//     majority rule with always-stay ties (code/SA_RRG.py:19-20) against the
-//     node's own bit.
+//   phase 2 (k_bin_apply_flat, one workgroup per destination tile): stream the
+//     tile's 16-bit destination offsets (phase-2 order: t-major, b inside) and
+//     the segments' message bytes, count +1 neighbours in LDS (byte counters),
+//     then apply the majority rule with always-stay ties (code/SA_RRG.py:19-20)
+//     against the node's own bit.
+// Segments start on 8-slot boundaries in BOTH orders, so the eight message bits
+// of an aligned 8-slot piece of a segment are one byte of msg.
 // Slot i of segment (b, t) is slot i in both orders, so the phases agree
 // without a per-slot index.  Algorithmic traffic per slot: 2.5 B of source
 // offset (20 bits: a 16-bit low part and a 4-bit high part) + 2 B of
@@ -323,7 +325,8 @@ extern "C" int mjx_graph_check_ell(const int32_t* adj, int64_t n, int d, unsigne
 // instead of one random line per slot.
 //
 // Plan (sizes from mjx_binned_plan_shape):
-//   src_lo uint16[src_len]   phase-1 order; block starts padded to 256 slots
+//   src_lo uint16[src_len]   phase-1 order; segment starts padded to 8 slots,
+//                            block starts to 256 slots
 //                            and every 256-slot chunk stored lane-transposed
 //                            (slot r of chunk c at 256c + 4*(r&63) + (r>>6)), so
 //                            one 8-B load per lane gives a wave the low parts of
@@ -363,7 +366,7 @@ inline Shape shape(int64_t n, int d, int64_t rows) {
     s.T = (rows + kTile - 1) >> kTileShift;
     s.S = s.K * s.T;
     s.slots = rows * d;
-    s.src_len = ((s.slots + 255) & ~255ll) + 256 * s.K;
+    s.src_len = align256(s.slots + 7 * s.S) + 256 * s.K;     // segments padded to 8 slots, blocks to 256
     s.off_len = s.slots + 8 * s.S + 8;
     s.index_len = (s.K + 1) + s.S + (s.S + 1);
     s.msg_words = s.src_len / 64 + 2;
@@ -415,7 +418,7 @@ __global__ void __launch_bounds__(256) k_bin_blockscan(const uint32_t* __restric
     long long carry = 0;
     for (int64_t t0 = 0; t0 < T; t0 += 256) {
         const int64_t t = t0 + threadIdx.x;
-        const long long x = (t < T) ? (long long)cntB[b * T + t] : 0;
+        const long long x = (t < T) ? (long long)((cntB[b * T + t] + 7u) & ~7u) : 0;   // 8-slot aligned segments
         sh[threadIdx.x] = x;
         __syncthreads();
         for (int o = 1; o < 256; o <<= 1) {
@@ -491,7 +494,11 @@ __device__ __forceinline__ int4 unpack_src(uint2 l, unsigned h) {
 }
 
 // phase 1: message bit of every slot of block b, in phase-1 order; `split`
-// workgroups share a block (each stages the block's 128 KB of state bits)
+// workgroups share a block (each stages the block's 128 KB of state bits).
+// UC chunks per wave step, loaded unconditionally (a step's last chunks are
+// clamped to the wave's last one and not stored) so that every load of a step
+// is in flight before the first ballot.
+template <int UC>
 __global__ void __launch_bounds__(kMsgThreads) k_bin_msg(const uint16_t* __restrict__ src_lo,
                                                          const uint16_t* __restrict__ src_hi,
                                                          const long long* __restrict__ blk, int64_t n, int split,
@@ -500,9 +507,24 @@ __global__ void __launch_bounds__(kMsgThreads) k_bin_msg(const uint16_t* __restr
     const int64_t b = blockIdx.x / split;
     const int part = blockIdx.x % split;
     const int64_t g0 = b * kSrcWords, nw32 = (n + 31) >> 5;
-    for (int i = threadIdx.x; i < kSrcWords; i += kMsgThreads) {
-        const int64_t g = g0 + i;
-        sb[i] = (g < nw32) ? s32[g] : 0u;
+    // stage the block's state bits: every thread's eight 16-B loads in flight at once
+    {
+        constexpr int V = kSrcWords / 4 / kMsgThreads;
+        uint4 x[V];
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+            const int64_t g = g0 + 4 * (threadIdx.x + (int64_t)k * kMsgThreads);
+            if (g + 3 < nw32) {
+                x[k] = *reinterpret_cast<const uint4*>(s32 + g);
+            } else {
+                x[k].x = (g < nw32) ? s32[g] : 0u;
+                x[k].y = (g + 1 < nw32) ? s32[g + 1] : 0u;
+                x[k].z = (g + 2 < nw32) ? s32[g + 2] : 0u;
+                x[k].w = 0u;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < V; ++k) reinterpret_cast<uint4*>(sb)[threadIdx.x + k * kMsgThreads] = x[k];
     }
     __syncthreads();
     const int64_t c0 = blk[b] >> 8, c1 = blk[b + 1] >> 8;   // 256-slot chunks of this block
@@ -512,21 +534,18 @@ __global__ void __launch_bounds__(kMsgThreads) k_bin_msg(const uint16_t* __restr
     constexpr int NW = kMsgThreads / 64;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint2* lo2 = reinterpret_cast<const uint2*>(src_lo);
-    // UC chunks per step: lane 4u+k stores message word k of chunk u
-    constexpr int UC = 4;
+    // this wave's chunks: a0 + wave + NW*i; lane 4u+k stores message word k of chunk u
+    const int64_t last = (a1 - 1 - a0 - wave >= 0) ? a0 + wave + ((a1 - 1 - a0 - wave) / NW) * NW : -1;
     for (int64_t c = a0 + wave; c < a1; c += UC * NW) {
         uint2 l[UC];
         unsigned h[UC];
 #pragma unroll
         for (int u = 0; u < UC; ++u) {
-            const int64_t cc = c + u * NW;
-            l[u] = make_uint2(0, 0);
-            h[u] = 0;
-            if (cc < a1) {
-                l[u] = lo2[cc * 64 + lane];
-                h[u] = src_hi[cc * 64 + lane];
-            }
+            const int64_t cc = (c + u * NW <= last) ? c + u * NW : last;
+            l[u] = lo2[cc * 64 + lane];
+            h[u] = src_hi[cc * 64 + lane];
         }
+        __builtin_amdgcn_sched_barrier(0);      // every load issued before the first use
         u64 mine = 0;
 #pragma unroll
         for (int u = 0; u < UC; ++u) {
@@ -602,6 +621,48 @@ __device__ __forceinline__ int64_t xcd_tile(int64_t bid, int64_t T) {
     return x * q + (x < r ? x : r) + i;
 }
 
+// the majority rule over a tile's counts: wave w takes the tile's 64-node
+// words [64w, 64w + 64); lane i loads the own bits of word i once, and lane k
+// keeps word k's result, so the state is read and written in coalesced 512-B runs
+__device__ __forceinline__ void tile_rule(const uint32_t* cnt, int64_t t, int64_t lo, int64_t hi, int d,
+                                          const uint32_t* __restrict__ s32, u64* __restrict__ s_out,
+                                          unsigned long long* __restrict__ counts, unsigned long long* red,
+                                          int nw) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t v0 = lo + t * kTile;                       // lo is 64-aligned: whole words
+    const int64_t v1 = (v0 + kTile < hi) ? v0 + kTile : hi;
+    const int64_t w0 = (v0 >> 6) + (int64_t)wave * 64, wend = (v1 + 63) >> 6;
+    const int64_t wl = w0 + lane;
+    const u64 own = (wl < wend) ? reinterpret_cast<const u64*>(s32)[wl] : 0ull;
+    u64 mine = 0;
+    unsigned long long ones = 0;
+    const int nk = (wend - w0 <= 0) ? 0 : (wend - w0 < 64 ? (int)(wend - w0) : 64);
+    for (int k = 0; k < nk; ++k) {
+        const u64 ow = (u64)readlane64((long long)own, k);
+        const int64_t v = ((w0 + k) << 6) + lane;
+        bool nb = false;
+        if (v < v1) {
+            const int64_t lv = v - v0;
+            const int c = (int)((cnt[lv >> 2] >> ((lv & 3) << 3)) & 0xffu);
+            const int o = (int)((ow >> lane) & 1ull);
+            nb = (2 * c > d) || ((2 * c == d) && o);         // always-stay ties (code/SA_RRG.py:19-20)
+        }
+        const u64 word = __ballot(nb);
+        if (lane == k) mine = word;
+        ones += __popcll(word);
+    }
+    if (wl < wend) s_out[wl] = mine;
+    if (counts) {
+        if (lane == 0) red[wave] = ones;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long tot = 0;
+            for (int i = 0; i < nw; ++i) tot += red[i];
+            if (tot) atomicAdd(counts, tot);
+        }
+    }
+}
+
 // phase 2: one workgroup per destination tile; U segments per step
 template <int U>
 __global__ void __launch_bounds__(kApplyThreads) k_bin_apply(const uint16_t* __restrict__ off,
@@ -660,33 +721,7 @@ __global__ void __launch_bounds__(kApplyThreads) k_bin_apply(const uint16_t* __r
         }
     }
     __syncthreads();
-    const int64_t v0 = lo + t * kTile;
-    const int64_t v1 = (v0 + kTile < hi) ? v0 + kTile : hi;
-    unsigned long long ones = 0;
-    for (int64_t w = (v0 >> 6) + wave; w < ((v1 + 63) >> 6); w += NW) {
-        const int64_t v = (w << 6) + lane;
-        bool nb = false;
-        if (v < v1) {
-            const int64_t lv = v - v0;
-            const int c = (int)((cnt[lv >> 2] >> ((lv & 3) << 3)) & 0xffu);
-            const int own = (s32[v >> 5] >> (v & 31)) & 1u;
-            nb = (2 * c > d) || ((2 * c == d) && own);
-        }
-        const u64 word = __ballot(nb);
-        if (lane == 0) {
-            s_out[w] = word;
-            ones += __popcll(word);
-        }
-    }
-    if (counts) {
-        if (lane == 0) red[wave] = ones;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned long long tot = 0;
-            for (int i = 0; i < NW; ++i) tot += red[i];
-            if (tot) atomicAdd(counts, tot);
-        }
-    }
+    tile_rule(cnt, t, lo, hi, d, s32, s_out, counts, red, NW);
 }
 
 // phase 2, flat form (K <= kFlatMaxK): the tile's segment starts (relative,
@@ -696,41 +731,69 @@ __global__ void __launch_bounds__(kApplyThreads) k_bin_apply(const uint16_t* __r
 // piece's segment with a forward cursor in LDS; four chunks per step.
 constexpr int kFlatMaxK = 960;      // 64 KB of counters + 12 B per segment stay within half of the CU's LDS
 
-__device__ __forceinline__ void tile_rule(const uint32_t* cnt, int64_t t, int64_t lo, int64_t hi, int d,
-                                          const uint32_t* __restrict__ s32, u64* __restrict__ s_out,
-                                          unsigned long long* __restrict__ counts, unsigned long long* red,
-                                          int nw) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t v0 = lo + t * kTile;
-    const int64_t v1 = (v0 + kTile < hi) ? v0 + kTile : hi;
-    unsigned long long ones = 0;
-    for (int64_t w = (v0 >> 6) + wave; w < ((v1 + 63) >> 6); w += nw) {
-        const int64_t v = (w << 6) + lane;
-        bool nb = false;
-        if (v < v1) {
-            const int64_t lv = v - v0;
-            const int c = (int)((cnt[lv >> 2] >> ((lv & 3) << 3)) & 0xffu);
-            const int own = (s32[v >> 5] >> (v & 31)) & 1u;
-            nb = (2 * c > d) || ((2 * c == d) && own);       // always-stay ties (code/SA_RRG.py:19-20)
-        }
-        const u64 word = __ballot(nb);
-        if (lane == 0) {
-            s_out[w] = word;
-            ones += __popcll(word);
-        }
+// one group of UC 8-slot pieces of a wave's stretch: 16-bit destination
+// offsets, the pieces' message bytes and their valid-slot masks
+template <int UC>
+struct Group {
+    uint4 o[UC];
+    unsigned m[UC];
+    unsigned lim[UC];
+};
+
+template <int UC>
+__device__ __forceinline__ void fetch_group(Group<UC>& g, int32_t c, int32_t a1, int lane, int32_t& b,
+                                            const int32_t* srel, const long long* spos, const uint16_t* offt,
+                                            const uint8_t* __restrict__ msg8) {
+    // positions first (LDS cursor), then every load of the group unconditionally:
+    // pieces past the stretch read its last piece and get an empty mask
+    const uint16_t* po[UC];
+    const uint8_t* pm[UC];
+#pragma unroll
+    for (int u = 0; u < UC; ++u) {
+        const int32_t j0 = c + u * 512 + 8 * lane;
+        const bool valid = j0 < a1;
+        const int32_t j = valid ? j0 : a1 - 8;
+        while ((srel[b + 1] & ~7) <= j) ++b;               // forward cursor (start[K] = Lt > j)
+        const int32_t sb = srel[b];
+        const int32_t st0 = sb & ~7;
+        const int32_t len = (srel[b + 1] & ~7) - st0 - (sb & 7);
+        const int32_t rel = j - st0;
+        po[u] = offt + j;
+        // segments start on 8-slot boundaries in both orders: the piece's
+        // eight message bits are one byte
+        pm[u] = msg8 + ((spos[b] + rel) >> 3);
+        const int32_t nb = len - rel;
+        g.lim[u] = !valid ? 0u : ((nb >= 8) ? 0xffu : (nb > 0 ? ((1u << nb) - 1) : 0u));
     }
-    if (counts) {
-        if (lane == 0) red[wave] = ones;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned long long tot = 0;
-            for (int i = 0; i < nw; ++i) tot += red[i];
-            if (tot) atomicAdd(counts, tot);
+#pragma unroll
+    for (int u = 0; u < UC; ++u) {
+        g.o[u] = *reinterpret_cast<const uint4*>(po[u]);
+        g.m[u] = *pm[u];
+    }
+}
+
+template <int UC>
+__device__ __forceinline__ void apply_group(uint32_t* cnt, const Group<UC>& g) {
+#pragma unroll
+    for (int u = 0; u < UC; ++u) {
+        const unsigned bits = g.m[u] & g.lim[u];
+        const unsigned oo[4] = {g.o[u].x, g.o[u].y, g.o[u].z, g.o[u].w};
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            // only +1 messages touch the LDS (adding zeros for every lane costs
+            // ~2 ms per sweep at N=1e9: the LDS atomic rate is per active lane)
+            if ((bits >> q) & 1u) {
+                const unsigned v = (oo[q >> 1] >> ((q & 1) * 16)) & 0xffffu;
+                atomicAdd(&cnt[v >> 2], 1u << ((v & 3) << 3));
+            }
         }
     }
 }
 
-__global__ void __launch_bounds__(kApplyThreads) k_bin_apply_flat(const uint16_t* __restrict__ off,
+// UC = 2 pieces per group, two groups in flight: <= 64 VGPRs keeps two
+// workgroups (8 waves per SIMD) on a CU; deeper groups (UC = 3, 4) measured slower
+template <int UC>
+__global__ void __launch_bounds__(kApplyThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) k_bin_apply_flat(const uint16_t* __restrict__ off,
                                                                   const long long* __restrict__ p1T,
                                                                   const long long* __restrict__ p2,
                                                                   const u64* __restrict__ msg, int64_t K, int64_t lo,
@@ -739,7 +802,6 @@ __global__ void __launch_bounds__(kApplyThreads) k_bin_apply_flat(const uint16_t
                                                                   unsigned long long* __restrict__ counts) {
     extern __shared__ uint32_t cnt[];
     constexpr int NW = kApplyThreads / 64;
-    constexpr int UC = 4;
     __shared__ unsigned long long red[NW];
     __shared__ int32_t srel[kFlatMaxK + 1];          // segment start - tile start | pad count
     __shared__ long long spos[kFlatMaxK];            // phase-1 position of the segment
@@ -773,39 +835,17 @@ __global__ void __launch_bounds__(kApplyThreads) k_bin_apply_flat(const uint16_t
         b = lo_b;
     }
     const uint16_t* offt = off + P0;
-    for (int32_t c = a0; c < a1; c += UC * 512) {
-        uint4 o[UC];
-        u64 m0[UC], m1[UC];
-        int sh[UC];
-        unsigned lim[UC];
-#pragma unroll
-        for (int u = 0; u < UC; ++u) {
-            const int32_t j = c + u * 512 + 8 * lane;
-            lim[u] = 0;
-            if (j < a1) {
-                while ((srel[b + 1] & ~7) <= j) ++b;           // forward cursor (start[K] = Lt > j)
-                const int32_t sb = srel[b];
-                const int32_t st0 = sb & ~7;
-                const int32_t len = (srel[b + 1] & ~7) - st0 - (sb & 7);
-                const int32_t rel = j - st0;
-                const long long pos = spos[b] + rel;
-                o[u] = *reinterpret_cast<const uint4*>(offt + j);
-                m0[u] = msg[pos >> 6];
-                m1[u] = msg[(pos >> 6) + 1];
-                sh[u] = (int)(pos & 63);
-                const int32_t nb = len - rel;
-                lim[u] = (nb >= 8) ? 0xffu : (nb > 0 ? ((1u << nb) - 1) : 0u);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < UC; ++u) {
-            if (lim[u]) {
-                Piece pc;
-                pc.o = o[u];
-                const u64 w = sh[u] ? ((m0[u] >> sh[u]) | (m1[u] << (64 - sh[u]))) : m0[u];
-                pc.bits = (unsigned)w & lim[u];
-                apply_piece(cnt, pc);
-            }
+    const uint8_t* msg8 = reinterpret_cast<const uint8_t*>(msg);
+    // two groups in flight: the loads of group i+1 are issued before the LDS
+    // counts of group i
+    if (a0 < a1) {
+        Group<UC> ga, gb;
+        fetch_group<UC>(ga, a0, a1, lane, b, srel, spos, offt, msg8);
+        for (int32_t c = a0; c < a1; c += 2 * UC * 512) {
+            fetch_group<UC>(gb, c + UC * 512, a1, lane, b, srel, spos, offt, msg8);
+            apply_group<UC>(cnt, ga);
+            fetch_group<UC>(ga, c + 2 * UC * 512, a1, lane, b, srel, spos, offt, msg8);
+            apply_group<UC>(cnt, gb);
         }
     }
     __syncthreads();
@@ -897,28 +937,26 @@ extern "C" int mjx_sweep_binned(const uint16_t* src_lo, const uint16_t* src_hi, 
     const long long* p1T = index + (s.K + 1);
     const long long* p2 = p1T + s.S;
     hipStream_t st = mjx::as_stream(stream);
-    MJX_HIP(hipFuncSetAttribute((const void*)k_bin_msg, hipFuncAttributeMaxDynamicSharedMemorySize,
+    MJX_HIP(hipFuncSetAttribute((const void*)k_bin_msg<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 kSrcWords * (int)sizeof(uint32_t)), "k_bin_msg lds");
     // a rank with all rows: 4 workgroups per source block (~4 per CU); with
     // fewer rows fewer, so that staging the block stays a small share
+    // (2, 4 and 8 measured within 5 % of each other at N=1e9, d=6)
     const int64_t rows = row_hi - row_lo;
     int split = (int)((kMsgSplitMax * rows + n - 1) / n);
     split = split < 1 ? 1 : (split > kMsgSplitMax ? kMsgSplitMax : split);
-    k_bin_msg<<<(unsigned)(s.K * split), kMsgThreads, kSrcWords * sizeof(uint32_t), st>>>(
+    k_bin_msg<4><<<(unsigned)(s.K * split), kMsgThreads, kSrcWords * sizeof(uint32_t), st>>>(
         src_lo, src_hi, blk, n, split, (const uint32_t*)s_in, (mjx::u64*)msg);
     MJX_LAUNCH_CHECK("k_bin_msg");
-    // two segments per phase-2 step (measured at N=1e9, d=6: one 8.30 ms per
-    // sweep, two 8.19, four 10.5 -- the LDS counts are not the bound: without
-    // them the sweep takes 7.7 ms)
     // the flat form streams the tile contiguously; it needs the tile's
     // segment table in LDS (K <= kFlatMaxK: n <= ~1e9); MJX_BIN_APPLY=segments
     // forces the per-segment form (tests)
     const char* form = getenv("MJX_BIN_APPLY");
     const bool flat = s.K <= kFlatMaxK && !(form && form[0] == 's');
     if (flat) {
-        MJX_HIP(hipFuncSetAttribute((const void*)k_bin_apply_flat, hipFuncAttributeMaxDynamicSharedMemorySize,
+        MJX_HIP(hipFuncSetAttribute((const void*)k_bin_apply_flat<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     kCntWords * (int)sizeof(uint32_t)), "k_bin_apply_flat lds");
-        k_bin_apply_flat<<<(unsigned)s.T, kApplyThreads, kCntWords * sizeof(uint32_t), st>>>(
+        k_bin_apply_flat<2><<<(unsigned)s.T, kApplyThreads, kCntWords * sizeof(uint32_t), st>>>(
             off, p1T, p2, (const mjx::u64*)msg, s.K, row_lo, row_hi, d, (const uint32_t*)s_in, (mjx::u64*)s_out,
             counts);
         MJX_LAUNCH_CHECK("k_bin_apply_flat");

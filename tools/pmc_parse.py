@@ -51,16 +51,22 @@ def main():
                  "read_bytes_corrected": 2 * fk * 1024, "write_bytes": wk * 1024,
                  "bytes_per_launch": 2 * fk * 1024 + wk * 1024}
         res[short(k)] = entry
-    # calibration: the copy dispatch with the largest write
-    cands = [(v["write_bytes"], k) for k, v in res.items() if not k.startswith("_") and "copy" in k.lower()]
-    if cands:
-        _, ck = max(cands)
-        c = res[ck]
+    # calibration: the copy dispatch whose write is closest to the known count
+    best = None
+    for k in set(fetch) & set(write):
+        if "copy" not in k.lower() or len(fetch[k]) != len(write[k]):
+            continue
+        for fk, wk in zip(fetch[k], write[k]):
+            err = abs(wk * 1024 - calib_bytes)
+            if best is None or err < best[0]:
+                best = (err, k, fk, wk)
+    if best is not None:
+        _, ck, fk, wk = best
         res["_calibration"] = {
-            "kernel": ck, "known_read_bytes": calib_bytes, "known_write_bytes": calib_bytes,
-            "fetch_bytes_raw": c["fetch_kib"] * 1024, "write_bytes_raw": c["write_bytes"],
-            "read_factor": calib_bytes / max(1.0, c["fetch_kib"] * 1024),
-            "write_factor": calib_bytes / max(1.0, c["write_bytes"]),
+            "kernel": short(ck), "known_read_bytes": calib_bytes, "known_write_bytes": calib_bytes,
+            "fetch_bytes_raw": fk * 1024, "write_bytes_raw": wk * 1024,
+            "read_factor": calib_bytes / max(1.0, fk * 1024),
+            "write_factor": calib_bytes / max(1.0, wk * 1024),
         }
     # bench.py key: the fused-count sweep and the plain sweep of the rollout
     sweeps = [v for k, v in res.items() if k.startswith("mjx::k_sweep_ell_rp") or "k_sweep_ell_rp" in k]
@@ -68,6 +74,23 @@ def main():
         tot = sum(v["bytes_per_launch"] * v["dispatches"] for v in sweeps)
         cnt = sum(v["dispatches"] for v in sweeps)
         res["k_sweep_ell_rp"] = {"bytes_per_launch": tot / cnt, "dispatches": cnt}
+    # HPR (C3) and binned C5 kernels: one entry per kernel family (the
+    # unqualified name without template arguments; k_bin_apply covers _flat)
+    def base(k):
+        return k.split("<")[0].split("::")[-1].strip()
+    fams = {"k_hpr_update_pipe": lambda b: b == "k_hpr_update_pipe",
+            "k_hpr_update": lambda b: b == "k_hpr_update",
+            "k_hpr_edge_z": lambda b: b == "k_hpr_edge_z",
+            "k_hpr_node_marg": lambda b: b == "k_hpr_node_marg",
+            "k_bin_msg": lambda b: b == "k_bin_msg",
+            "k_bin_apply": lambda b: b.startswith("k_bin_apply")}
+    entries = {k: v for k, v in res.items() if isinstance(v, dict) and "fetch_kib" in v}
+    for fam, match in fams.items():
+        ks = [v for k, v in entries.items() if match(base(k))]
+        if ks:
+            tot = sum(v["bytes_per_launch"] * v["dispatches"] for v in ks)
+            cnt = sum(v["dispatches"] for v in ks)
+            res[fam] = {"bytes_per_launch": tot / cnt, "dispatches": cnt}
     os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)

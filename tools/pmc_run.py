@@ -3,7 +3,9 @@
 
 Runs, on cuda:0, exactly the bench.py sweep (d=4 RRG, N=1e6, R=4096
 replica-packed, 2 sweeps per rollout, fused count on the last one) a few
-times, preceded by a calibration copy of a known byte count (torch's
+times, then (unless --no-hpr) the C3 HPR iteration (d=4 RRG, N=1e5,
+p=c=2, fp32: HPr_dp + marginals_comp) and (unless --no-giant) a few sweeps
+of the C5 partitioned N=1e9 d=6 graph on one rank, preceded by a calibration copy of a known byte count (torch's
 vectorised copy, 16 B per lane) that tools/pmc_parse.py uses to check the
 gfx950 FETCH_SIZE correction (MI355X_MICROARCH.md, HBM section).
 """
@@ -23,6 +25,9 @@ def main():
     ap.add_argument("--T", type=int, default=2)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--calib-mb", type=int, default=1024)
+    ap.add_argument("--no-hpr", action="store_true")
+    ap.add_argument("--no-giant", action="store_true")
+    ap.add_argument("--giant-n", type=int, default=1_000_000_000)
     args = ap.parse_args()
     import torch
     import mjx
@@ -48,6 +53,33 @@ def main():
         counts.zero_()
         mjx.rollout(g, s0, args.T, words=W, out=out, tmp=tmp, counts=counts)
     torch.cuda.synchronize()
+    del s0, out, tmp, g
+    if not args.no_hpr:
+        hn, hd, p, c = 100_000, 4, 2, 2
+        plan = mjx.HPRPlan(mjx.random_regular_edges(hd, hn, seed=3), hn, hd)
+        nc = 4 ** (p + c)
+        chi = torch.rand((2 * plan.E, nc), dtype=torch.float32, device=dev, generator=gen)
+        chi /= chi.sum(1, keepdim=True)
+        b = torch.rand((hn, 2), dtype=torch.float32, device=dev, generator=gen)
+        b /= b.sum(1, keepdim=True)
+        hout = torch.empty_like(chi)
+        z = torch.empty(4 * plan.E, dtype=torch.float32, device=dev)
+        mg = torch.empty((hn, 2), dtype=torch.float32, device=dev)
+        for _ in range(args.reps):
+            mjx.HPr_dp(chi, b, plan, p, c, 1, 25 * hn, 0.4, out=hout)
+            mjx.marginals_comp(hout, plan, p, c, zwork=z, out=mg)
+        torch.cuda.synchronize()
+        del chi, hout, plan
+        print("pmc_run hpr done", flush=True)
+    if not args.no_giant:
+        sh = mjx.ShardedRRG(6, args.giant_n, seed=12345, mode="binned")
+        sh.drop_adjacency()
+        sh.buf[sh.cur].copy_(torch.randint(-2 ** 62, 2 ** 62, sh.buf[sh.cur].shape, dtype=torch.int64,
+                                           device=dev, generator=gen))
+        for _ in range(args.reps):
+            sh.sweep()
+        torch.cuda.synchronize()
+        print("pmc_run giant done", flush=True)
     print(f"pmc_run done: n={n} d={d} R={R} T={args.T} reps={args.reps} calib={nb} B", flush=True)
 
 
