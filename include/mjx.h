@@ -348,10 +348,24 @@ int64_t mjx_bdcm_scratch_bytes(int D, int p, int c);
  * reads chi before any of its own rows change: Jacobi within a class,
  * Gauss-Seidel across classes when called in ascending D).  damp >= 1 assigns
  * normalize(chi2): with D = 0 that is the leaf reset of nb:404-417.
- * delta_bits (nullable): atomic max of |new - old| as IEEE bits (a NaN wins). */
+ * delta_bits (nullable): atomic max of |new - old| as IEEE bits (a NaN wins).
+ * gate (nullable): when *gate != 0 on the device the launches do nothing (the
+ * stop flag of a captured convergence loop, ctl + 1 below).
+ * w_dev (nullable): two doubles {exp(-lmbd), exp(lmbd)} read on the device in
+ * place of the lmbd argument, so one captured loop serves every lambda. */
 int mjx_bdcm_update_class(double* chi, const int32_t* rows, const int32_t* inc, int64_t m, int D, int p, int c,
                           int attr_value, double lmbd, double damp, double eps, double* upd,
-                          unsigned long long* delta_bits, void* scratch, int64_t scratch_bytes, void* stream);
+                          unsigned long long* delta_bits, const long long* gate, const double* w_dev, void* scratch,
+                          int64_t scratch_bytes, void* stream);
+/* The notebook's convergence loop on the device (nb:422-431: while delta > eps,
+ * t += 1, stop at T_max), for capture in a hipGraph with one host read per
+ * batch.  ctl[4] int64: [0] delta bits of the running sweep (pass ctl as
+ * delta_bits), [1] stop flag (pass ctl + 1 as gate), [2] sweeps done t,
+ * [3] delta bits of the last completed sweep.  begin: if not stopped, ctl[0] = 0;
+ * end: if not stopped, t += 1, ctl[3] = ctl[0], stop when !(delta > eps) or
+ * t >= t_max.  Zero ctl before the loop. */
+int mjx_bdcm_iter_begin(long long* ctl, void* stream);
+int mjx_bdcm_iter_end(long long* ctl, double eps, int64_t t_max, void* stream);
 /* Zi_ER for the m nodes of degree D (nb:211-276): zi[nodes[k]] = max(Zi, eps);
  * inc[k*D + j] = row of the message from the j-th neighbour into the node. */
 int mjx_bdcm_node_z(const double* chi, const int32_t* nodes, const int32_t* inc, int64_t m, int D, int p, int c,

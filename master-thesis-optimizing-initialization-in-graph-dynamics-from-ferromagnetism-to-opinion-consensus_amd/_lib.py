@@ -67,7 +67,9 @@ SIGNATURES = {
     "mjx_bdcm_lds_bytes": [c_int, c_int, c_int],
     "mjx_bdcm_scratch_bytes": [c_int, c_int, c_int],
     "mjx_bdcm_update_class": [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_int, c_dbl, c_dbl, c_dbl, c_vp,
-                              c_vp, c_vp, c_i64, c_vp],
+                              c_vp, c_vp, c_vp, c_vp, c_i64, c_vp],
+    "mjx_bdcm_iter_begin": [c_vp, c_vp],
+    "mjx_bdcm_iter_end": [c_vp, c_dbl, c_i64, c_vp],
     "mjx_bdcm_node_z": [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_int, c_dbl, c_dbl, c_vp, c_vp, c_i64,
                         c_vp],
     "mjx_bdcm_edge_obs": [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_dbl, c_vp, c_vp, c_vp],

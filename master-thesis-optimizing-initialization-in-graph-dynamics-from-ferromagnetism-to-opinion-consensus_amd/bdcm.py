@@ -17,9 +17,11 @@ explicit arguments:
 
 ``chi`` is the notebook's message array in float64, shape (2E, 4^T) or
 (2E,) + (2,)*2T, resident on the device and updated in place like the
-reference's.  Every update and observable is a libmjx kernel; the host only
-loops over degree classes and lambdas and reads back one convergence scalar
-per iteration (the reference's own ``while(delta>eps)`` test).
+reference's.  Every update and observable is a libmjx kernel.  The convergence loop
+(the reference's ``while(delta>eps)``, nb:422-431) runs on the device: a
+batch of sweeps is captured once per lambda as a hipGraph, each sweep gated by
+a device stop flag that the sweep's end sets (mjx_bdcm_iter_end), and the host
+reads the control block once per batch.
 """
 
 import numpy as np
@@ -98,6 +100,8 @@ class BDCMPlan:
         self._work = torch.empty(256, dtype=torch.float64, device=dev)
         self._sums = torch.zeros(4, dtype=torch.float64, device=dev)
         self._delta = torch.zeros(1, dtype=torch.int64, device=dev)
+        self._ctl = torch.zeros(4, dtype=torch.int64, device=dev)     # device loop control (mjx_bdcm_iter_*)
+        self._w = torch.zeros(2, dtype=torch.float64, device=dev)      # lambda weights of a captured loop
         self._upd = None
 
     @property
@@ -170,23 +174,82 @@ def _scratch_args(plan, p, c):
     return (_device.ptr(sc), sc.numel()) if sc is not None else (None, 0)
 
 
-def _update(ch, plan, D, rows, inc, m, p, c, attr_value, lmbd, damp, eps, delta):
+def _update(ch, plan, D, rows, inc, m, p, c, attr_value, lmbd, damp, eps, delta, gate=None, w_dev=None):
     _lib.call("mjx_bdcm_update_class", _device.ptr(ch), _device.ptr(rows), _device.ptr(inc) if D else None, m, D,
               int(p), int(c), int(attr_value), float(lmbd), float(damp), float(eps),
               _device.ptr(plan.upd(ch.shape[1])), _device.ptr(delta) if delta is not None else None,
+              _device.ptr(gate) if gate is not None else None, _device.ptr(w_dev) if w_dev is not None else None,
               *_scratch_args(plan, p, c), _device.stream_handle())
 
 
-def BDCM_ER(chi, plan, p, c, attr_value, lmbd_in, damppar, epsilon=0.0, delta=None):
+def BDCM_ER(chi, plan, p, c, attr_value, lmbd_in, damppar, epsilon=0.0, delta=None, gate=None, w_dev=None):
     """One BDCM sweep over the edge classes D > 0 in ascending order, each class
     reading chi as already overwritten by the earlier ones (nb:133-198).
     Updates chi in place and returns it.  ``delta`` (int64 device tensor of 1,
-    optional): receives max |chi_new - chi_old| as float64 bits (atomic max)."""
+    optional): receives max |chi_new - chi_old| as float64 bits (atomic max).
+    ``gate`` (int64 device tensor, optional): the sweep does nothing while
+    gate[0] != 0 (the stop flag of a captured loop).  ``w_dev`` (float64
+    device tensor of 2, optional): {exp(-lmbd), exp(lmbd)} read on the device
+    instead of ``lmbd_in``."""
     ch = _chi2d(chi, plan, p, c)
     for (D, rows, inc, m) in plan.edge_classes:
         if D > 0:
-            _update(ch, plan, D, rows, inc, m, p, c, attr_value, lmbd_in, damppar, epsilon, delta)
+            _update(ch, plan, D, rows, inc, m, p, c, attr_value, lmbd_in, damppar, epsilon, delta, gate, w_dev)
     return chi
+
+
+def _sweep_gated(ch, plan, p, c, attr_value, lmbd, damppar, epsilon, eps, T_max, w_dev=None):
+    """One iteration of the device loop: begin, the gated sweep, end."""
+    st = _device.stream_handle()
+    ctl = plan._ctl
+    _lib.call("mjx_bdcm_iter_begin", _device.ptr(ctl), st)
+    BDCM_ER(ch, plan, p, c, attr_value, lmbd, damppar, epsilon, delta=ctl[0:1], gate=ctl[1:2], w_dev=w_dev)
+    _lib.call("mjx_bdcm_iter_end", _device.ptr(ctl), float(eps), int(T_max), st)
+
+
+def converge(chi, plan, p, c, attr_value, lmbd_in, damppar, eps, T_max, epsilon=0.0, batch=32, graph=True):
+    """BDCM_ER until max|delta chi| <= eps or T_max sweeps (nb:422-431) with the
+    loop test on the device: batches of ``batch`` gated sweeps, one host read
+    per batch.  ``graph``: the batch is captured once as a hipGraph (kept on the
+    plan for the same chi and arguments; lambda is read from device memory, so
+    one capture serves the whole lambda sweep) and replayed; else the sweeps
+    are launched eagerly.  Returns (t, delta of the last sweep) like the
+    reference's loop; chi ends in the state after sweep t exactly (the sweeps
+    past the stop are no-ops)."""
+    ch = _chi2d(chi, plan, p, c)
+    plan.check_sizes(p, c)
+    plan.upd(ch.shape[1])                    # every buffer exists before a capture
+    ctl = plan._ctl
+    ctl.zero_()
+    g = None
+    w_dev = None
+    if graph:
+        import math
+        w_dev = plan._w
+        w_dev.copy_(torch.tensor([math.exp(-lmbd_in), math.exp(lmbd_in)], dtype=torch.float64))
+        key = (ch.data_ptr(), int(p), int(c), int(attr_value), float(damppar), float(eps),
+               int(T_max), float(epsilon), int(batch))
+        cache = getattr(plan, "_graphs", None)
+        if cache is None:
+            cache = plan._graphs = {}
+        g = cache.get(key)
+        if g is None:
+            # capture on a side stream (torch's rule); replayed on the current one
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(batch):
+                    _sweep_gated(ch, plan, p, c, attr_value, lmbd_in, damppar, epsilon, eps, T_max, w_dev)
+            cache.clear()                    # one live graph per plan
+            cache[key] = g
+    while True:
+        if graph:
+            g.replay()
+        else:
+            for _ in range(batch):
+                _sweep_gated(ch, plan, p, c, attr_value, lmbd_in, damppar, epsilon, eps, T_max)
+        h = ctl.cpu()
+        if int(h[1]):
+            return int(h[2]), float(h[3:4].view(torch.float64)[0])
 
 
 def bdcm_leaf_reset(chi, plan, p, c, attr_value, lmbd_in):
@@ -251,11 +314,14 @@ def avg_m_init_GENERAL_ER(chi, plan, p, c, attr_value, epsilon=0.0):
 
 
 def BDCM_entropy_procedure_GENERAL_ER(chi, plan, lambdas, T_max=1300, p=1, c=1, attr_value=1, eps=1e-6,
-                                      damppar=0.1, epsilon=0.0, stop_ent=-0.05, verbose=False):
+                                      damppar=0.1, epsilon=0.0, stop_ent=-0.05, verbose=False, device_loop=True,
+                                      batch=32):
     """The lambda sweep of nb:394-452: per lambda, leaf reset, BDCM_ER until
     max|delta chi| <= eps or T_max iterations (warm start from the previous
     lambda), then phi, m_init and ent1 = phi + lambda*m_init; stops after
     ent1 < stop_ent or a non-converged lambda (the reference's ``counts``).
+    ``device_loop``: the convergence loop runs as captured batches with a
+    device stop flag (``converge``); False: one host read per sweep.
     Returns dict(m_init, ent1, ent, counts, iters) (zeros past an early stop)."""
     ch = _chi2d(chi, plan, p, c)
     plan.check_sizes(p, c)
@@ -268,15 +334,20 @@ def BDCM_entropy_procedure_GENERAL_ER(chi, plan, lambdas, T_max=1300, p=1, c=1, 
     dval = dbits.view(torch.float64)
     for k, lm in enumerate(lambdas.tolist()):
         bdcm_leaf_reset(ch, plan, p, c, attr_value, lm)
-        delta, t = 1.0, 0
-        while delta > eps:
-            dbits.zero_()
-            BDCM_ER(ch, plan, p, c, attr_value, lm, damppar, epsilon, delta=dbits)
-            delta = float(dval.item())
-            t += 1
+        if device_loop:
+            t, _ = converge(ch, plan, p, c, attr_value, lm, damppar, eps, T_max, epsilon, batch=batch)
             if t >= T_max:
-                delta = 0
                 counts = lm
+        else:
+            delta, t = 1.0, 0
+            while delta > eps:
+                dbits.zero_()
+                BDCM_ER(ch, plan, p, c, attr_value, lm, damppar, epsilon, delta=dbits)
+                delta = float(dval.item())
+                t += 1
+                if t >= T_max:
+                    delta = 0
+                    counts = lm
         iters[k] = t
         ent[k], m_init[k] = observables(ch, plan, p, c, attr_value, lm, epsilon)
         ent1[k] = ent[k] + lm * m_init[k]

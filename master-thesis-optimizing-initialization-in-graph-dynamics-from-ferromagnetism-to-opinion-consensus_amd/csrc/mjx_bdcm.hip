@@ -20,9 +20,11 @@
 // over (D+1)^T count vectors becomes one lookup per (x_a, x_b).  The node factor
 // of Zi_ER (nb:211-276) is the same box with no receiver term.
 //
-// Kernel geometry: one wave per message (or node).  The DP table of every valid
-// x_a lives in LDS and is convolved in place one neighbour at a time (top-down
-// chunks, read-then-write), then turned into directional cumulative sums.
+// Kernel geometry: one workgroup per message (or node), one to four waves by the
+// table size.  The DP table of every valid x_a lives in LDS and is convolved in
+// place one neighbour at a time (top-down chunks of the workgroup's width, all
+// reads of a chunk before a barrier and its writes: an entry reads only entries
+// at or below itself), then turned into directional cumulative sums.
 #include "mjx_common.h"
 #include <math.h>
 
@@ -37,6 +39,7 @@ constexpr size_t kMaxLds = 160 * 1024;
 struct Geo {
     int T, P, D, X, XV, B, S, ab;     // ab: trajectory index bit of the attractor spin at t = T-1
     int pw[kMaxT];                    // B^(T-1-t)
+    int src_tab;                      // 1: the convolution's source indices are tabulated in LDS
 };
 
 __host__ __device__ inline int bspin(int x, int t, int T) { return ((x >> (T - 1 - t)) & 1) ? 1 : -1; }
@@ -62,12 +65,18 @@ static bool make_geo(int D, int p, int c, int attr_value, Geo* g) {
     for (int t = T; t < kMaxT; ++t) g->pw[t] = 0;
     g->S = (int)S;
     g->ab = attr_value > 0 ? 1 : 0;
+    g->src_tab = 0;
     return true;
 }
 
 static size_t tab_bytes(const Geo& g) { return (size_t)g.XV * g.S * sizeof(double); }
 static size_t m_bytes(const Geo& g) { return (size_t)g.D * g.XV * g.XV * sizeof(double); }
 static size_t lds_bytes(const Geo& g) { return tab_bytes(g) + m_bytes(g); }
+// per table entry: the row offset a*XV of its x_a and, per x_k, the entry it
+// reads in a convolution step (-1: none) -- the index arithmetic (runtime
+// divisions by the mixed radix) done once per item instead of once per step
+static size_t src_bytes(const Geo& g) { return (size_t)g.XV * g.S * (g.XV + 1) * sizeof(int32_t); }
+constexpr size_t kSrcTabMax = 32 * 1024;
 
 // the spin the condition on rho_t must produce, and the spin a tie keeps
 // (traj_condition for t < T-1, atr_condition for t = T-1; nb:66-83)
@@ -116,30 +125,74 @@ __device__ inline double wave_sum(double v) {
 // LL of item e for every valid x_a into tab[XV][S], then directional cumulative
 // sums.  inc[e*D + m] = row of the m-th incoming message k_m -> a.
 __device__ void build_table(const Geo& g, const double* __restrict__ chi, const int32_t* __restrict__ inc, int64_t e,
-                            double* tab, double* M, int lane) {
+                            double* tab, double* M, int lane, int32_t* srct) {
+    // every loop strides over the workgroup (one to four waves per item)
+    const int nt = blockDim.x;
     const int X = g.X, NC = X * X, XV = g.XV, S = g.S, D = g.D, ab = g.ab, T = g.T;
     // M[m][a][k] = chi^{k_m -> a}(x_k, x_a), valid x_a = 2a+ab, x_k = 2k+ab
-    for (int q = lane; q < D * XV * XV; q += 64) {
+    for (int q = lane; q < D * XV * XV; q += nt) {
         const int m = q / (XV * XV), r = q % (XV * XV), a = r / XV, k = r % XV;
         const int64_t row = inc[e * D + m];
         M[q] = chi[row * NC + (2 * k + ab) * X + (2 * a + ab)];
     }
-    for (int q = lane; q < XV * S; q += 64) tab[q] = 0.0;
+    for (int q = lane; q < XV * S; q += nt) tab[q] = 0.0;
     __syncthreads();
     if (D == 0) {
         if (lane < XV) tab[lane * S] = 1.0;
     } else {
-        for (int q = lane; q < XV * XV; q += 64) {
+        for (int q = lane; q < XV * XV; q += nt) {
             const int a = q / XV, k = q % XV;
             tab[a * S + traj_off(g, 2 * k + ab)] = M[q];
         }
     }
-    __syncthreads();
     const int tot = XV * S;
-    for (int m = 1; m < D; ++m) {
+    if (srct && D > 1) {
+        for (int q = lane; q < tot; q += nt) {
+            const int a = q / S, i = q % S;
+            int dg[kMaxT];
+            int rem = i;
+            for (int t = 0; t < T; ++t) {
+                dg[t] = rem / g.pw[t];
+                rem -= dg[t] * g.pw[t];
+            }
+            int32_t* row = srct + q * (XV + 1);
+            row[0] = a * XV;
+            for (int k = XV - 1; k >= 0; --k) {
+                const int xk = 2 * k + ab;
+                int src = i;
+                bool ok = true;
+                for (int t = 0; t < T; ++t)
+                    if (bspin(xk, t, T) > 0) {
+                        ok = ok && dg[t] > 0;
+                        src -= g.pw[t];
+                    }
+                row[1 + k] = ok ? a * S + src : -1;
+            }
+        }
+    }
+    __syncthreads();
+    for (int m = 1; m < D && srct; ++m) {
+        const double* Mm = M + m * XV * XV;
+        for (int base = ((tot - 1) / nt) * nt; base >= 0; base -= nt) {
+            const int q = base + lane;
+            double acc = 0.0;
+            if (q < tot) {
+                const int32_t* row = srct + q * (XV + 1);
+                const double* Ma = Mm + row[0];
+                for (int k = XV - 1; k >= 0; --k) {       // the same order as below
+                    const int src = row[1 + k];
+                    if (src >= 0) acc += tab[src] * Ma[k];
+                }
+            }
+            __syncthreads();
+            if (q < tot) tab[q] = acc;
+            __syncthreads();
+        }
+    }
+    for (int m = 1; m < D && !srct; ++m) {
         const double* Mm = M + m * XV * XV;
         // in place, top-down: an entry only reads entries at or below itself
-        for (int base = ((tot - 1) / 64) * 64; base >= 0; base -= 64) {
+        for (int base = ((tot - 1) / nt) * nt; base >= 0; base -= nt) {
             const int q = base + lane;
             double acc = 0.0;
             if (q < tot) {
@@ -171,7 +224,7 @@ __device__ void build_table(const Geo& g, const double* __restrict__ chi, const 
     const int lines = XV * (S / g.B);
     for (int t = 0; t < T; ++t) {
         const int step = g.pw[t], span = step * g.B;
-        for (int L = lane; L < lines; L += 64) {
+        for (int L = lane; L < lines; L += nt) {
             const int a = L / (S / g.B), r = L % (S / g.B);
             double* p = tab + a * S + (r / step) * span + (r % step);
             double run = 0.0;
@@ -195,16 +248,25 @@ __device__ void build_table(const Geo& g, const double* __restrict__ chi, const 
 // damp >= 1 assigns normalize(chi2) (the leaf reset of nb:404-417 is class D = 0).
 // The count table lives in LDS, or (a class whose table exceeds the LDS budget)
 // in the global slab gtab, one table per workgroup of the launch; item e0 + blockIdx.x.
-__global__ void __launch_bounds__(64) k_bdcm_edge(const double* __restrict__ chi, const int32_t* __restrict__ rows,
+__global__ void __launch_bounds__(256) k_bdcm_edge(const double* __restrict__ chi, const int32_t* __restrict__ rows,
                                                   const int32_t* __restrict__ inc, Geo g, double w_plus,
                                                   double w_minus, double eps, double damp, double* __restrict__ upd,
-                                                  int64_t e0, double* __restrict__ gtab) {
+                                                  int64_t e0, double* __restrict__ gtab,
+                                                  const long long* __restrict__ gate,
+                                                  const double* __restrict__ w_dev) {
+    if (gate && *gate) return;                 // a converged loop replays as no-ops
+    if (w_dev) {                               // lambda's weights from device memory (a captured loop)
+        w_plus = w_dev[0];
+        w_minus = w_dev[1];
+    }
     extern __shared__ __align__(16) double sm[];
     double* M = sm;
     double* tab = gtab ? gtab + (size_t)blockIdx.x * g.XV * g.S : sm + (size_t)g.D * g.XV * g.XV;
     const int lane = threadIdx.x;
     const int64_t e = e0 + blockIdx.x;
-    build_table(g, chi, inc, e, tab, M, lane);
+    build_table(g, chi, inc, e, tab, M, lane,
+                g.src_tab ? reinterpret_cast<int32_t*>(sm + (size_t)g.D * g.XV * g.XV + (size_t)g.XV * g.S) : nullptr);
+    if (lane >= 64) return;                    // the epilogue is one wave's (no barrier follows)
     const int X = g.X, NC = X * X;
     double v[4];
     double rs = 0.0;
@@ -238,7 +300,9 @@ __global__ void __launch_bounds__(64) k_bdcm_edge(const double* __restrict__ chi
 // scatter the class's new rows into chi; max |new - old| as double bits
 __global__ void __launch_bounds__(256) k_bdcm_commit(double* __restrict__ chi, const int32_t* __restrict__ rows,
                                                      int64_t m, int NC, const double* __restrict__ upd,
-                                                     unsigned long long* __restrict__ delta_bits) {
+                                                     unsigned long long* __restrict__ delta_bits,
+                                                     const long long* __restrict__ gate) {
+    if (gate && *gate) return;
     unsigned long long mx = 0;
     const int64_t total = m * NC;
     for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < total; q += (int64_t)gridDim.x * 256) {
@@ -260,8 +324,26 @@ __global__ void __launch_bounds__(256) k_bdcm_commit(double* __restrict__ chi, c
     }
 }
 
+// the notebook's convergence loop on the device (nb:422-431):
+//   while delta > eps: delta = BDCM sweep; t += 1; if t >= T_max: stop
+// ctl[0] = delta bits of the running sweep, ctl[1] = stop flag, ctl[2] = t,
+// ctl[3] = delta bits of the last completed sweep.  One thread, plain stores.
+__global__ void k_bdcm_iter_begin(long long* __restrict__ ctl) {
+    if (threadIdx.x == 0 && ctl[1] == 0) ctl[0] = 0;
+}
+
+__global__ void k_bdcm_iter_end(long long* __restrict__ ctl, double eps, long long t_max) {
+    if (threadIdx.x != 0 || ctl[1] != 0) return;
+    const long long bits = ctl[0];
+    const double delta = __longlong_as_double(bits);
+    const long long t = ctl[2] + 1;
+    ctl[2] = t;
+    ctl[3] = bits;
+    if (!(delta > eps) || t >= t_max) ctl[1] = 1;      // NaN ends the loop too (while NaN > eps is false)
+}
+
 // Zi_ER for one node-degree class (nb:211-276): zi[node] = max(sum_xa w Ai LL, eps)
-__global__ void __launch_bounds__(64) k_bdcm_node(const double* __restrict__ chi, const int32_t* __restrict__ nodes,
+__global__ void __launch_bounds__(256) k_bdcm_node(const double* __restrict__ chi, const int32_t* __restrict__ nodes,
                                                   const int32_t* __restrict__ inc, Geo g, double w_plus,
                                                   double w_minus, double eps, double* __restrict__ zi, int64_t e0,
                                                   double* __restrict__ gtab) {
@@ -270,7 +352,9 @@ __global__ void __launch_bounds__(64) k_bdcm_node(const double* __restrict__ chi
     double* tab = gtab ? gtab + (size_t)blockIdx.x * g.XV * g.S : sm + (size_t)g.D * g.XV * g.XV;
     const int lane = threadIdx.x;
     const int64_t e = e0 + blockIdx.x;
-    build_table(g, chi, inc, e, tab, M, lane);
+    build_table(g, chi, inc, e, tab, M, lane,
+                g.src_tab ? reinterpret_cast<int32_t*>(sm + (size_t)g.D * g.XV * g.XV + (size_t)g.XV * g.S) : nullptr);
+    if (lane >= 64) return;
     double z = 0.0;
     if (lane < g.XV) {
         const int xa = 2 * lane + g.ab;
@@ -352,9 +436,18 @@ static int set_lds(K kern) {
 
 // items per launch and dynamic LDS: everything in LDS when the table fits,
 // else as many tables as the scratch slab holds (0: unsupported)
-static int64_t plan_launch(const Geo& g, int64_t m, void* scratch, int64_t scratch_bytes, size_t* lds, bool* in_lds) {
+// one wave per item for small tables, up to four for the hub classes (the
+// convolution is a serial chain of D-1 steps over ceil(tot / width) chunks)
+static int item_threads(const Geo& g) {
+    const int64_t tot = (int64_t)g.XV * g.S;
+    return tot <= 128 ? 64 : (tot <= 512 ? 128 : 256);
+}
+
+static int64_t plan_launch(Geo& g, int64_t m, void* scratch, int64_t scratch_bytes, size_t* lds, bool* in_lds) {
     *in_lds = lds_bytes(g) <= kMaxLds;
     *lds = *in_lds ? lds_bytes(g) : m_bytes(g);
+    g.src_tab = (*in_lds && g.D > 1 && src_bytes(g) <= kSrcTabMax && lds_bytes(g) + src_bytes(g) <= kMaxLds) ? 1 : 0;
+    if (g.src_tab) *lds += src_bytes(g);
     if (!*in_lds && m_bytes(g) > kMaxLds) return 0;
     if (*in_lds) return m;
     return scratch ? scratch_bytes / (int64_t)tab_bytes(g) : 0;
@@ -382,8 +475,8 @@ extern "C" int64_t mjx_bdcm_scratch_bytes(int D, int p, int c) {
 
 extern "C" int mjx_bdcm_update_class(double* chi, const int32_t* rows, const int32_t* inc, int64_t m, int D, int p,
                                      int c, int attr_value, double lmbd, double damp, double eps, double* upd,
-                                     unsigned long long* delta_bits, void* scratch, int64_t scratch_bytes,
-                                     void* stream) {
+                                     unsigned long long* delta_bits, const long long* gate, const double* w_dev,
+                                     void* scratch, int64_t scratch_bytes, void* stream) {
     if (m < 0 || !chi) return MJX_EINVAL;
     if (m == 0) return MJX_OK;
     if (!rows || !upd || (D > 0 && !inc) || !(damp > 0.0)) return MJX_EINVAL;
@@ -400,13 +493,27 @@ extern "C" int mjx_bdcm_update_class(double* chi, const int32_t* rows, const int
     for (int64_t e0 = 0; e0 < m; e0 += per) {
         const int64_t cnt = (m - e0 < per) ? m - e0 : per;
         if (cnt > (int64_t)INT32_MAX) return MJX_ERANGE;
-        k_bdcm_edge<<<(unsigned)cnt, 64, lds, st>>>(chi, rows, inc, g, exp(-lmbd), exp(lmbd), eps, damp, upd, e0,
-                                                    in_lds ? nullptr : (double*)scratch);
+        k_bdcm_edge<<<(unsigned)cnt, item_threads(g), lds, st>>>(chi, rows, inc, g, exp(-lmbd), exp(lmbd), eps, damp, upd, e0,
+                                                    in_lds ? nullptr : (double*)scratch, gate, w_dev);
         MJX_LAUNCH_CHECK("k_bdcm_edge");
     }
     const int NC = g.X * g.X;
-    k_bdcm_commit<<<grid_for(m * NC), 256, 0, st>>>(chi, rows, m, NC, upd, delta_bits);
+    k_bdcm_commit<<<grid_for(m * NC), 256, 0, st>>>(chi, rows, m, NC, upd, delta_bits, gate);
     MJX_LAUNCH_CHECK("k_bdcm_commit");
+    return MJX_OK;
+}
+
+extern "C" int mjx_bdcm_iter_begin(long long* ctl, void* stream) {
+    if (!ctl) return MJX_EINVAL;
+    k_bdcm_iter_begin<<<1, 64, 0, as_stream(stream)>>>(ctl);
+    MJX_LAUNCH_CHECK("k_bdcm_iter_begin");
+    return MJX_OK;
+}
+
+extern "C" int mjx_bdcm_iter_end(long long* ctl, double eps, int64_t t_max, void* stream) {
+    if (!ctl) return MJX_EINVAL;
+    k_bdcm_iter_end<<<1, 64, 0, as_stream(stream)>>>(ctl, eps, (long long)t_max);
+    MJX_LAUNCH_CHECK("k_bdcm_iter_end");
     return MJX_OK;
 }
 
@@ -428,7 +535,7 @@ extern "C" int mjx_bdcm_node_z(const double* chi, const int32_t* nodes, const in
     for (int64_t e0 = 0; e0 < m; e0 += per) {
         const int64_t cnt = (m - e0 < per) ? m - e0 : per;
         if (cnt > (int64_t)INT32_MAX) return MJX_ERANGE;
-        k_bdcm_node<<<(unsigned)cnt, 64, lds, st>>>(chi, nodes, inc, g, exp(-lmbd), exp(lmbd), eps, zi, e0,
+        k_bdcm_node<<<(unsigned)cnt, item_threads(g), lds, st>>>(chi, nodes, inc, g, exp(-lmbd), exp(lmbd), eps, zi, e0,
                                                     in_lds ? nullptr : (double*)scratch);
         MJX_LAUNCH_CHECK("k_bdcm_node");
     }

@@ -127,3 +127,52 @@ def test_bdcm_rejects_unsupported_trajectories(mjx_mod):
     chi = torch.ones((2 * plan.E, 4 ** 5), dtype=torch.float64, device="cuda")
     with pytest.raises(mjx_mod.MjxError):
         mjx_mod.BDCM_entropy_procedure_GENERAL_ER(chi, plan, [0.0], p=4, c=1)
+
+
+@pytest.mark.parametrize("graph", [True, False])
+def test_bdcm_device_loop_equals_host_loop(mjx_mod, graph):
+    """The convergence loop with the device stop flag (captured batches, one
+    host read per batch) stops at the same sweep as the reference's
+    while(delta > eps) (nb:422-431) and leaves chi bit-identical: the sweeps
+    of a batch past the stop are no-ops."""
+    z = load_golden(CASES[0])
+    p, c, damp = int(z["p"]), int(z["c"]), float(z["damppar"])
+    plan = plan_of(mjx_mod, z)
+    eps = float(z["eps"])
+    for lm, batch in ((0.0, 32), (0.5, 7)):
+        a = dev(z["chi0"])
+        b = dev(z["chi0"])
+        mjx_mod.bdcm_leaf_reset(a, plan, p, c, 1, lm)
+        mjx_mod.bdcm_leaf_reset(b, plan, p, c, 1, lm)
+        t_dev, d_dev = mjx_mod.bdcm_converge(a, plan, p, c, 1, lm, damp, eps, 1300, batch=batch, graph=graph)
+        delta, t = 1.0, 0
+        dbits = plan._delta
+        while delta > eps:
+            dbits.zero_()
+            mjx_mod.BDCM_ER(b, plan, p, c, 1, lm, damp, delta=dbits)
+            delta = float(dbits.view(torch.float64).item())
+            t += 1
+        assert t_dev == t and d_dev == delta
+        assert torch.equal(a, b)
+
+
+def test_bdcm_device_loop_stops_at_t_max(mjx_mod):
+    """eps = 0 never converges: the device loop stops after exactly T_max
+    sweeps (the reference's counts = lambda branch) even inside a batch."""
+    z = load_golden(CASES[0])
+    p, c, damp = int(z["p"]), int(z["c"]), float(z["damppar"])
+    plan = plan_of(mjx_mod, z)
+    a = dev(z["chi0"])
+    b = dev(z["chi0"])
+    t, _ = mjx_mod.bdcm_converge(a, plan, p, c, 1, 0.3, damp, 0.0, 11, batch=8)
+    for _ in range(11):
+        mjx_mod.BDCM_ER(b, plan, p, c, 1, 0.3, damp)
+    assert t == 11 and torch.equal(a, b)
+    res = mjx_mod.BDCM_entropy_procedure_GENERAL_ER(dev(z["chi0"]), plan, [0.0, 0.5], T_max=5, p=p, c=c, eps=0.0,
+                                                    damppar=damp)
+    host = mjx_mod.BDCM_entropy_procedure_GENERAL_ER(dev(z["chi0"]), plan, [0.0, 0.5], T_max=5, p=p, c=c, eps=0.0,
+                                                     damppar=damp, device_loop=False)
+    # lambda = 0 sets counts = 0 (no stop), lambda = 0.5 sets counts = 0.5 and stops (nb:428-452)
+    assert res["counts"] == host["counts"] == 0.5 and list(res["iters"]) == list(host["iters"]) == [5, 5]
+    for k in ("m_init", "ent1", "ent"):
+        assert np.array_equal(res[k], host[k])
