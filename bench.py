@@ -83,6 +83,26 @@ def parse():
 # ---------------------------------------------------------------------------
 # CPU baseline (runs BEFORE the GPU is touched: forked workers, no exec)
 # ---------------------------------------------------------------------------
+def host_info():
+    """CPU model, os.cpu_count() and library versions."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    info = {"cpu_model": model, "os_cpu_count": os.cpu_count(), "numpy": np.__version__}
+    try:
+        import torch
+        info["torch"] = torch.__version__
+    except ImportError:
+        pass
+    return info
+
+
 def _cpu_worker(args):
     adj, steps_per_rollout, seconds, seed = args
     from oracle import majority as orc
@@ -115,7 +135,7 @@ def cpu_baseline(adj, T, seconds):
     n = adj.shape[0]
     value = rollouts * n * T / max(r[1] for r in res)
     return {
-        "value": value, "unit": "node-updates/s", "cores": cores, "kind": "port",
+        "value": value, "unit": "node-updates/s", "cores": cores, "kind": "port", "host": host_info(),
         "sample": (f"oracle/majority.py s_endstate (numpy, same ops as code/SA_RRG.py:18-26) on the bench graph "
                    f"(d={adj.shape[1]}, N={n}), {T} sweeps per rollout, one replica per rollout, "
                    f"{rollouts} rollouts in ~{seconds:.0f}s per process x {cores} processes "
@@ -204,7 +224,7 @@ def bench_sa_c1(args, rank, world, dist, dev):
         t0 = time.perf_counter()
         o = orc.sa_loop(adj, p, c, seeds[0], max_steps=2000)
         cpu_s = time.perf_counter() - t0
-        res["cpu_baseline"] = {"proposals_per_s": o["num_steps"] / cpu_s, "cores": 1, "kind": "port",
+        res["cpu_baseline"] = {"proposals_per_s": o["num_steps"] / cpu_s, "cores": 1, "kind": "port", "host": host_info(),
                                "sample": f"oracle/majority.py sa_loop (numpy, code/SA_RRG.py:63-88, three rollouts "
                                          f"per proposal) on the same graph, seed {seeds[0]}, {o['num_steps']} "
                                          f"proposals in {cpu_s:.1f} s, one core (the reference runs its replicas "
@@ -405,7 +425,7 @@ def bench_hpr(args, rank, world, dist, dev):
             done += rows.size
         cpu_s = time.perf_counter() - t0
         torch.set_num_threads(old_threads)
-        res["cpu_baseline"] = {"messages_per_s": done / cpu_s, "cores": cores, "kind": "port",
+        res["cpu_baseline"] = {"messages_per_s": done / cpu_s, "cores": cores, "kind": "port", "host": host_info(),
                                "sample": f"oracle/hpr_torch.py HPr_dp (torch CPU ops, float64, "
                                          f"code/HPR_pytorch_RRG.py:183-218) on {rows.size} sampled output rows of "
                                          f"the same graph, repeated for {cpu_s:.1f} s, torch threads = {cores}",
