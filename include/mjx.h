@@ -239,6 +239,12 @@ int mjx_hpr_new_biases(int dtype, void* biases, const void* marg, const double* 
  * zwork[4E] = per-row normalised (Z+ [2E], Z- [2E]) of every directed row. */
 int mjx_hpr_edge_z(int dtype, const void* chi, int64_t E, int p, int c, double eps, void* zwork,
                    void* stream);
+/* Node-indexed bias pairs for mjx_hpr_update from the reference's own bias arrays:
+ * out[2v+k] = src[idx[v]*stride + k*half], k = 0, 1.  From biases_chi
+ * (new_biases_chi, code/HPR_pytorch_RRG.py:128-133): stride = 4^T, half = 4^T/2 and
+ * idx[v] = a row whose source node is v; from biases_i: stride 2, half 1. */
+int mjx_hpr_node_biases(int dtype, const void* src, const int64_t* idx, int64_t stride, int64_t half,
+                        int64_t n, void* out, void* stream);
 
 /* ---- HPR on Erdos-Renyi graphs (the "general (ER)" HPR of code/README.md:1) -
  * HPr_dp with the degree taken per message: rows of degree class D (the

@@ -19,6 +19,7 @@ from .hpr_er import HPRERPlan, HPr_dp_er, marginals_comp_er, hpr_er_plan, hpr_er
 from .bdcm import (BDCMPlan, bdcm_er_plan, BDCM_ER, bdcm_leaf_reset, Zij, Zi_ER, phi_BP_GENERAL_ER,
                    avg_m_init_GENERAL_ER, BDCM_entropy_procedure_GENERAL_ER, bdcm_er_run)
 from .bdcm import converge as bdcm_converge
+from . import drop_in  # reference-signature HPR drop-ins (code/HPR_pytorch_RRG.py)
 
 __all__ = [
     "MjxError", "lib_path", "BinnedPlan", "Graph", "neighbours", "csr_from_networkx", "random_regular_graph",
@@ -28,7 +29,7 @@ __all__ = [
     "HPRPlan", "HPRState", "HPr_dp", "marginals_comp", "new_biases_i", "hpr_run",
     "HPRERPlan", "HPr_dp_er", "marginals_comp_er", "hpr_er_plan", "hpr_er_run",
     "BDCMPlan", "bdcm_er_plan", "BDCM_ER", "bdcm_converge", "bdcm_leaf_reset", "Zij", "Zi_ER", "phi_BP_GENERAL_ER",
-    "avg_m_init_GENERAL_ER", "BDCM_entropy_procedure_GENERAL_ER", "bdcm_er_run",
+    "avg_m_init_GENERAL_ER", "BDCM_entropy_procedure_GENERAL_ER", "bdcm_er_run", "drop_in",
 ]
 
 

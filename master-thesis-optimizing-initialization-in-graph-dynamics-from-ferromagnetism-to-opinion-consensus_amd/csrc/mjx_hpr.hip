@@ -86,3 +86,33 @@ extern "C" int mjx_hpr_new_biases(int dtype, void* biases, const void* marg, con
     MJX_LAUNCH_CHECK("k_hpr_new_biases");
     return MJX_OK;
 }
+
+// per-node bias pairs out[2v + k] = src[idx[v] * stride + k * half]: the
+// node-indexed biases the update kernels read, taken from the reference's
+// chi-shaped biases_chi (stride = 4^T, half = 4^T / 2; code/HPR_pytorch_RRG.py:
+// 120-133, first half of a row = x_k^0 = +1) or from a permuted biases_i
+// (stride 2, half 1)
+template <typename S>
+__global__ void k_hpr_node_biases(const S* __restrict__ src, const int64_t* __restrict__ idx, int64_t stride,
+                                  int64_t half, int64_t n, S* __restrict__ out) {
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t a = idx[v] * stride;
+        out[2 * v] = src[a];
+        out[2 * v + 1] = src[a + half];
+    }
+}
+
+extern "C" int mjx_hpr_node_biases(int dtype, const void* src, const int64_t* idx, int64_t stride, int64_t half,
+                                   int64_t n, void* out, void* stream) {
+    if (n < 1 || stride < 1 || half < 0 || half >= stride || !src || !idx || !out) return MJX_EINVAL;
+    hipStream_t st = as_stream(stream);
+    const unsigned grid = (unsigned)grid_for(n, 8);
+    if (dtype == MJX_F32)
+        k_hpr_node_biases<float><<<grid, 256, 0, st>>>((const float*)src, idx, stride, half, n, (float*)out);
+    else if (dtype == MJX_F64)
+        k_hpr_node_biases<double><<<grid, 256, 0, st>>>((const double*)src, idx, stride, half, n, (double*)out);
+    else
+        return MJX_EINVAL;
+    MJX_LAUNCH_CHECK("k_hpr_node_biases");
+    return MJX_OK;
+}

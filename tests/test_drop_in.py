@@ -1,0 +1,138 @@
+"""Reference-signature drop-ins (mjx.drop_in) for code/HPR_pytorch_RRG.py.
+
+CPU: the graph recovered from the reference's N_edg_pos_chi_mat is the
+fixture graph (up to the node naming the function documents).
+GPU: HPr_dp / marginals_comp called with the reference's own argument lists
+(the arrays the reference builds, as stored in tests/golden/hpr_*.npz) match
+the reference's per-step vectors (1e-12 in float64, 1e-5 in float32), for
+both forms of biases_chi; and the reference's main loop (:342-356) written
+with the drop-ins reproduces the reference's whole-script fixture.
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, load_golden
+from oracle import hpr as orc
+
+CASES = sorted(os.path.basename(f) for f in glob.glob(os.path.join(GOLDEN, "hpr_d*.npz")))
+TOL = {torch.float32: 1e-5, torch.float64: 1e-12}
+
+
+def _src_rows(edges):
+    E = edges.shape[0]
+    return np.concatenate([edges[:, 0], edges[:, 1]])
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_graph_recovered_from_positions(mjx_mod, name):
+    z = load_golden(name)
+    n, d, p, c = (int(z[k]) for k in ("n", "d", "p", "c"))
+    nc = 4 ** (p + c)
+    edges, n2, d2, rep = mjx_mod.drop_in.plan_arrays_from_positions(z["N_edg_pos_chi_mat"], nc)
+    assert (n2, d2) == (n, d)
+    # node v of the recovered graph is the source of row rep[v]
+    ref_id = _src_rows(z["edges"])[rep]
+    assert np.array_equal(np.sort(ref_id), np.arange(n))
+    assert np.array_equal(ref_id[edges], z["edges"])
+
+
+def test_positions_rejects_non_regular(mjx_mod):
+    z = load_golden(CASES[0])
+    P = z["N_edg_pos_chi_mat"].copy()
+    P[0, 0] = P[5, 0]
+    nc = 4 ** (int(z["p"]) + int(z["c"]))
+    with pytest.raises(ValueError):
+        mjx_mod.drop_in.plan_arrays_from_positions(P, nc)
+    with pytest.raises(ValueError):
+        mjx_mod.drop_in.plan_arrays_from_positions(P[:, :1] + 1, nc)
+
+
+def _aux(edges, nbrs, n, p, c):
+    """The reference's auxiliary arrays (code/HPR_pytorch_RRG.py:264-325)."""
+    nc = 4 ** (p + c)
+    inr, src = orc.incoming_rows(edges, nbrs)
+    pos = np.repeat(src, nc).reshape(-1, nc)                      # positions_biases (:120-125)
+    pos[:, nc // 2:] += n
+    return {
+        "N_edg_pos_chi_mat": torch.tensor(inr * nc, dtype=torch.int32, device="cuda"),
+        "N_edges_pos": torch.tensor(orc.edges_pos(edges, nbrs), dtype=torch.int32, device="cuda"),
+        "N_nodes": torch.tensor(np.asarray(nbrs), dtype=torch.int32, device="cuda"),
+        "pos_biases": torch.tensor(pos.reshape(-1), dtype=torch.int32, device="cuda"),
+        "rho_D1": torch.zeros((2 ** (p + c), p + c), dtype=torch.int32, device="cuda"),
+        "pairs": None, "pji": None,
+    }
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("name", CASES)
+def test_reference_signature_step(mjx_mod, name, dtype):
+    di = mjx_mod.drop_in
+    z = load_golden(name)
+    n, d, p, c = (int(z[k]) for k in ("n", "d", "p", "c"))
+    aux = _aux(z["edges"], z["N_nodes"], n, p, c)
+    assert np.array_equal(aux["N_edges_pos"].cpu().numpy(), z["N_edges_pos"])
+    assert np.array_equal(aux["N_edg_pos_chi_mat"].cpu().numpy(), z["N_edg_pos_chi_mat"])
+    attr, lmbd, damp = int(z["attr_value"]), int(z["lmbd_in"]), float(z["damppar"])
+    for k in range(int(z["chain"])):
+        src_chi = z["chi0"] if k == 0 else z[f"it{k - 1}_chi"]
+        src_b = z["biases0"] if k == 0 else z[f"it{k - 1}_biases"]
+        chi_mat = torch.tensor(src_chi, dtype=dtype, device="cuda")
+        biases_i = torch.tensor(src_b, dtype=dtype, device="cuda")
+        lazy = di.new_biases_chi(biases_i, aux["pos_biases"])
+        full = lazy.materialize()
+        assert full.shape == (chi_mat.numel(),)
+        for bc in (lazy, full):
+            col, mat = di.HPr_dp(chi_mat, chi_mat.reshape(-1), bc, aux["rho_D1"], aux["N_edg_pos_chi_mat"], d, p, c,
+                                 attr, lmbd, damp)
+            assert mat.dtype == dtype and col.data_ptr() == mat.data_ptr() and col.shape == (mat.numel(),)
+            got = mat.double().cpu().numpy()
+            ref = z[f"it{k}_chi"]
+            err = float(np.max(np.abs(got - ref) / np.max(np.abs(ref), axis=1, keepdims=True)))
+            assert err <= TOL[dtype], (k, type(bc).__name__, err)
+        ref_chi = torch.tensor(z[f"it{k}_chi"], dtype=dtype, device="cuda")
+        marg = di.marginals_comp(ref_chi, aux["pairs"], aux["pji"], aux["N_edges_pos"],
+                                 epsilon=torch.tensor(1e-15, dtype=torch.float64, device="cuda"))
+        assert float(np.max(np.abs(marg.double().cpu().numpy() - z[f"it{k}_marg"]))) <= TOL[dtype]
+
+
+@pytest.mark.gpu
+def test_reference_main_loop_with_drop_ins(mjx_mod):
+    """code/HPR_pytorch_RRG.py:327-362 written with the drop-ins and the global
+    torch generator (float64, the reference's default dtype) reproduces the
+    reference's whole-script runs (num_steps, conf, mag_reached)."""
+    di = mjx_mod.drop_in
+    full = load_golden("hpr_fullscript.npz")
+    keys = sorted({k.rsplit("_", 1)[0] for k in full if k.endswith("_params")})
+    exact_ties = {"n30_d3_p2c1"}
+    for key in keys:
+        n, d, p, c, TT, tseed = (int(x) for x in full[f"{key}_params"])
+        nbrs = full[f"{key}_graphs"][0].astype(np.int64)
+        edges = full[f"{key}_edges"]
+        aux = _aux(edges, nbrs, n, p, c)
+        nc = 4 ** (p + c)
+        torch.manual_seed(tseed)
+        chi_mat = torch.rand((len(edges) * 2, nc), dtype=torch.float64)
+        chi_mat = (chi_mat / torch.sum(chi_mat, axis=1, keepdims=True)).cuda()
+        chi_col = chi_mat.reshape(-1)
+        biases_i = torch.rand((n, 2), dtype=torch.float64)
+        biases_i = (biases_i / torch.sum(biases_i, axis=1, keepdims=True)).cuda()
+        s = (2 * (biases_i[:, 0] > biases_i[:, 1]).int() - 1)
+        t = 0
+        m_final = di.m(di.s_endstate(aux["N_nodes"], s, p, c))
+        while m_final < 1:
+            biases_chi = di.new_biases_chi(biases_i, aux["pos_biases"])
+            chi_col, chi_mat = di.HPr_dp(chi_mat, chi_col, biases_chi, aux["rho_D1"], aux["N_edg_pos_chi_mat"], d, p,
+                                         c, 1, 25 * n, 0.4)
+            marginals = di.marginals_comp(chi_mat, aux["pairs"], aux["pji"], aux["N_edges_pos"])
+            biases_i, s = di.new_biases_i(biases_i, 0.3, 0.1, marginals, t)
+            t += 1
+            m_final = 2 if t > TT else di.m(di.s_endstate(aux["N_nodes"], s, p, c))
+        assert t == full[f"{key}_num_steps"][0], key
+        if key in exact_ties:
+            continue
+        assert np.array_equal(s.cpu().numpy(), full[f"{key}_conf"][0]), key
