@@ -28,6 +28,7 @@ Secondary line items in the same JSON object:
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -401,6 +402,43 @@ def bench_hpr(args, rank, world, dist, dev):
            "marginals_bytes_per_iter": marg_bytes,
            "hpr_dp_traffic_bytes": rocprof_traffic("k_hpr_update_pipe"),
            "marginals_edge_z_traffic_bytes": rocprof_traffic("k_hpr_edge_z")}
+    # the loop's own state layout (HPRState layout="q", the default of hpr_run
+    # here): invalid-sender quadrants kept undecayed, read with the scale
+    st = mjx.HPRState(plan, p, c, chi, b, dtype=torch.float32, layout="q")
+    from mjx import _lib as L, _device as D
+    code, sptr, sz = L.MJX_F32, st._sc.data_ptr(), st._sc.element_size()
+    wp, wm = math.exp(-lmbd / n), math.exp(lmbd / n)
+    bufs = (st.chi, st.chi_b)
+
+    def run_q():
+        s_ = D.stream_handle()
+        e[0].record(stream)
+        for k in range(K):
+            L.call("mjx_hpr_update_q", code, bufs[k % 2].data_ptr(), bufs[1 - k % 2].data_ptr(), st.biases.data_ptr(),
+                   plan.nbr.data_ptr(), plan.in_row.data_ptr(), plan.out_row.data_ptr(), n, d, p, c, 1, wp, wm, 0.4,
+                   sptr, s_)
+        e[1].record(stream)
+        for k in range(K):
+            L.call("mjx_hpr_marginals_q", code, bufs[k % 2].data_ptr(), plan.out_row.data_ptr(), n, d, p, c, 1e-15,
+                   sptr + sz, st.zwork.data_ptr(), st.marg.data_ptr(), s_)
+        e[2].record(stream)
+
+    run_q()
+    el_q = _timed(run_q, dist, dev)
+    upd_q = e[0].elapsed_time(e[1]) / K
+    marg_q = e[1].elapsed_time(e[2]) / K
+    # per message: first half of its old row (damping) + the VV and IV quadrants
+    # of its incoming row + first half written, indices and biases
+    qbytes = msgs * (3 * (nc // 2) * 4 + 3 * 4 + 2 * 4)
+    res["loop_state_q"] = {
+        "layout": "decay-split (HPRState layout='q'): invalid-sender quadrants undecayed, read with (1-damp)^t",
+        "ms_per_iter": 1e3 * el_q / K, "iters_per_s": world * K / el_q, "messages_per_s": world * msgs * K / el_q,
+        "hpr_dp_ms": upd_q, "marginals_ms": marg_q, "hpr_dp_bytes_per_iter": qbytes,
+        "hpr_dp_algorithmic_GBps": qbytes / (upd_q / 1e3) / 1e9,
+        "hpr_dp_frac_of_hbm_peak": qbytes / (upd_q / 1e3) / 1e9 / HBM_PEAK_GBS,
+        "hpr_dp_traffic_bytes": rocprof_traffic("k_hpr_update_pipe_q"),
+        "marginals_edge_z_traffic_bytes": rocprof_traffic("k_hpr_edge_z_q")}
+    del st
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # the reference runs HPr_dp as torch ops; on the host that is torch's CPU
         # backend with every core: oracle/hpr_torch.py, the same DP in torch ops

@@ -245,6 +245,31 @@ int mjx_hpr_edge_z(int dtype, const void* chi, int64_t E, int p, int c, double e
  * idx[v] = a row whose source node is v; from biases_i: stride 2, half 1. */
 int mjx_hpr_node_biases(int dtype, const void* src, const int64_t* idx, int64_t stride, int64_t half,
                         int64_t n, void* out, void* stream);
+/* The decay-split layout of the HPR loop state.  HPr_dp writes nothing into the
+ * entries of a row whose sender trajectory is invalid (x_s[T-1] != attr_value):
+ * they are only damped, chi_t = (1-damp)^t chi_0 (code/HPR_pytorch_RRG.py:215).
+ * The loop state keeps each row as quadrants VV | VI | IV | II of (2^(T-1))^2
+ * entries (first letter: sender valid/invalid, second: receiver), entry
+ * (x_s, x_r) at quad*4^(T-1) + (x_s>>1)*2^(T-1) + (x_r>>1); the IV and II quadrants
+ * hold chi_0 undecayed and are read with the scale (1-damp)^t from device
+ * memory, so an update reads and writes only the first half of its own rows and
+ * the VV and IV quadrants of its incoming rows.
+ * mjx_hpr_q_supported: 1 if mjx_hpr_update_q runs this (dtype, d, p, c)
+ * (MJX_F32, p+c = 4, 2 <= d <= 4).  mjx_hpr_qlayout: to_q = 1: dst = src
+ * (reference layout) permuted; to_q = 0: dst = src (decay-split) in the reference
+ * layout with the invalid-sender entries times scale.  mjx_hpr_update_q: HPr_dp on
+ * the decay-split layout, *scale_in = chi_in's scale (dtype); chi_out's IV and II
+ * quadrants are not written (they must already hold chi_0).  mjx_hpr_marginals_q:
+ * marginals_comp of a decay-split chi with scale *scale. */
+int mjx_hpr_q_supported(int dtype, int d, int p, int c);
+int mjx_hpr_qlayout(int dtype, const void* src, void* dst, int64_t rows, int p, int c, int attr_value, int to_q,
+                    double scale, void* stream);
+int mjx_hpr_update_q(int dtype, const void* chi_in, void* chi_out, const void* biases, const int32_t* nbr,
+                     const int32_t* in_row, const int32_t* out_row, int64_t n, int d, int p, int c,
+                     int attr_value, double w_plus, double w_minus, double damp, const void* scale_in,
+                     void* stream);
+int mjx_hpr_marginals_q(int dtype, const void* chi, const int32_t* out_row, int64_t n, int d, int p, int c,
+                        double eps, const void* scale, void* zwork, void* marg, void* stream);
 
 /* ---- HPR on Erdos-Renyi graphs (the "general (ER)" HPR of code/README.md:1) -
  * HPr_dp with the degree taken per message: rows of degree class D (the

@@ -116,3 +116,74 @@ extern "C" int mjx_hpr_node_biases(int dtype, const void* src, const int64_t* id
     MJX_LAUNCH_CHECK("k_hpr_node_biases");
     return MJX_OK;
 }
+
+// ---- the decay-split layout of the HPR loop state (see mjx_hpr_impl.h) -------
+extern "C" int mjx_hpr_q_supported(int dtype, int d, int p, int c) {
+    return (dtype == MJX_F32 && q_supported(d, p, c)) ? 1 : 0;
+}
+
+extern "C" int mjx_hpr_qlayout(int dtype, const void* src, void* dst, int64_t rows, int p, int c, int attr_value,
+                               int to_q, double scale, void* stream) {
+    const int T = p + c;
+    if (rows < 0 || p < 1 || c < 1 || T > 6 || (attr_value != 1 && attr_value != -1) || src == dst) return MJX_EINVAL;
+    if (rows == 0) return MJX_OK;
+    if (!src || !dst) return MJX_EINVAL;
+    const int pv = attr_value > 0 ? 0 : 1;
+    hipStream_t st = as_stream(stream);
+    const unsigned grid = (unsigned)grid_for(rows << (2 * T), 8);
+    if (dtype == MJX_F32)
+        k_hpr_qperm<float><<<grid, 256, 0, st>>>((const float*)src, (float*)dst, rows, T, pv, to_q, (float)scale);
+    else if (dtype == MJX_F64)
+        k_hpr_qperm<double><<<grid, 256, 0, st>>>((const double*)src, (double*)dst, rows, T, pv, to_q, scale);
+    else
+        return MJX_EINVAL;
+    MJX_LAUNCH_CHECK("k_hpr_qperm");
+    return MJX_OK;
+}
+
+extern "C" int mjx_hpr_update_q(int dtype, const void* chi_in, void* chi_out, const void* biases, const int32_t* nbr,
+                                const int32_t* in_row, const int32_t* out_row, int64_t n, int d, int p, int c,
+                                int attr_value, double w_plus, double w_minus, double damp, const void* scale_in,
+                                void* stream) {
+    if (n < 1 || d < 2 || p < 1 || c < 1 || (attr_value != 1 && attr_value != -1)) return MJX_EINVAL;
+    if (!chi_in || !chi_out || !biases || !nbr || !in_row || !out_row || !scale_in || chi_in == chi_out)
+        return MJX_EINVAL;
+    if (dtype != MJX_F32) return MJX_ERANGE;
+    if (n * (int64_t)d > (int64_t)INT32_MAX) return MJX_ERANGE;
+    return update_q_f32(chi_in, chi_out, biases, nbr, in_row, out_row, n, d, p, c, attr_value > 0 ? 1 : 0, w_plus,
+                        w_minus, damp, (const float*)scale_in, as_stream(stream));
+}
+
+template <typename S>
+static int marginals_q_impl(const void* chi, const int32_t* out_row, int64_t n, int d, int T, double eps,
+                            const void* scale, void* zwork, void* marg, hipStream_t st) {
+    const int64_t E = n * (int64_t)d / 2;
+    S* zp = (S*)zwork;
+    S* zm = zp + 2 * E;
+#define MJX_EDGE_ZQ(TT)                                                                                  \
+    case TT: {                                                                                           \
+        auto k = k_hpr_edge_z_q<S, TT>;                                                                  \
+        const int64_t lanes = E * (1 << TT) / 2;                                                         \
+        k<<<resident_grid(k, 256, 0, lanes), 256, 0, st>>>((const S*)chi, E, (S)eps, (const S*)scale, zp, zm); \
+        break;                                                                                           \
+    }
+    switch (T) {
+        MJX_EDGE_ZQ(2) MJX_EDGE_ZQ(3) MJX_EDGE_ZQ(4) MJX_EDGE_ZQ(5)
+        default: return MJX_ERANGE;
+    }
+#undef MJX_EDGE_ZQ
+    MJX_LAUNCH_CHECK("k_hpr_edge_z_q");
+    k_hpr_node_marg<S><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(zp, zm, out_row, n, d, (S*)marg);
+    MJX_LAUNCH_CHECK("k_hpr_node_marg");
+    return MJX_OK;
+}
+
+extern "C" int mjx_hpr_marginals_q(int dtype, const void* chi, const int32_t* out_row, int64_t n, int d, int p, int c,
+                                   double eps, const void* scale, void* zwork, void* marg, void* stream) {
+    if (n < 1 || d < 1 || p < 1 || c < 1 || !chi || !out_row || !scale || !zwork || !marg) return MJX_EINVAL;
+    if ((n * (int64_t)d) % 2) return MJX_EINVAL;
+    hipStream_t st = as_stream(stream);
+    if (dtype == MJX_F32) return marginals_q_impl<float>(chi, out_row, n, d, p + c, eps, scale, zwork, marg, st);
+    if (dtype == MJX_F64) return marginals_q_impl<double>(chi, out_row, n, d, p + c, eps, scale, zwork, marg, st);
+    return MJX_EINVAL;
+}

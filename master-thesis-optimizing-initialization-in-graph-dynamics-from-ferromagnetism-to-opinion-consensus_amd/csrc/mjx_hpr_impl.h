@@ -148,10 +148,14 @@ template <int D>
 __device__ __forceinline__ int a_local_of(int lane) { return lane / D; }
 
 // HALF: the buffer holds only the valid-x_a half of each incoming row,
-// element x_k * 2^(T-1) + (x_a >> 1)
-template <typename S, int T, int P, int D, int XA, int RS = Cfg<S, T, P, D>::STRIDE, bool HALF = false>
+// element x_k * 2^(T-1) + (x_a >> 1).  QL (with HALF): the rows are in the
+// decay-split layout (qpos below) and the buffer holds their VV and IV
+// quadrants, element (x_k valid ? 0 : H^2) + (x_k >> 1) * H + (x_a >> 1), H =
+// 2^(T-1); the IV entries (x_k invalid) are stored undecayed and scaled by sc.
+template <typename S, int T, int P, int D, int XA, int RS = Cfg<S, T, P, D>::STRIDE, bool HALF = false,
+          bool QL = false>
 __device__ __forceinline__ S xa_messages(const S* __restrict__ rows, const S* __restrict__ bias, int a_local, int m,
-                                         S w, S (&out)[1 << T]) {
+                                         S w, S (&out)[1 << T], S sc = S(1)) {
     using C = Cfg<S, T, P, D>;
     using TB = Tabs<T, P, D, XA>;
     constexpr int X = C::X, K = C::K, BASE = C::BASE, NS = C::NS;
@@ -162,10 +166,22 @@ __device__ __forceinline__ S xa_messages(const S* __restrict__ rows, const S* __
     auto loadM = [&](int j, S (&Mj)[X]) {
         const int slot = a_local * D + (j < m ? j : j + 1);
         const S bp = bias[2 * slot], bm = bias[2 * slot + 1];
-        constexpr int CS = HALF ? X / 2 : X;          // stride between x_k
-        const S* r = rows + slot * RS + (HALF ? (XA >> 1) : XA);
+        if constexpr (QL) {
+            constexpr int H = X / 2;
+            const S* r = rows + slot * RS + (XA >> 1);
+            const S bps = bp * sc, bms = bm * sc;
 #pragma unroll
-        for (int x = 0; x < X; ++x) Mj[x] = (x < X / 2 ? bp : bm) * r[x * CS];
+            for (int x = 0; x < X; ++x) {
+                const bool valid = (x & 1) == (XA & 1);              // x_k[T-1] = attr, like x_a
+                const int e = (valid ? 0 : H * H) + (x >> 1) * H;
+                Mj[x] = (x < X / 2 ? (valid ? bp : bps) : (valid ? bm : bms)) * r[e];
+            }
+        } else {
+            constexpr int CS = HALF ? X / 2 : X;          // stride between x_k
+            const S* r = rows + slot * RS + (HALF ? (XA >> 1) : XA);
+#pragma unroll
+            for (int x = 0; x < X; ++x) Mj[x] = (x < X / 2 ? bp : bm) * r[x * CS];
+        }
     };
     // count table of the first K neighbours
     S tab[NS];
@@ -356,6 +372,24 @@ k_hpr_update(const S* __restrict__ chi_in, S* __restrict__ chi_out, const S* __r
     MJX_PROF_MARK(3);
 }
 
+// ---- decay-split message layout (the HPR loop's own state) --------------------
+// A row's entries with an invalid sender trajectory (x_s[T-1] != attr) are never
+// produced by HPr_dp: chi_new = 0 there, so the update only damps them,
+// chi_t = (1-damp)^t chi_0 (code/HPR_pytorch_RRG.py:215 with chi_mat2 = 0).  The
+// loop state therefore keeps every row as four quadrants of H^2 entries (H =
+// 2^(T-1); v/i = valid/invalid sender, then receiver):
+//   VV | VI | IV | II,   position qpos(x_s, x_r) = quad * H^2 + (x_s >> 1) * H + (x_r >> 1)
+// VV and VI (the first half) are rewritten by every update; IV and II keep the
+// undecayed chi_0 and are read with the scale (1-damp)^t (device memory, one
+// per iteration).  The update reads the old first half (damping), the VV and
+// IV quadrants of its incoming rows (x_a valid) and writes the first half: 1.5
+// instead of 3 KB per message at T = 4 fp32; the marginals weigh each product
+// by scale^(number of invalid senders) (k_hpr_edge_z_q).
+__host__ __device__ constexpr int qpos(int xs, int xr, int T, int pv) {
+    return ((((xs & 1) != pv) ? 2 : 0) + (((xr & 1) != pv) ? 1 : 0)) * (1 << (2 * T - 2)) +
+           (xs >> 1) * (1 << (T - 1)) + (xr >> 1);
+}
+
 // ---- software-pipelined form (fp32, T = 4: 1 KB message rows) ---------------
 // One persistent 512-thread workgroup per CU walks tiles t = blockIdx.x,
 // + gridDim.x, ...; wave w owns the valid x_a 2w(+1) (XPW = 1).  Everything a
@@ -400,13 +434,12 @@ __device__ __forceinline__ void glds4(const float* gsrc, uint32_t lds_byte_addr)
                  : "memory");
 }
 
-template <int T, int P, int D>
-__global__ void __launch_bounds__(512) k_hpr_update_pipe(const float* __restrict__ chi_in, float* __restrict__ chi_out,
-                                                          const float* __restrict__ biases,
-                                                          const int32_t* __restrict__ nbr,
-                                                          const int32_t* __restrict__ in_row,
-                                                          const int32_t* __restrict__ out_row, int64_t n,
-                                                          int attr_plus, float w_plus, float w_minus, float damp) {
+template <int T, int P, int D, bool QL>
+__device__ __forceinline__ void hpr_update_pipe(const float* __restrict__ chi_in, float* __restrict__ chi_out,
+                                                const float* __restrict__ biases, const int32_t* __restrict__ nbr,
+                                                const int32_t* __restrict__ in_row,
+                                                const int32_t* __restrict__ out_row, int64_t n, int attr_plus,
+                                                float w_plus, float w_minus, float damp, float sc) {
     using PC = PipeCfg<T, P, D>;
     constexpr int X = 1 << T, NC = X * X, NT = PC::NT, NL = PC::NL, NW = PC::NW, RPW = PC::RPW;
     static_assert(NC == 256, "pipelined HPR update: 1 KB rows (T = 4, fp32)");
@@ -446,17 +479,23 @@ __global__ void __launch_bounds__(512) k_hpr_update_pipe(const float* __restrict
         for (int k = 0; k < RPW; ++k) {
             if (ri[k] >= 0) {
                 const int slot = wave * RPW + k;
-                const float* src = chi_in + (int64_t)ri[k] * NC + hcol0;
                 const uint32_t dst = rows_lds + (uint32_t)((b * PC::BUF + (size_t)slot * PIPE_HRS) * sizeof(float));
-                glds4(src, dst);                                   // x_k 0..7
-                glds4(src + 8 * X, dst + 64 * sizeof(float));     // x_k 8..15
+                if (QL) {                                          // VV, IV quadrants: two 256-B runs
+                    const float* src = chi_in + (int64_t)ri[k] * NC + lane;
+                    glds4(src, dst);
+                    glds4(src + NC / 2, dst + 64 * sizeof(float));
+                } else {
+                    const float* src = chi_in + (int64_t)ri[k] * NC + hcol0;
+                    glds4(src, dst);                                   // x_k 0..7
+                    glds4(src + 8 * X, dst + 64 * sizeof(float));     // x_k 8..15
+                }
             }
         }
     };
     auto dma_old = [&](const int32_t (&ro)[RPW]) {                // whole old rows
 #pragma unroll
         for (int k = 0; k < RPW; ++k) {
-            if (ro[k] >= 0) {
+            if (ro[k] >= 0 && (!QL || lane < 32)) {                // QL: the first half only
                 const int slot = wave * RPW + k;
                 glds16(chi_in + (int64_t)ro[k] * NC + lane * 4,
                        old_lds + (uint32_t)((size_t)slot * PIPE_ORS * sizeof(float)));
@@ -523,10 +562,10 @@ __global__ void __launch_bounds__(512) k_hpr_update_pipe(const float* __restrict
                 if (wave == wv) {
                     constexpr int XP = 2 * wv, XM = 2 * wv + 1;
                     const float wgt0 = (XP < X / 2) ? w_plus : w_minus;
-                    if (attr_plus) rs = xa_messages<float, T, P, D, XP, PIPE_HRS, true>(rb, bb, a_local_of<D>(lane),
-                                                                                         lane % D, wgt0, out);
-                    else rs = xa_messages<float, T, P, D, XM, PIPE_HRS, true>(rb, bb, a_local_of<D>(lane), lane % D,
-                                                                               wgt0, out);
+                    if (attr_plus) rs = xa_messages<float, T, P, D, XP, PIPE_HRS, true, QL>(
+                                         rb, bb, a_local_of<D>(lane), lane % D, wgt0, out, sc);
+                    else rs = xa_messages<float, T, P, D, XM, PIPE_HRS, true, QL>(
+                                   rb, bb, a_local_of<D>(lane), lane % D, wgt0, out, sc);
                 }
             });
         }
@@ -542,6 +581,33 @@ __global__ void __launch_bounds__(512) k_hpr_update_pipe(const float* __restrict
             const float inv = 1.0f / tot;
             const float* ol = oldb + lane * PIPE_ORS;
             float* dst = chi_out + (int64_t)orow * NC;
+            if (QL) {
+                // row entries (x_a = this wave's valid sender, x_b): VV at q*8 + (x_b>>1)
+                // for valid x_b, VI at 64 + q*8 + (x_b>>1) for the others
+                constexpr int H = X / 2;
+#pragma unroll
+                for (int half = 0; half < 2; ++half) {
+                    const int base = half * H * H + q * H;
+#pragma unroll
+                    for (int k = 0; k < H / 4; ++k) {
+                        const float4 ov = *reinterpret_cast<const float4*>(ol + base + 4 * k);
+                        float o[4];
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const int j = 4 * k + e;                        // x_b >> 1
+                            // x_b = 2j + (valid ? pv : 1 - pv), pv = attr_plus ? 0 : 1
+                            const bool odd = (half == 0) != (attr_plus != 0);
+                            o[e] = odd ? out[2 * j + 1] : out[2 * j];
+                        }
+                        float4 v;
+                        v.x = damp * (o[0] * inv) + keep * ov.x;
+                        v.y = damp * (o[1] * inv) + keep * ov.y;
+                        v.z = damp * (o[2] * inv) + keep * ov.z;
+                        v.w = damp * (o[3] * inv) + keep * ov.w;
+                        *reinterpret_cast<float4*>(dst + base + 4 * k) = v;
+                    }
+                }
+            } else {
 #pragma unroll
             for (int k = 0; k < X / 4; ++k) {
                 const float4 ov = *reinterpret_cast<const float4*>(ol + cv + 4 * k);
@@ -558,6 +624,7 @@ __global__ void __launch_bounds__(512) k_hpr_update_pipe(const float* __restrict
                 *reinterpret_cast<float4*>(dst + cv + 4 * k) = v;
                 *reinterpret_cast<float4*>(dst + ci + 4 * k) = z;
             }
+            }
         }
         if (wave == 0 && lane < NL) {              // next tile's biases (buffer 1-b)
             bias[(1 - b) * NL * 2 + 2 * lane] = nbp;
@@ -568,6 +635,31 @@ __global__ void __launch_bounds__(512) k_hpr_update_pipe(const float* __restrict
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
     }
+}
+
+template <int T, int P, int D>
+__global__ void __launch_bounds__(512) k_hpr_update_pipe(const float* __restrict__ chi_in, float* __restrict__ chi_out,
+                                                          const float* __restrict__ biases,
+                                                          const int32_t* __restrict__ nbr,
+                                                          const int32_t* __restrict__ in_row,
+                                                          const int32_t* __restrict__ out_row, int64_t n,
+                                                          int attr_plus, float w_plus, float w_minus, float damp) {
+    hpr_update_pipe<T, P, D, false>(chi_in, chi_out, biases, nbr, in_row, out_row, n, attr_plus, w_plus, w_minus,
+                                    damp, 1.0f);
+}
+
+// the decay-split layout; scale_in = decay of chi_in's IV quadrants
+template <int T, int P, int D>
+__global__ void __launch_bounds__(512) k_hpr_update_pipe_q(const float* __restrict__ chi_in,
+                                                            float* __restrict__ chi_out,
+                                                            const float* __restrict__ biases,
+                                                            const int32_t* __restrict__ nbr,
+                                                            const int32_t* __restrict__ in_row,
+                                                            const int32_t* __restrict__ out_row, int64_t n,
+                                                            int attr_plus, float w_plus, float w_minus, float damp,
+                                                            const float* __restrict__ scale_in) {
+    hpr_update_pipe<T, P, D, true>(chi_in, chi_out, biases, nbr, in_row, out_row, n, attr_plus, w_plus, w_minus,
+                                   damp, *scale_in);
 }
 
 // ---- marginals (code/HPR_pytorch_RRG.py:147-167) ---------------------------
@@ -640,6 +732,96 @@ __global__ void __launch_bounds__(256) k_hpr_edge_z(const S* __restrict__ chi, i
                 zp[r + E] = bp / sb; zm[r + E] = bm / sb;
             }
         }
+    }
+}
+
+// the same Z sums over rows in the decay-split layout: entry j of row r is
+// (x_u, x_v) = (sender, receiver) of quadrant j / H^2, its transposed partner
+// in row r+E sits in the quadrant with the two validity bits swapped, and a
+// product carries scale^(number of invalid senders) (IV / II entries are
+// stored undecayed).  Z+ by x_u[0] = +1 <=> (x_u >> 1) < H/2.
+template <typename S, int T>
+__global__ void __launch_bounds__(256) k_hpr_edge_z_q(const S* __restrict__ chi, int64_t E, S eps,
+                                                       const S* __restrict__ scale, S* __restrict__ zp,
+                                                       S* __restrict__ zm) {
+    constexpr int X = 1 << T, NC = X * X, H = X / 2, HH = H * H;
+    using V = typename Vec16<S>::T;
+    constexpr int VN = Vec16<S>::N;
+    constexpr int G = X < 64 ? X : 64;               // lanes per edge
+    constexpr int NV = NC / (VN * G);                // 16-B pieces per lane per row
+    constexpr int EPW = 64 / G;                      // edges per wave instruction
+    constexpr int U = 2;                             // edge groups in flight per lane
+    const S s1 = *scale, s2 = s1 * s1;
+    const int lane = threadIdx.x & 63;
+    const int g = lane / G, l = lane % G;
+    const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * 256) >> 6;
+    for (int64_t base = wave * EPW * U; base < E; base += nwaves * EPW * U) {
+        S f[U][NV][VN], b[U][NV][VN];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t r = base + u * EPW + g;
+            const int64_t rr = r < E ? r : E - 1;            // branch-free loads
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                const int j0 = (v * G + l) * VN;
+                const V x = *reinterpret_cast<const V*>(chi + rr * NC + j0);
+                const S* xs = reinterpret_cast<const S*>(&x);
+#pragma unroll
+                for (int e = 0; e < VN; ++e) {
+                    const int j = j0 + e, q = j / HH, w = j % HH;
+                    const int jt = (((q & 1) << 1) | (q >> 1)) * HH + (w % H) * H + w / H;
+                    f[u][v][e] = xs[e];
+                    b[u][v][e] = chi[(rr + E) * NC + jt];
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t r = base + u * EPW + g;
+            S sp = 0, sm = 0, bp = 0, bm = 0;            // by x_u[0], by x_v[0]
+#pragma unroll
+            for (int v = 0; v < NV; ++v)
+#pragma unroll
+                for (int e = 0; e < VN; ++e) {
+                    const int j = (v * G + l) * VN + e, q = j / HH, w = j % HH;
+                    const S fac = q == 0 ? S(1) : (q == 3 ? s2 : s1);
+                    const S z = fac * (f[u][v][e] * b[u][v][e]);
+                    if (w / H < H / 2) sp += z; else sm += z;
+                    if (w % H < H / 2) bp += z; else bm += z;
+                }
+#pragma unroll
+            for (int off = G / 2; off > 0; off >>= 1) {
+                sp += __shfl_xor(sp, off, 64);
+                sm += __shfl_xor(sm, off, 64);
+                bp += __shfl_xor(bp, off, 64);
+                bm += __shfl_xor(bm, off, 64);
+            }
+            if (l == 0 && r < E) {
+                S fp = sp > eps ? sp : eps, fm = sm > eps ? sm : eps;
+                bp = bp > eps ? bp : eps; bm = bm > eps ? bm : eps;
+                const S sf = fp + fm, sb = bp + bm;
+                zp[r] = fp / sf; zm[r] = fm / sf;
+                zp[r + E] = bp / sb; zm[r + E] = bm / sb;
+            }
+        }
+    }
+}
+
+// reference layout <-> decay-split layout (to_q: dst = permuted src; else dst =
+// src un-permuted with the sender-invalid entries scaled)
+template <typename S>
+__global__ void k_hpr_qperm(const S* __restrict__ src, S* __restrict__ dst, int64_t rows, int T, int pv, int to_q,
+                            S scale) {
+    const int X = 1 << T, NC = X * X;
+    const int64_t total = rows * NC;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / NC;
+        const int col = (int)(i - r * NC), xs = col / X, xr = col % X;
+        const int64_t qi = r * NC + qpos(xs, xr, T, pv);
+        if (to_q) dst[qi] = src[i];
+        else dst[i] = ((xs & 1) != pv) ? src[qi] * scale : src[qi];
     }
 }
 
@@ -729,6 +911,36 @@ static int launch_update(const void* chi_in, void* chi_out, const void* biases, 
     }
 }
 
+// the decay-split update (fp32, T = 4, register table: d <= 4)
+template <int T, int P, int D>
+static int launch_update_q(const void* chi_in, void* chi_out, const void* biases, const int32_t* nbr,
+                           const int32_t* in_row, const int32_t* out_row, int64_t n, int attr_plus, double w_plus,
+                           double w_minus, double damp, const float* scale_in, hipStream_t st) {
+    using C = Cfg<float, T, P, D>;
+    using PC = PipeCfg<T, P, D>;
+    if constexpr (T != 4 || C::NS > 128 || PC::LDS > 160 * 1024) {
+        return MJX_ERANGE;
+    } else {
+        const int64_t tiles = (n + C::NT - 1) / C::NT;
+        if (tiles > INT32_MAX) return MJX_ERANGE;
+        auto pk = k_hpr_update_pipe_q<T, P, D>;
+        static bool pattr = false;
+        if (!pattr) {
+            MJX_HIP(hipFuncSetAttribute((const void*)pk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)PC::LDS),
+                    "hpr pipe q set lds");
+            pattr = true;
+        }
+        const int per = resident_blocks_per_cu((const void*)pk, 512, PC::LDS);
+        int64_t grid = (int64_t)kCUs * (per > 0 ? per : 1);
+        if (grid > tiles) grid = tiles;
+        pk<<<(unsigned)grid, 512, PC::LDS, st>>>((const float*)chi_in, (float*)chi_out, (const float*)biases, nbr,
+                                                 in_row, out_row, n, attr_plus, (float)w_plus, (float)w_minus,
+                                                 (float)damp, scale_in);
+        MJX_LAUNCH_CHECK("k_hpr_update_pipe<q>");
+        return MJX_OK;
+    }
+}
+
 template <typename S, int T, int P>
 static int dispatch_d(int d, const void* ci, void* co, const void* b, const int32_t* nb, const int32_t* ir,
                       const int32_t* orr, int64_t n, int ap, double wp, double wm, double dp, hipStream_t st) {
@@ -754,7 +966,12 @@ static int dispatch_tp(int p, int c, int d, const void* ci, void* co, const void
     return MJX_ERANGE;
 }
 
+inline bool q_supported(int d, int p, int c) { return p >= 1 && c >= 1 && p + c == 4 && d >= 2 && d <= 4; }
+
 // per-dtype instantiation units (mjx_hpr_f32.hip, mjx_hpr_f64.hip)
+int update_q_f32(const void* ci, void* co, const void* b, const int32_t* nb, const int32_t* ir, const int32_t* orr,
+                 int64_t n, int d, int p, int c, int ap, double wp, double wm, double dp, const float* sc,
+                 hipStream_t st);
 int update_f32(const void* ci, void* co, const void* b, const int32_t* nb, const int32_t* ir, const int32_t* orr,
                int64_t n, int d, int p, int c, int ap, double wp, double wm, double dp, hipStream_t st);
 int update_f64(const void* ci, void* co, const void* b, const int32_t* nb, const int32_t* ir, const int32_t* orr,

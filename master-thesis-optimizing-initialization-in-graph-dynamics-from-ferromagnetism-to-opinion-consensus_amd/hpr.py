@@ -176,17 +176,40 @@ def new_biases_i(biases_i, pie, gamma, marginals, t, u=None, generator=None, s_o
 
 class HPRState:
     """Device buffers of one HPR run; ``step`` is one iteration of the main loop
-    (code/HPR_pytorch_RRG.py:345-356) and returns sum(s_endstate(s))."""
+    (code/HPR_pytorch_RRG.py:345-356) and returns sum(s_endstate(s)).
+
+    ``layout``: "ref" keeps the messages in the reference's (2E, 4^T) layout;
+    "q" (the default where the library has it: fp32, p+c = 4, d <= 4) keeps
+    them in the decay-split layout (mjx_hpr_impl.h): the entries with an
+    invalid sender trajectory, which HPr_dp only damps ((1-damp)^t chi_0,
+    :215), stay undecayed and are read with the scale, so an update moves 1.5
+    instead of 3 KB per message.  ``messages()`` returns the reference layout
+    either way."""
 
     def __init__(self, plan, p, c, chi0, biases0, dtype=torch.float32, damppar=0.4, attr_value=1,
-                 lmbd_in=None, pie=0.3, gamma=0.1):
+                 lmbd_in=None, pie=0.3, gamma=0.1, layout=None):
         self.plan, self.p, self.c = plan, int(p), int(c)
         self.dtype = dtype
         self.damppar, self.attr_value = float(damppar), int(attr_value)
         self.lmbd_in = 25 * plan.n if lmbd_in is None else lmbd_in
         self.pie, self.gamma = float(pie), float(gamma)
-        self.chi = _device.to_device(chi0, dtype=dtype)
-        self.chi_b = torch.empty_like(self.chi)
+        q_ok = _lib.load().mjx_hpr_q_supported(_code(dtype), plan.d, self.p, self.c) == 1
+        if layout is None:
+            layout = "q" if q_ok else "ref"
+        if layout not in ("q", "ref") or (layout == "q" and not q_ok):
+            raise _lib.MjxError(f"HPR state layout {layout!r} not available for dtype={dtype}, d={plan.d}, "
+                                f"p={p}, c={c}")
+        self.layout = layout
+        chi0 = _device.to_device(chi0, dtype=dtype)
+        if layout == "q":
+            self.chi = torch.empty_like(chi0)
+            _lib.call("mjx_hpr_qlayout", _code(dtype), _device.ptr(chi0), _device.ptr(self.chi), chi0.shape[0],
+                      self.p, self.c, self.attr_value, 1, 1.0, _device.stream_handle())
+            self.chi_b = self.chi.clone()        # both buffers carry chi_0's invalid-sender quadrants
+            self._sc = torch.ones(2, dtype=dtype, device=chi0.device)
+        else:
+            self.chi = chi0
+            self.chi_b = torch.empty_like(self.chi)
         self.biases = _device.to_device(biases0, dtype=dtype).clone()
         dev = self.chi.device
         self.zwork = torch.empty(4 * plan.E, dtype=dtype, device=dev)
@@ -194,6 +217,7 @@ class HPRState:
         self.s = torch.empty(plan.n, dtype=torch.int32, device=dev)
         self.cnt = torch.zeros(1, dtype=torch.int64, device=dev)
         self.t = 0
+        self._t0 = 0
 
     def s_from_biases(self):
         """s = 2*(b0 > b1) - 1 (code/HPR_pytorch_RRG.py:337-338): the bias kernel
@@ -211,12 +235,45 @@ class HPRState:
         rollout(self.plan.graph, bits, self.p + self.c - 1, counts=self.cnt)
         return 2 * int(self.cnt.item()) - self.plan.n
 
+    def decay(self, t):
+        """(1-damp)^(t - t0): the scale of the invalid-sender quadrants after
+        iteration t (t0 = the iteration the state was built at)."""
+        return (1.0 - self.damppar) ** (t - self._t0)
+
+    def messages(self):
+        """The current messages in the reference's (2E, 4^T) layout."""
+        if self.layout == "ref":
+            return self.chi
+        out = torch.empty_like(self.chi)
+        _lib.call("mjx_hpr_qlayout", _code(self.dtype), _device.ptr(self.chi), _device.ptr(out), self.chi.shape[0],
+                  self.p, self.c, self.attr_value, 0, self.decay(self.t), _device.stream_handle())
+        return out
+
+    def _update(self, src, dst, sc_in=None, sc_out=None):
+        """HPr_dp src -> dst and marginals_comp(dst) (scales: device pointers,
+        decay-split layout)."""
+        st = _device.stream_handle()
+        if self.layout == "q":
+            plan = self.plan
+            wp, wm = _weights(self.lmbd_in, plan.n)
+            _lib.call("mjx_hpr_update_q", _code(self.dtype), _device.ptr(src), _device.ptr(dst),
+                      _device.ptr(self.biases), _device.ptr(plan.nbr), _device.ptr(plan.in_row),
+                      _device.ptr(plan.out_row), plan.n, plan.d, self.p, self.c, self.attr_value, wp, wm,
+                      self.damppar, sc_in, st)
+            _lib.call("mjx_hpr_marginals_q", _code(self.dtype), _device.ptr(dst), _device.ptr(plan.out_row), plan.n,
+                      plan.d, self.p, self.c, 1e-15, sc_out, _device.ptr(self.zwork), _device.ptr(self.marg), st)
+        else:
+            HPr_dp(src, self.biases, self.plan, self.p, self.c, self.attr_value, self.lmbd_in, self.damppar, out=dst)
+            marginals_comp(dst, self.plan, self.p, self.c, zwork=self.zwork, out=self.marg)
+
     def step(self, u=None, generator=None):
-        HPr_dp(self.chi, self.biases, self.plan, self.p, self.c, self.attr_value, self.lmbd_in, self.damppar,
-               out=self.chi_b)
+        if self.layout == "q":
+            self._sc.copy_(torch.tensor([self.decay(self.t), self.decay(self.t + 1)], dtype=self.dtype))
+            self._update(self.chi, self.chi_b, self._sc.data_ptr(), self._sc.data_ptr() + self._sc.element_size())
+        else:
+            self._update(self.chi, self.chi_b)
         self.chi, self.chi_b = self.chi_b, self.chi
         self._graph = None                   # a captured batch holds the old buffer roles
-        marginals_comp(self.chi, self.plan, self.p, self.c, zwork=self.zwork, out=self.marg)
         new_biases_i(self.biases, self.pie, self.gamma, self.marg, self.t, u=u, generator=generator, s_out=self.s)
         self.t += 1
         return self.sum_end()
@@ -229,6 +286,7 @@ class HPRState:
             self._u = torch.empty((k, n), dtype=torch.float64, device=dev)
             self._s_hist = torch.empty((k, n), dtype=torch.int32, device=dev)
             self._cnt = torch.zeros(k, dtype=torch.int64, device=dev)
+            self._scales = torch.ones(k + 1, dtype=self.dtype, device=dev)
             self._bits = torch.empty((n + 63) // 64, dtype=torch.int64, device=dev)
             self._rtmp = (torch.empty_like(self._bits), torch.empty_like(self._bits))
             self._graph = None
@@ -242,10 +300,11 @@ class HPRState:
         to row j of self._s_hist and sum(s_endstate(s)) to self._cnt[j]."""
         n, T, st = self.plan.n, self.p + self.c - 1, _device.stream_handle()
         self._cnt.zero_()
+        sz = self._scales.element_size()
         for j in range(k):
             src, dst = (self.chi, self.chi_b) if j % 2 == 0 else (self.chi_b, self.chi)
-            HPr_dp(src, self.biases, self.plan, self.p, self.c, self.attr_value, self.lmbd_in, self.damppar, out=dst)
-            marginals_comp(dst, self.plan, self.p, self.c, zwork=self.zwork, out=self.marg)
+            # decay-split layout: row j of self._scales is (1-damp)^(t+j), set before each replay
+            self._update(src, dst, self._scales.data_ptr() + j * sz, self._scales.data_ptr() + (j + 1) * sz)
             _lib.call("mjx_hpr_new_biases", _code(self.dtype), _device.ptr(self.biases), _device.ptr(self.marg),
                       _device.ptr(self._u[j]), 0.5, self.pie, n, _device.ptr(self._s_hist[j]), st)
             _lib.call("mjx_pack_np", _device.ptr(self._s_hist[j]), _lib.MJX_I32, n, _device.ptr(self._bits), st)
@@ -277,6 +336,8 @@ class HPRState:
             thresh = 1 - (1 + (self.t + j)) ** (-self.gamma)            # code/HPR_pytorch_RRG.py:142
             sel[j] = torch.where(u < thresh, 0.0, 1.0)                  # kernel: refresh iff sel < 0.5
         self._u.copy_(sel)
+        if self.layout == "q":
+            self._scales.copy_(torch.tensor([self.decay(self.t + j) for j in range(k + 1)], dtype=self.dtype))
         if graph and self._graph is not None:
             self._graph.replay()
         elif graph and getattr(self, "_warm", False):
@@ -293,7 +354,8 @@ class HPRState:
 
 
 def hpr_run(d, n, p, c, damppar=0.4, attr_value=1, lmbd_in=None, pie=0.3, gamma=0.1, TT=10000, edges=None,
-            nbrs=None, seed=0, dtype=torch.float32, chi0=None, biases0=None, generator=None, batch=16, graph=True):
+            nbrs=None, seed=0, dtype=torch.float32, chi0=None, biases0=None, generator=None, batch=16, graph=True,
+            layout=None):
     """The HPR experiment of code/HPR_pytorch_RRG.py:224-377 for one graph.
 
     Randomness follows the reference: with ``generator`` a torch CPU generator
@@ -303,6 +365,7 @@ def hpr_run(d, n, p, c, damppar=0.4, attr_value=1, lmbd_in=None, pie=0.3, gamma=
     loop runs in device batches of ``batch`` iterations (one host read each,
     replayed as a hipGraph with ``graph``); on return the generator has made
     exactly the draws the reference makes up to its stop iteration.
+    ``layout``: the message state's layout (HPRState).
     Returns the np.savez keys of :377 (mag_reached, conf, num_steps, graphs).
     """
     from .graph import random_regular_edges
@@ -319,7 +382,7 @@ def hpr_run(d, n, p, c, damppar=0.4, attr_value=1, lmbd_in=None, pie=0.3, gamma=
         biases0 = torch.rand((n, 2), dtype=torch.float64, generator=generator)
         biases0 = biases0 / torch.sum(biases0, axis=1, keepdims=True)
     st = HPRState(plan, p, c, chi0, biases0, dtype=dtype, damppar=damppar, attr_value=attr_value,
-                  lmbd_in=lmbd_in, pie=pie, gamma=gamma)
+                  lmbd_in=lmbd_in, pie=pie, gamma=gamma, layout=layout)
     st.s_from_biases()
     total = st.sum_end()
     m_final = total / n

@@ -69,7 +69,7 @@ def test_hpr_loop_state_chain(mjx_mod, name):
                           gamma=float(z["gamma"]))
     for k in range(int(z["chain"])):
         tot = st.step(u=z[f"it{k}_u"])
-        assert rownorm_err(st.chi.cpu().numpy(), z[f"it{k}_chi"]) < 1e-12
+        assert rownorm_err(st.messages().cpu().numpy(), z[f"it{k}_chi"]) < 1e-12
         assert np.array_equal(st.s.cpu().numpy(), z[f"it{k}_s"])
         assert tot / n == float(z[f"it{k}_m_end"])
 
