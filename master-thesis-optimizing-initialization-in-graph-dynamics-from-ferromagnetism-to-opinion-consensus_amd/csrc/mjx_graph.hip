@@ -326,13 +326,11 @@ extern "C" int mjx_graph_check_ell(const int32_t* adj, int64_t n, int d, unsigne
 //
 // Plan (sizes from mjx_binned_plan_shape):
 //   src_lo uint16[src_len]   phase-1 order; segment starts padded to 8 slots,
-//                            block starts to 256 slots
-//                            and every 256-slot chunk stored lane-transposed
-//                            (slot r of chunk c at 256c + 4*(r&63) + (r>>6)), so
-//                            one 8-B load per lane gives a wave the low parts of
-//                            four whole message words;
-//   src_hi uint16[src_len/4] the four high nibbles of lane l of chunk c in
-//                            entry 64c + l (nibble k = slot 64k + l);
+//                            block starts to 256 slots: slot j's source offset
+//                            (20 bits within its block) >> 4, i.e. the index of
+//                            the 16-bit state word that holds its bit;
+//   src_hi uint16[src_len/4] the bit within that word (offset & 15) of slots
+//                            4i..4i+3 in entry i (nibble k = slot 4i+k);
 //   off   uint16[off_len] phase-2 order; segment starts padded to 8 slots;
 //   index int64           blk[K+1]  phase-1 padded block starts |
 //                         p1T[S]    phase-1 start of segment (b,t), at t*K+b |
@@ -374,7 +372,6 @@ inline Shape shape(int64_t n, int d, int64_t rows) {
     return s;
 }
 
-__host__ __device__ inline int64_t p1pos(int64_t j) { return (j & ~255ll) | ((j & 63) << 2) | ((j >> 6) & 3); }
 
 // ---- plan construction (setup, once per graph) ------------------------------
 
@@ -462,67 +459,66 @@ __global__ void __launch_bounds__(256) k_bin_fill(const int32_t* __restrict__ ad
         if (u < 0 || u >= n) continue;
         const int64_t b = u >> kSrcShift;
         const unsigned r = atomicAdd(&cur[b], 1u);
-        src[p1pos(p1[b * T + t] + r)] = (int32_t)(u & (kSrc - 1));
+        src[p1[b * T + t] + r] = (int32_t)(u & (kSrc - 1));
         off[(p2[t * K + b] & ~7ll) + r] = (uint16_t)(q / d - t * kTile);
     }
 }
 
-// int32 source offsets (20 bits) -> 16-bit low parts + 4-bit high parts
+// int32 source offsets (20 bits) -> 16-bit state-word indices + 4-bit bit positions
 __global__ void k_bin_pack(const int32_t* __restrict__ src32, int64_t chunks, uint16_t* __restrict__ lo,
                            uint16_t* __restrict__ hi) {
-    const int64_t lanes = chunks * 64;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < lanes; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t quads = chunks * 64;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < quads; i += (int64_t)gridDim.x * blockDim.x) {
         const int4 x = reinterpret_cast<const int4*>(src32)[i];
         uint2 l;
-        l.x = ((unsigned)x.x & 0xffffu) | (((unsigned)x.y & 0xffffu) << 16);
-        l.y = ((unsigned)x.z & 0xffffu) | (((unsigned)x.w & 0xffffu) << 16);
+        l.x = ((unsigned)x.x >> 4) | (((unsigned)x.y >> 4) << 16);
+        l.y = ((unsigned)x.z >> 4) | (((unsigned)x.w >> 4) << 16);
         reinterpret_cast<uint2*>(lo)[i] = l;
-        hi[i] = (uint16_t)((((unsigned)x.x >> 16) & 15u) | ((((unsigned)x.y >> 16) & 15u) << 4) |
-                           ((((unsigned)x.z >> 16) & 15u) << 8) | ((((unsigned)x.w >> 16) & 15u) << 12));
+        hi[i] = (uint16_t)(((unsigned)x.x & 15u) | (((unsigned)x.y & 15u) << 4) | (((unsigned)x.z & 15u) << 8) |
+                           (((unsigned)x.w & 15u) << 12));
     }
 }
 
 // ---- the sweep ----------------------------------------------------------------
 
-__device__ __forceinline__ bool state_bit(const uint32_t* sb, int32_t u) {
-    return (sb[(u & (int32_t)(kSrc - 1)) >> 5] >> (u & 31)) & 1u;
-}
-
-__device__ __forceinline__ int4 unpack_src(uint2 l, unsigned h) {
-    return make_int4((int)((l.x & 0xffffu) | ((h & 15u) << 16)), (int)((l.x >> 16) | (((h >> 4) & 15u) << 16)),
-                     (int)((l.y & 0xffffu) | (((h >> 8) & 15u) << 16)), (int)((l.y >> 16) | (((h >> 12) & 15u) << 16)));
-}
-
-// UC chunks of a wave's phase-1 stream: lane l's four source offsets of each
+// UC chunks of a wave's phase-1 stream: lane l holds slots 4l..4l+3 of each
 template <int UC>
 struct MsgGroup {
     static constexpr int NW = kMsgThreads / 64;
-    uint2 l[UC];
-    unsigned h[UC];
-    // chunks c, c + NW, ... (clamped to the wave's last chunk: always a valid load)
+    uint2 l[UC];       // four 16-bit state-word indices
+    unsigned h[UC];    // four 4-bit bit positions
+    // chunks c, c + NW, ... (clamped to the wave's last chunk: always a valid
+    // load); c and last are wave-uniform, so every address is a scalar base
+    // plus the lane's constant offset
     __device__ __forceinline__ void fetch(const uint2* __restrict__ lo2, const uint16_t* __restrict__ src_hi,
                                           int64_t c, int64_t last, int lane) {
 #pragma unroll
         for (int u = 0; u < UC; ++u) {
             const int64_t cc = (c + u * NW <= last) ? c + u * NW : last;
-            l[u] = lo2[cc * 64 + lane];
-            h[u] = src_hi[cc * 64 + lane];
+            const uint2* pl = lo2 + cc * 64;
+            const uint16_t* ph = src_hi + cc * 64;
+            l[u] = pl[lane];
+            h[u] = ph[lane];
         }
     }
-    // the message words of chunks c, c + NW, ... below a1
-    __device__ __forceinline__ void emit(const uint32_t* sb, int64_t c, int64_t a1, int lane,
-                                         u64* __restrict__ msg) const {
-        u64 mine = 0;
+    // message bits of chunks c, c + NW, ... below a1: lane l's four bits are
+    // bits 4l..4l+3 of its chunk, so three DPP row shifts assemble 32-bit
+    // words in lanes 0, 8, .., 56 (no ballots, no lane selects)
+    __device__ __forceinline__ void emit(const uint16_t* sb16, int64_t c, int64_t a1, int lane,
+                                         uint32_t* __restrict__ msg32) const {
 #pragma unroll
         for (int u = 0; u < UC; ++u) {
-            const int4 x = unpack_src(l[u], h[u]);
-            const u64 w0 = __ballot(state_bit(sb, x.x)), w1 = __ballot(state_bit(sb, x.y));
-            const u64 w2 = __ballot(state_bit(sb, x.z)), w3 = __ballot(state_bit(sb, x.w));
-            if ((lane >> 2) == u) mine = (lane & 2) ? ((lane & 1) ? w3 : w2) : ((lane & 1) ? w1 : w0);
-        }
-        if (lane < 4 * UC) {
-            const int64_t cc = c + (lane >> 2) * NW;
-            if (cc < a1) msg[cc * 4 + (lane & 3)] = mine;
+            const unsigned x = l[u].x, y = l[u].y, hh = h[u];
+            const unsigned v0 = sb16[x & 0xffffu], v1 = sb16[x >> 16];
+            const unsigned v2 = sb16[y & 0xffffu], v3 = sb16[y >> 16];
+            unsigned m = __builtin_amdgcn_ubfe(v0, hh & 15u, 1) | (__builtin_amdgcn_ubfe(v1, (hh >> 4) & 15u, 1) << 1) |
+                         (__builtin_amdgcn_ubfe(v2, (hh >> 8) & 15u, 1) << 2) | (__builtin_amdgcn_ubfe(v3, hh >> 12, 1) << 3);
+            // row_shl:k (dpp_ctrl 0x100 + k): lane i reads lane i + k of its 16-lane row
+            m |= (unsigned)__builtin_amdgcn_mov_dpp((int)m, 0x101, 0xf, 0xf, true) << 4;
+            m |= (unsigned)__builtin_amdgcn_mov_dpp((int)m, 0x102, 0xf, 0xf, true) << 8;
+            m |= (unsigned)__builtin_amdgcn_mov_dpp((int)m, 0x104, 0xf, 0xf, true) << 16;
+            const int64_t cc = c + u * NW;
+            if ((lane & 7) == 0 && cc < a1) msg32[cc * 8 + (lane >> 3)] = m;
         }
     }
 };
@@ -566,21 +562,25 @@ __global__ void __launch_bounds__(kMsgThreads) k_bin_msg(const uint16_t* __restr
     const int64_t a0 = c0 + part * per;
     const int64_t a1 = (a0 + per < c1) ? a0 + per : c1;
     constexpr int NW = kMsgThreads / 64;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint2* lo2 = reinterpret_cast<const uint2*>(src_lo);
-    // this wave's chunks: a0 + wave + NW*i; lane 4u+k stores message word k of chunk u
+    // this wave's chunks: a0 + wave + NW*i
     const int64_t last = (a1 - 1 - a0 - wave >= 0) ? a0 + wave + ((a1 - 1 - a0 - wave) / NW) * NW : -1;
+    const uint16_t* sb16 = reinterpret_cast<const uint16_t*>(sb);
+    uint32_t* msg32 = reinterpret_cast<uint32_t*>(msg);
     // two groups in flight: the loads of group i+1 are issued before the
     // lookups of group i (unrolled by two, so no register copies wait on them);
-    // 3.40 -> 3.35 ms per sweep at N=1e9, d=6 (UC 2: 3.53, UC 8: 3.37)
+    // 3.40 -> 3.35 ms per sweep at N=1e9, d=6 (UC 2: 3.53, UC 8: 3.37).  With
+    // the LDS lookups removed (timing build) the kernel takes the same time:
+    // it is bound by the stream, not by the lookups or the VALU work.
     if (last < 0) return;
     MsgGroup<UC> ga, gb;
     ga.fetch(lo2, src_hi, a0 + wave, last, lane);
     for (int64_t c = a0 + wave; c < a1; c += 2 * UC * NW) {
         gb.fetch(lo2, src_hi, c + UC * NW, last, lane);
-        ga.emit(sb, c, a1, lane, msg);
+        ga.emit(sb16, c, a1, lane, msg32);
         ga.fetch(lo2, src_hi, c + 2 * UC * NW, last, lane);
-        gb.emit(sb, c + UC * NW, a1, lane, msg);
+        gb.emit(sb16, c + UC * NW, a1, lane, msg32);
     }
 }
 
