@@ -4,7 +4,8 @@
 Runs, on cuda:0, exactly the bench.py sweep (d=4 RRG, N=1e6, R=4096
 replica-packed, 2 sweeps per rollout, fused count on the last one) a few
 times, then (unless --no-hpr) the C3 HPR iteration (d=4 RRG, N=1e5,
-p=c=2, fp32: HPr_dp + marginals_comp) and (unless --no-giant) a few sweeps
+p=c=2, fp32: HPr_dp + marginals_comp, in the reference layout and in the
+loop state's decay-split layout) and (unless --no-giant) a few sweeps
 of the C5 partitioned N=1e9 d=6 graph on one rank, preceded by a calibration copy of a known byte count (torch's
 vectorised copy, 16 B per lane) that tools/pmc_parse.py uses to check the
 gfx950 FETCH_SIZE correction (MI355X_MICROARCH.md, HBM section).
@@ -68,8 +69,12 @@ def main():
         for _ in range(args.reps):
             mjx.HPr_dp(chi, b, plan, p, c, 1, 25 * hn, 0.4, out=hout)
             mjx.marginals_comp(hout, plan, p, c, zwork=z, out=mg)
+        # the loop state's decay-split layout (HPRState layout="q")
+        st = mjx.HPRState(plan, p, c, chi, b, dtype=torch.float32, layout="q")
+        for k in range(args.reps):
+            st.step(u=torch.rand(hn, dtype=torch.float64, generator=torch.Generator().manual_seed(k)))
         torch.cuda.synchronize()
-        del chi, hout, plan
+        del chi, hout, plan, st
         print("pmc_run hpr done", flush=True)
     if not args.no_giant:
         sh = mjx.ShardedRRG(6, args.giant_n, seed=12345, mode="binned")
