@@ -420,7 +420,7 @@ def bench_hpr(args, rank, world, dist, dev):
         e[1].record(stream)
         for k in range(K):
             L.call("mjx_hpr_marginals_q", code, bufs[k % 2].data_ptr(), plan.out_row.data_ptr(), n, d, p, c, 1e-15,
-                   sptr + sz, st.zwork.data_ptr(), st.marg.data_ptr(), s_)
+                   sptr + sz, st._ii.data_ptr(), st.zwork.data_ptr(), st.marg.data_ptr(), s_)
         e[2].record(stream)
 
     run_q()
@@ -438,6 +438,29 @@ def bench_hpr(args, rank, world, dist, dev):
         "hpr_dp_frac_of_hbm_peak": qbytes / (upd_q / 1e3) / 1e9 / HBM_PEAK_GBS,
         "hpr_dp_traffic_bytes": rocprof_traffic("k_hpr_update_pipe_q"),
         "marginals_edge_z_traffic_bytes": rocprof_traffic("k_hpr_edge_z_q")}
+    # the whole loop iteration of code/HPR_pytorch_RRG.py:344-356 (update,
+    # marginals, bias refresh, trial configuration, majority check) in
+    # hipGraph-replayed batches of 16 with one host read per batch
+    gcpu = torch.Generator().manual_seed(args.seed + rank)
+    st.steps_batched(16, gcpu)                      # eager batch
+    st.steps_batched(16, gcpu)                      # capture + replay
+    nb = max(1, K // 4)
+    drawn = [st.draw_batch(16, gcpu)]
+
+    def run_loop():
+        # hpr_run's loop: the next batch's uniforms drawn on the host while
+        # this batch runs, one host read per batch
+        for _ in range(nb):
+            st.launch_batch(drawn[0])
+            drawn[0] = st.draw_batch(16, gcpu)
+            st.collect_batch()
+
+    el_loop = _timed(run_loop, dist, dev)
+    res["loop_state_q"]["loop_ms_per_iter"] = 1e3 * el_loop / (16 * nb)
+    res["loop_state_q"]["loop_note"] = ("hpr_run's loop in batches of 16: update + marginals + new_biases_i + "
+                                        "pack + p+c-1 sweeps + count per iteration on the device; the reference's "
+                                        "torch.rand(n) per iteration drawn on the host (CPU generator) while the "
+                                        "previous batch runs; one host read per batch")
     del st
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # the reference runs HPr_dp as torch ops; on the host that is torch's CPU

@@ -235,6 +235,10 @@ int mjx_hpr_marginals(int dtype, const void* chi, const int32_t* out_row, int64_
  * place and writes s[n] = +-1 (int32, nullable). */
 int mjx_hpr_new_biases(int dtype, void* biases, const void* marg, const double* u, double thresh,
                        double pie, int64_t n, int32_t* s, void* stream);
+/* The same with the comparison u_i < thresh made by the caller: refresh[n] (uint8,
+ * nonzero = refresh node i's biases). */
+int mjx_hpr_new_biases_mask(int dtype, void* biases, const void* marg, const uint8_t* refresh, double pie,
+                            int64_t n, int32_t* s, void* stream);
 /* The edge half of marginals_comp (code/HPR_pytorch_RRG.py:150-161) alone:
  * zwork[4E] = per-row normalised (Z+ [2E], Z- [2E]) of every directed row. */
 int mjx_hpr_edge_z(int dtype, const void* chi, int64_t E, int p, int c, double eps, void* zwork,
@@ -269,7 +273,12 @@ int mjx_hpr_update_q(int dtype, const void* chi_in, void* chi_out, const void* b
                      int attr_value, double w_plus, double w_minus, double damp, const void* scale_in,
                      void* stream);
 int mjx_hpr_marginals_q(int dtype, const void* chi, const int32_t* out_row, int64_t n, int d, int p, int c,
-                        double eps, const void* scale, void* zwork, void* marg, void* stream);
+                        double eps, const void* scale, const void* ii, void* zwork, void* marg, void* stream);
+/* ii[4E] (dtype): per edge the four sums of its II x II products (by x_u[0] = +1/-1,
+ * by x_v[0] = +1/-1), which never change: computed once from the loop state's
+ * chi_0 quadrants; mjx_hpr_marginals_q then skips reading the II quadrants
+ * (ii may be NULL: everything is read). */
+int mjx_hpr_q_ii(int dtype, const void* chi, int64_t E, int p, int c, void* ii, void* stream);
 
 /* ---- HPR on Erdos-Renyi graphs (the "general (ER)" HPR of code/README.md:1) -
  * HPr_dp with the degree taken per message: rows of degree class D (the

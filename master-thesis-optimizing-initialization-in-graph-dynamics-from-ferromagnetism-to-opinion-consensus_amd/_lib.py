@@ -50,13 +50,15 @@ SIGNATURES = {
                        c_dbl, c_dbl, c_dbl, c_vp],
     "mjx_hpr_marginals": [c_int, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_dbl, c_vp, c_vp, c_vp],
     "mjx_hpr_new_biases": [c_int, c_vp, c_vp, c_vp, c_dbl, c_dbl, c_i64, c_vp, c_vp],
+    "mjx_hpr_new_biases_mask": [c_int, c_vp, c_vp, c_vp, c_dbl, c_i64, c_vp, c_vp],
     "mjx_hpr_edge_z": [c_int, c_vp, c_i64, c_int, c_int, c_dbl, c_vp, c_vp],
     "mjx_hpr_node_biases": [c_int, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp],
     "mjx_hpr_q_supported": [c_int, c_int, c_int, c_int],
     "mjx_hpr_qlayout": [c_int, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_int, c_dbl, c_vp],
     "mjx_hpr_update_q": [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_int,
                          c_dbl, c_dbl, c_dbl, c_vp, c_vp],
-    "mjx_hpr_marginals_q": [c_int, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_dbl, c_vp, c_vp, c_vp, c_vp],
+    "mjx_hpr_marginals_q": [c_int, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "mjx_hpr_q_ii": [c_int, c_vp, c_i64, c_int, c_int, c_vp, c_vp],
     "mjx_hpr_er_scratch_bytes": [c_int, c_int, c_int, c_int],
     "mjx_hpr_er_update_class": [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_int,
                                 c_dbl, c_dbl, c_dbl, c_vp, c_i64, c_vp],

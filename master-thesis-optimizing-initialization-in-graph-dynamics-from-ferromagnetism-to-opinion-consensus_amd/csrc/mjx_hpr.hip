@@ -87,6 +87,21 @@ extern "C" int mjx_hpr_new_biases(int dtype, void* biases, const void* marg, con
     return MJX_OK;
 }
 
+extern "C" int mjx_hpr_new_biases_mask(int dtype, void* biases, const void* marg, const uint8_t* refresh,
+                                       double pie, int64_t n, int32_t* s, void* stream) {
+    if (n < 1 || !biases || !marg || !refresh) return MJX_EINVAL;
+    hipStream_t st = as_stream(stream);
+    const unsigned grid = (unsigned)((n + 255) / 256);
+    if (dtype == MJX_F32)
+        k_hpr_new_biases_mask<float><<<grid, 256, 0, st>>>((float*)biases, (const float*)marg, refresh, (float)pie, n, s);
+    else if (dtype == MJX_F64)
+        k_hpr_new_biases_mask<double><<<grid, 256, 0, st>>>((double*)biases, (const double*)marg, refresh, pie, n, s);
+    else
+        return MJX_EINVAL;
+    MJX_LAUNCH_CHECK("k_hpr_new_biases_mask");
+    return MJX_OK;
+}
+
 // per-node bias pairs out[2v + k] = src[idx[v] * stride + k * half]: the
 // node-indexed biases the update kernels read, taken from the reference's
 // chi-shaped biases_chi (stride = 4^T, half = 4^T / 2; code/HPR_pytorch_RRG.py:
@@ -156,15 +171,26 @@ extern "C" int mjx_hpr_update_q(int dtype, const void* chi_in, void* chi_out, co
 
 template <typename S>
 static int marginals_q_impl(const void* chi, const int32_t* out_row, int64_t n, int d, int T, double eps,
-                            const void* scale, void* zwork, void* marg, hipStream_t st) {
+                            const void* scale, const void* ii, void* zwork, void* marg, hipStream_t st) {
     const int64_t E = n * (int64_t)d / 2;
     S* zp = (S*)zwork;
     S* zm = zp + 2 * E;
+    // ii (nullable): precomputed II x II sums (mjx_hpr_q_ii), used where whole
+    // 16-B pieces fall in one quadrant
 #define MJX_EDGE_ZQ(TT)                                                                                  \
     case TT: {                                                                                           \
-        auto k = k_hpr_edge_z_q<S, TT>;                                                                  \
         const int64_t lanes = E * (1 << TT) / 2;                                                         \
-        k<<<resident_grid(k, 256, 0, lanes), 256, 0, st>>>((const S*)chi, E, (S)eps, (const S*)scale, zp, zm); \
+        if constexpr (QZ<S, TT>::ALIGNED) {                                                              \
+            if (ii) {                                                                                    \
+                auto k = k_hpr_edge_z_q<S, TT, true>;                                                    \
+                k<<<resident_grid(k, 256, 0, lanes), 256, 0, st>>>((const S*)chi, E, (S)eps, (const S*)scale, \
+                                                                   zp, zm, (const S*)ii);                \
+                break;                                                                                   \
+            }                                                                                            \
+        }                                                                                                \
+        auto k = k_hpr_edge_z_q<S, TT, false>;                                                           \
+        k<<<resident_grid(k, 256, 0, lanes), 256, 0, st>>>((const S*)chi, E, (S)eps, (const S*)scale, zp, zm, \
+                                                           nullptr);                                     \
         break;                                                                                           \
     }
     switch (T) {
@@ -179,11 +205,31 @@ static int marginals_q_impl(const void* chi, const int32_t* out_row, int64_t n, 
 }
 
 extern "C" int mjx_hpr_marginals_q(int dtype, const void* chi, const int32_t* out_row, int64_t n, int d, int p, int c,
-                                   double eps, const void* scale, void* zwork, void* marg, void* stream) {
+                                   double eps, const void* scale, const void* ii, void* zwork, void* marg,
+                                   void* stream) {
     if (n < 1 || d < 1 || p < 1 || c < 1 || !chi || !out_row || !scale || !zwork || !marg) return MJX_EINVAL;
     if ((n * (int64_t)d) % 2) return MJX_EINVAL;
     hipStream_t st = as_stream(stream);
-    if (dtype == MJX_F32) return marginals_q_impl<float>(chi, out_row, n, d, p + c, eps, scale, zwork, marg, st);
-    if (dtype == MJX_F64) return marginals_q_impl<double>(chi, out_row, n, d, p + c, eps, scale, zwork, marg, st);
+    if (dtype == MJX_F32) return marginals_q_impl<float>(chi, out_row, n, d, p + c, eps, scale, ii, zwork, marg, st);
+    if (dtype == MJX_F64) return marginals_q_impl<double>(chi, out_row, n, d, p + c, eps, scale, ii, zwork, marg, st);
     return MJX_EINVAL;
+}
+
+extern "C" int mjx_hpr_q_ii(int dtype, const void* chi, int64_t E, int p, int c, void* ii, void* stream) {
+    if (E < 1 || p < 1 || c < 1 || !chi || !ii) return MJX_EINVAL;
+    hipStream_t st = as_stream(stream);
+    const unsigned grid = (unsigned)grid_for(E, 8);
+#define MJX_QII(TT)                                                                                      \
+    case TT:                                                                                             \
+        if (dtype == MJX_F32) k_hpr_q_ii<float, TT><<<grid, 256, 0, st>>>((const float*)chi, E, (float*)ii); \
+        else if (dtype == MJX_F64) k_hpr_q_ii<double, TT><<<grid, 256, 0, st>>>((const double*)chi, E, (double*)ii); \
+        else return MJX_EINVAL;                                                                          \
+        break;
+    switch (p + c) {
+        MJX_QII(2) MJX_QII(3) MJX_QII(4) MJX_QII(5)
+        default: return MJX_ERANGE;
+    }
+#undef MJX_QII
+    MJX_LAUNCH_CHECK("k_hpr_q_ii");
+    return MJX_OK;
 }

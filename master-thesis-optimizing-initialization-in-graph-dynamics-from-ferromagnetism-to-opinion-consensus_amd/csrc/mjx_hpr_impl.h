@@ -740,10 +740,22 @@ __global__ void __launch_bounds__(256) k_hpr_edge_z(const S* __restrict__ chi, i
 // in row r+E sits in the quadrant with the two validity bits swapped, and a
 // product carries scale^(number of invalid senders) (IV / II entries are
 // stored undecayed).  Z+ by x_u[0] = +1 <=> (x_u >> 1) < H/2.
+// IIP: the II x II products never change (both factors stay chi_0), so their
+// four sums per edge come precomputed (ii[4e..4e+3] = by x_u[0] +/-, by x_v[0]
+// +/-, k_hpr_q_ii) and the II pieces of both rows are not read: 1.5 instead of
+// 2 KB per edge at T = 4 fp32.  Needs whole 16-B pieces per quadrant
+// (q_ii_aligned).
 template <typename S, int T>
+struct QZ {
+    static constexpr int X = 1 << T, H = X / 2, HH = H * H;
+    static constexpr int VN = Vec16<S>::N, G = X < 64 ? X : 64;
+    static constexpr bool ALIGNED = HH % (G * VN) == 0;
+};
+
+template <typename S, int T, bool IIP = false>
 __global__ void __launch_bounds__(256) k_hpr_edge_z_q(const S* __restrict__ chi, int64_t E, S eps,
                                                        const S* __restrict__ scale, S* __restrict__ zp,
-                                                       S* __restrict__ zm) {
+                                                       S* __restrict__ zm, const S* __restrict__ ii = nullptr) {
     constexpr int X = 1 << T, NC = X * X, H = X / 2, HH = H * H;
     using V = typename Vec16<S>::T;
     constexpr int VN = Vec16<S>::N;
@@ -751,6 +763,9 @@ __global__ void __launch_bounds__(256) k_hpr_edge_z_q(const S* __restrict__ chi,
     constexpr int NV = NC / (VN * G);                // 16-B pieces per lane per row
     constexpr int EPW = 64 / G;                      // edges per wave instruction
     constexpr int U = 2;                             // edge groups in flight per lane
+    static_assert(!IIP || QZ<S, T>::ALIGNED, "II skip needs whole pieces per quadrant");
+    // piece v lies in quadrant v * G * VN / HH (when aligned); II = 3
+    constexpr int NVR = IIP ? NV - NV / 4 : NV;       // pieces read per row
     const S s1 = *scale, s2 = s1 * s1;
     const int lane = threadIdx.x & 63;
     const int g = lane / G, l = lane % G;
@@ -763,7 +778,7 @@ __global__ void __launch_bounds__(256) k_hpr_edge_z_q(const S* __restrict__ chi,
             const int64_t r = base + u * EPW + g;
             const int64_t rr = r < E ? r : E - 1;            // branch-free loads
 #pragma unroll
-            for (int v = 0; v < NV; ++v) {
+            for (int v = 0; v < NVR; ++v) {
                 const int j0 = (v * G + l) * VN;
                 const V x = *reinterpret_cast<const V*>(chi + rr * NC + j0);
                 const S* xs = reinterpret_cast<const S*>(&x);
@@ -781,7 +796,7 @@ __global__ void __launch_bounds__(256) k_hpr_edge_z_q(const S* __restrict__ chi,
             const int64_t r = base + u * EPW + g;
             S sp = 0, sm = 0, bp = 0, bm = 0;            // by x_u[0], by x_v[0]
 #pragma unroll
-            for (int v = 0; v < NV; ++v)
+            for (int v = 0; v < NVR; ++v)
 #pragma unroll
                 for (int e = 0; e < VN; ++e) {
                     const int j = (v * G + l) * VN + e, q = j / HH, w = j % HH;
@@ -798,6 +813,10 @@ __global__ void __launch_bounds__(256) k_hpr_edge_z_q(const S* __restrict__ chi,
                 bm += __shfl_xor(bm, off, 64);
             }
             if (l == 0 && r < E) {
+                if (IIP) {
+                    sp += s2 * ii[4 * r]; sm += s2 * ii[4 * r + 1];
+                    bp += s2 * ii[4 * r + 2]; bm += s2 * ii[4 * r + 3];
+                }
                 S fp = sp > eps ? sp : eps, fm = sm > eps ? sm : eps;
                 bp = bp > eps ? bp : eps; bm = bm > eps ? bm : eps;
                 const S sf = fp + fm, sb = bp + bm;
@@ -805,6 +824,21 @@ __global__ void __launch_bounds__(256) k_hpr_edge_z_q(const S* __restrict__ chi,
                 zp[r + E] = bp / sb; zm[r + E] = bm / sb;
             }
         }
+    }
+}
+
+// the four II x II sums of every edge of a decay-split chi (its chi_0 quadrants)
+template <typename S, int T>
+__global__ void k_hpr_q_ii(const S* __restrict__ chi, int64_t E, S* __restrict__ ii) {
+    constexpr int X = 1 << T, NC = X * X, H = X / 2, HH = H * H;
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < E; r += (int64_t)gridDim.x * blockDim.x) {
+        S sp = 0, sm = 0, bp = 0, bm = 0;
+        for (int w = 0; w < HH; ++w) {
+            const S z = chi[r * NC + 3 * HH + w] * chi[(r + E) * NC + 3 * HH + (w % H) * H + w / H];
+            if (w / H < H / 2) sp += z; else sm += z;
+            if (w % H < H / 2) bp += z; else bm += z;
+        }
+        ii[4 * r] = sp; ii[4 * r + 1] = sm; ii[4 * r + 2] = bp; ii[4 * r + 3] = bm;
     }
 }
 
@@ -851,6 +885,25 @@ __global__ void __launch_bounds__(256) k_hpr_new_biases(S* __restrict__ biases, 
     if (i >= n) return;
     S b0 = biases[2 * i], b1 = biases[2 * i + 1];
     if (u[i] < thresh) {
+        const bool minus = marg[2 * i + 1] >= marg[2 * i];
+        b0 = minus ? pie : S(1) - pie;
+        b1 = minus ? S(1) - pie : pie;
+        biases[2 * i] = b0;
+        biases[2 * i + 1] = b1;
+    }
+    if (s) s[i] = b0 > b1 ? 1 : -1;
+}
+
+// the same with the refresh decision made on the host (refresh[i] = u_i <
+// 1-(1+t)^-gamma, :142): one byte per node crosses the bus instead of a double
+template <typename S>
+__global__ void __launch_bounds__(256) k_hpr_new_biases_mask(S* __restrict__ biases, const S* __restrict__ marg,
+                                                              const uint8_t* __restrict__ refresh, S pie, int64_t n,
+                                                              int32_t* __restrict__ s) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    S b0 = biases[2 * i], b1 = biases[2 * i + 1];
+    if (refresh[i]) {
         const bool minus = marg[2 * i + 1] >= marg[2 * i];
         b0 = minus ? pie : S(1) - pie;
         b1 = minus ? S(1) - pie : pie;

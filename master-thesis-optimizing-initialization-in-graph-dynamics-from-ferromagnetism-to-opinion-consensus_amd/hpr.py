@@ -207,6 +207,10 @@ class HPRState:
                       self.p, self.c, self.attr_value, 1, 1.0, _device.stream_handle())
             self.chi_b = self.chi.clone()        # both buffers carry chi_0's invalid-sender quadrants
             self._sc = torch.ones(2, dtype=dtype, device=chi0.device)
+            # the II x II sums never change: once, so the marginals skip the II quadrants
+            self._ii = torch.empty(4 * plan.E, dtype=dtype, device=chi0.device)
+            _lib.call("mjx_hpr_q_ii", _code(dtype), _device.ptr(self.chi), plan.E, self.p, self.c,
+                      _device.ptr(self._ii), _device.stream_handle())
         else:
             self.chi = chi0
             self.chi_b = torch.empty_like(self.chi)
@@ -261,7 +265,8 @@ class HPRState:
                       _device.ptr(plan.out_row), plan.n, plan.d, self.p, self.c, self.attr_value, wp, wm,
                       self.damppar, sc_in, st)
             _lib.call("mjx_hpr_marginals_q", _code(self.dtype), _device.ptr(dst), _device.ptr(plan.out_row), plan.n,
-                      plan.d, self.p, self.c, 1e-15, sc_out, _device.ptr(self.zwork), _device.ptr(self.marg), st)
+                      plan.d, self.p, self.c, 1e-15, sc_out, _device.ptr(self._ii), _device.ptr(self.zwork),
+                      _device.ptr(self.marg), st)
         else:
             HPr_dp(src, self.biases, self.plan, self.p, self.c, self.attr_value, self.lmbd_in, self.damppar, out=dst)
             marginals_comp(dst, self.plan, self.p, self.c, zwork=self.zwork, out=self.marg)
@@ -283,7 +288,13 @@ class HPRState:
         if getattr(self, "_bk", None) != k:
             n, dev = self.plan.n, self.s.device
             self._bk = k
-            self._u = torch.empty((k, n), dtype=torch.float64, device=dev)
+            self._mask = torch.empty((k, n), dtype=torch.bool, device=dev)
+            # host staging, double-buffered: batch i+1 is drawn while batch i runs
+            self._pin = [(torch.empty((k, n), dtype=torch.bool).pin_memory(),
+                          torch.empty(k + 1, dtype=self.dtype).pin_memory()) for _ in range(2)]
+            self._pin_i = 0
+            self._sums_host = torch.empty(k, dtype=torch.int64).pin_memory()
+            self._done = torch.cuda.Event()
             self._s_hist = torch.empty((k, n), dtype=torch.int32, device=dev)
             self._cnt = torch.zeros(k, dtype=torch.int64, device=dev)
             self._scales = torch.ones(k + 1, dtype=self.dtype, device=dev)
@@ -295,9 +306,10 @@ class HPRState:
         """The launches of k iterations (code/HPR_pytorch_RRG.py:345-356) on the
         current stream, every argument fixed: iteration j reads the messages from
         buffer j % 2 and writes the other (k even: the batch ends where it
-        started); its uniforms are row j of self._u (already compared with the
-        reinforcement threshold, see steps_batched), its trial configuration goes
-        to row j of self._s_hist and sum(s_endstate(s)) to self._cnt[j]."""
+        started); its refresh decisions are row j of self._mask (the uniforms
+        already compared with the reinforcement threshold on the host, see
+        draw_batch), its trial configuration goes to row j of self._s_hist and
+        sum(s_endstate(s)) to self._cnt[j]."""
         n, T, st = self.plan.n, self.p + self.c - 1, _device.stream_handle()
         self._cnt.zero_()
         sz = self._scales.element_size()
@@ -305,8 +317,8 @@ class HPRState:
             src, dst = (self.chi, self.chi_b) if j % 2 == 0 else (self.chi_b, self.chi)
             # decay-split layout: row j of self._scales is (1-damp)^(t+j), set before each replay
             self._update(src, dst, self._scales.data_ptr() + j * sz, self._scales.data_ptr() + (j + 1) * sz)
-            _lib.call("mjx_hpr_new_biases", _code(self.dtype), _device.ptr(self.biases), _device.ptr(self.marg),
-                      _device.ptr(self._u[j]), 0.5, self.pie, n, _device.ptr(self._s_hist[j]), st)
+            _lib.call("mjx_hpr_new_biases_mask", _code(self.dtype), _device.ptr(self.biases), _device.ptr(self.marg),
+                      _device.ptr(self._mask[j]), self.pie, n, _device.ptr(self._s_hist[j]), st)
             _lib.call("mjx_pack_np", _device.ptr(self._s_hist[j]), _lib.MJX_I32, n, _device.ptr(self._bits), st)
             if T:
                 rollout(self.plan.graph, self._bits, T, out=self._rtmp[0], tmp=self._rtmp[1],
@@ -314,30 +326,38 @@ class HPRState:
             else:
                 _lib.call("mjx_popcount_np", _device.ptr(self._bits), n, _device.ptr(self._cnt[j:j + 1]), st)
 
-    def steps_batched(self, k, generator, graph=True):
-        """k iterations of the main loop (code/HPR_pytorch_RRG.py:345-356) with no
-        host read in between; one read returns every iteration's
-        sum(s_endstate(s)).  The k uniform vectors are drawn up front from the
-        CPU generator in the reference's order (one torch.rand(n) per iteration,
-        :142) and compared on the host with that iteration's threshold
-        1-(1+t)^-gamma (the same float64 comparison the reference makes), so
-        the device batch has no per-iteration argument: after one eager batch
-        it is captured once as a hipGraph and replayed (``graph``).
-        Returns (sums[k] int64 numpy, s_hist (k, n) int32 device tensor,
-        generator state before the draws)."""
+    def draw_batch(self, k, generator, t0=None):
+        """Host half of a batch of k iterations starting at iteration t0 (default
+        self.t): the k uniform vectors drawn from the CPU generator in the
+        reference's order (one torch.rand(n) per iteration, :142) and compared
+        with each iteration's threshold 1-(1+t)^-gamma (the float64 comparison
+        the reference makes) into pinned refresh masks.  Returns a handle for
+        launch_batch holding the generator state before the draws."""
         if k % 2:
             raise ValueError("batch size must be even (the message buffers alternate)")
         self._batch_buffers(k)
+        t0 = self.t if t0 is None else t0
         n = self.plan.n
+        mask, scales = self._pin[self._pin_i]
+        self._pin_i ^= 1
         g_state = generator.get_state()
-        sel = torch.empty((k, n), dtype=torch.float64)
         for j in range(k):
             u = torch.rand(n, dtype=torch.float64, generator=generator)
-            thresh = 1 - (1 + (self.t + j)) ** (-self.gamma)            # code/HPR_pytorch_RRG.py:142
-            sel[j] = torch.where(u < thresh, 0.0, 1.0)                  # kernel: refresh iff sel < 0.5
-        self._u.copy_(sel)
+            torch.lt(u, 1 - (1 + (t0 + j)) ** (-self.gamma), out=mask[j])     # code/HPR_pytorch_RRG.py:142
         if self.layout == "q":
-            self._scales.copy_(torch.tensor([self.decay(self.t + j) for j in range(k + 1)], dtype=self.dtype))
+            scales.copy_(torch.tensor([self.decay(t0 + j) for j in range(k + 1)], dtype=self.dtype))
+        return {"k": k, "t0": t0, "mask": mask, "scales": scales, "g_state": g_state}
+
+    def launch_batch(self, drawn, graph=True):
+        """Device half: the batch's masks (and decay scales) copied in, its k
+        iterations launched (a hipGraph replay after one eager batch), the sums
+        queued for one host read (collect_batch).  Nothing here waits."""
+        k = drawn["k"]
+        if drawn["t0"] != self.t:
+            raise ValueError("batch drawn for another iteration")
+        self._mask.copy_(drawn["mask"], non_blocking=True)
+        if self.layout == "q":
+            self._scales.copy_(drawn["scales"], non_blocking=True)
         if graph and self._graph is not None:
             self._graph.replay()
         elif graph and getattr(self, "_warm", False):
@@ -350,7 +370,22 @@ class HPRState:
             self._warm = True
         self.t += k
         self.s.copy_(self._s_hist[k - 1])
-        return 2 * self._cnt.cpu().numpy() - n, self._s_hist, g_state
+        self._sums_host.copy_(self._cnt, non_blocking=True)
+        self._done.record()
+
+    def collect_batch(self):
+        """The one host read of a batch: sum(s_endstate(s)) of every iteration."""
+        self._done.synchronize()
+        return 2 * self._sums_host.numpy().copy() - self.plan.n
+
+    def steps_batched(self, k, generator, graph=True):
+        """k iterations of the main loop (code/HPR_pytorch_RRG.py:345-356) with no
+        host read in between (draw_batch + launch_batch + collect_batch).
+        Returns (sums[k] int64 numpy, s_hist (k, n) int32 device tensor,
+        generator state before the draws)."""
+        drawn = self.draw_batch(k, generator)
+        self.launch_batch(drawn, graph=graph)
+        return self.collect_batch(), self._s_hist, drawn["g_state"]
 
 
 def hpr_run(d, n, p, c, damppar=0.4, attr_value=1, lmbd_in=None, pie=0.3, gamma=0.1, TT=10000, edges=None,
@@ -387,13 +422,20 @@ def hpr_run(d, n, p, c, damppar=0.4, attr_value=1, lmbd_in=None, pie=0.3, gamma=
     total = st.sum_end()
     m_final = total / n
     s_dev = st.s
+    B = batch + batch % 2 if batch else 0
+    drawn = st.draw_batch(B, generator) if B > 1 and m_final < 1 else None
     while m_final < 1:                                     # code/HPR_pytorch_RRG.py:344-356
-        if batch and batch > 1:
+        if B > 1:
             # `batch` iterations per host read; the run stops at the first
-            # iteration the reference would stop at (t > TT, or consensus)
+            # iteration the reference would stop at (t > TT, or consensus).
+            # The next batch's uniforms are drawn on the host while this one
+            # runs on the device (and discarded if the run stops in it).
             t0 = st.t
-            sums, s_hist, g_state = st.steps_batched(batch + batch % 2, generator, graph=graph)
-            for j in range(batch + batch % 2):
+            st.launch_batch(drawn, graph=graph)
+            g_state = drawn["g_state"]
+            drawn = st.draw_batch(B, generator, t0=t0 + B)
+            sums, s_hist = st.collect_batch(), st._s_hist
+            for j in range(B):
                 t = t0 + j + 1
                 if t > TT:
                     m_final = 2

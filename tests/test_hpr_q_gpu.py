@@ -139,3 +139,27 @@ def test_q_batches_track_ref_layout(mjx_mod):
     res = mjx_mod.hpr_run(d, n, p, c, TT=60, edges=edges, seed=5, dtype=torch.float32, layout="q")
     assert set(res) == {"mag_reached", "num_steps", "conf", "graphs"}
     assert res["conf"].shape == (1, n) and 1 <= res["num_steps"][0] <= 61
+
+
+def test_marginals_q_precomputed_ii_equals_full_read(mjx_mod):
+    """The II x II sums precomputed once (mjx_hpr_q_ii) give the marginals of
+    the full read (ii = NULL) and of the reference layout, at a decayed
+    scale, within 1e-6 (fp32)."""
+    lib = mjx_mod.load_library()
+    F32 = mjx_mod._lib.MJX_F32
+    n, d, p, c = 20_000, 4, 2, 2
+    plan, mk = _pair(mjx_mod, n, d, p, c, seed=9)
+    a = mk("q")
+    st = torch.cuda.current_stream().cuda_stream
+    sc = torch.tensor([0.6 ** 3], dtype=torch.float32, device="cuda")
+    z = torch.empty(4 * plan.E, dtype=torch.float32, device="cuda")
+    m_ii = torch.empty((n, 2), dtype=torch.float32, device="cuda")
+    m_full = torch.empty_like(m_ii)
+    for ii, out in ((a._ii.data_ptr(), m_ii), (None, m_full)):
+        assert lib.mjx_hpr_marginals_q(F32, a.chi.data_ptr(), plan.out_row.data_ptr(), n, d, p, c, 1e-15,
+                                       sc.data_ptr(), ii, z.data_ptr(), out.data_ptr(), st) == 0
+    assert float((m_ii - m_full).abs().max()) <= 1e-6
+    ref = torch.empty(a.chi.shape, dtype=torch.float32, device="cuda")
+    assert lib.mjx_hpr_qlayout(F32, a.chi.data_ptr(), ref.data_ptr(), a.chi.shape[0], p, c, 1, 0, 0.6 ** 3, st) == 0
+    m_ref = mjx_mod.marginals_comp(ref, plan, p, c)
+    assert float((m_ii - m_ref).abs().max()) <= 1e-6
