@@ -445,22 +445,24 @@ def bench_hpr(args, rank, world, dist, dev):
     st.steps_batched(16, gcpu)                      # eager batch
     st.steps_batched(16, gcpu)                      # capture + replay
     nb = max(1, K // 4)
-    drawn = [st.draw_batch(16, gcpu)]
+    st.rng_attach(gcpu)
+    drawn = [st.draw_batch_device(16)]
 
     def run_loop():
-        # hpr_run's loop: the next batch's uniforms drawn on the host while
-        # this batch runs, one host read per batch
+        # hpr_run's loop: the next batch's uniforms drawn (the CPU generator's
+        # stream continued on the device, its own stream) while this batch
+        # runs, one host read per batch
         for _ in range(nb):
             st.launch_batch(drawn[0])
-            drawn[0] = st.draw_batch(16, gcpu)
+            drawn[0] = st.draw_batch_device(16, st.t)
             st.collect_batch()
 
     el_loop = _timed(run_loop, dist, dev)
     res["loop_state_q"]["loop_ms_per_iter"] = 1e3 * el_loop / (16 * nb)
     res["loop_state_q"]["loop_note"] = ("hpr_run's loop in batches of 16: update + marginals + new_biases_i + "
                                         "pack + p+c-1 sweeps + count per iteration on the device; the reference's "
-                                        "torch.rand(n) per iteration drawn on the host (CPU generator) while the "
-                                        "previous batch runs; one host read per batch")
+                                        "torch.rand(n) per iteration (CPU generator stream) continued on the device "
+                                        "on a stream of its own beside the batch; one host read per batch")
     del st
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # the reference runs HPr_dp as torch ops; on the host that is torch's CPU

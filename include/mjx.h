@@ -239,6 +239,15 @@ int mjx_hpr_new_biases(int dtype, void* biases, const void* marg, const double* 
  * nonzero = refresh node i's biases). */
 int mjx_hpr_new_biases_mask(int dtype, void* biases, const void* marg, const uint8_t* refresh, double pie,
                             int64_t n, int32_t* s, void* stream);
+/* The reference's torch.rand(n) per iteration (torch's CPU generator, :142) on the
+ * device: state[624] (uint32) and left_next[2] = the CPU engine's `left`, `next`
+ * (its get_state() fields); k iterations of n float64 uniforms u = ((y_hi<<32 |
+ * y_lo) & (2^53-1)) * 2^-53 from consecutive outputs, compared with thresh[j]
+ * (device float64) into mask[j*n + i] (uint8).  state/left_next are left where the
+ * CPU generator would be after the same draws.  One workgroup; run it on a
+ * stream of its own beside the iterations that consume the masks. */
+int mjx_hpr_refresh_masks(uint32_t* state, int32_t* left_next, int64_t n, int k, const double* thresh,
+                          uint8_t* mask, void* stream);
 /* The edge half of marginals_comp (code/HPR_pytorch_RRG.py:150-161) alone:
  * zwork[4E] = per-row normalised (Z+ [2E], Z- [2E]) of every directed row. */
 int mjx_hpr_edge_z(int dtype, const void* chi, int64_t E, int p, int c, double eps, void* zwork,

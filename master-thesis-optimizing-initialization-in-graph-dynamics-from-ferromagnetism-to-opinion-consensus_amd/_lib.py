@@ -51,6 +51,7 @@ SIGNATURES = {
     "mjx_hpr_marginals": [c_int, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_dbl, c_vp, c_vp, c_vp],
     "mjx_hpr_new_biases": [c_int, c_vp, c_vp, c_vp, c_dbl, c_dbl, c_i64, c_vp, c_vp],
     "mjx_hpr_new_biases_mask": [c_int, c_vp, c_vp, c_vp, c_dbl, c_i64, c_vp, c_vp],
+    "mjx_hpr_refresh_masks": [c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp],
     "mjx_hpr_edge_z": [c_int, c_vp, c_i64, c_int, c_int, c_dbl, c_vp, c_vp],
     "mjx_hpr_node_biases": [c_int, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp],
     "mjx_hpr_q_supported": [c_int, c_int, c_int, c_int],

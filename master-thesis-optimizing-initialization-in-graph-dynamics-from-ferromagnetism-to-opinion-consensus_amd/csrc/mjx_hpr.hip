@@ -233,3 +233,108 @@ extern "C" int mjx_hpr_q_ii(int dtype, const void* chi, int64_t E, int p, int c,
     MJX_LAUNCH_CHECK("k_hpr_q_ii");
     return MJX_OK;
 }
+
+// ---- the reference's per-iteration torch.rand(n) on the device -----------------
+// new_biases_i draws torch.rand(n) on torch's CPU generator every iteration
+// (code/HPR_pytorch_RRG.py:142).  That generator is an MT19937 whose float64
+// uniform is ((y_hi << 32 | y_lo) & (2^53 - 1)) * 2^-53 from two consecutive
+// 32-bit outputs, with the engine state (624 words, `left`, `next`: a call
+// decrements left, twists when it reaches 0, then returns state[next++]
+// tempered).  One workgroup continues that stream from the caller's state for k
+// iterations of n uniforms and writes the refresh masks mask[j*n + i] =
+// (u < thresh[j]); the state is left where the CPU generator would be.  The
+// twist runs in LDS in three dependency phases (words [0,227), [227,454),
+// [454,624)); each block of 624 outputs is tempered and paired in parallel.
+namespace {
+constexpr int kMT = 624, kMTM = 397;
+
+__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+}
+
+__device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t m) {
+    const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+    return m ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+}
+
+__global__ void __launch_bounds__(1024) k_mt_refresh_masks(uint32_t* __restrict__ state, int32_t* __restrict__ ln,
+                                                            int64_t n, int k, const double* __restrict__ thresh,
+                                                            uint8_t* __restrict__ mask) {
+    __shared__ uint32_t buf[2][kMT];           // the state, ping-pong across twists
+    const int tid = threadIdx.x;
+    for (int i = tid; i < kMT; i += blockDim.x) buf[0][i] = state[i];
+    int cur = 0;
+    const int left0 = ln[0], next0 = ln[1];
+    __syncthreads();
+    const int64_t total = 2 * n * (int64_t)k;  // 32-bit outputs to consume
+    int64_t done = 0;                          // outputs consumed so far
+    int pos = next0;                           // next state word to read
+    int avail = left0 - 1;                     // words readable before a twist
+    bool carry = false;                        // an unpaired high word from the previous block
+    uint32_t cval = 0;
+    while (done < total) {
+        if (avail == 0) {
+            // twist into the other buffer: three dependency phases, one barrier each
+            const uint32_t* o = buf[cur];
+            uint32_t* w = buf[cur ^ 1];
+            if (tid < 227) w[tid] = mt_mix(o[tid], o[tid + 1], o[tid + kMTM]);
+            __syncthreads();
+            if (tid < 227) w[tid + 227] = mt_mix(o[tid + 227], o[tid + 228], w[tid]);
+            __syncthreads();
+            if (tid < 170) {
+                const int i = tid + 454;
+                w[i] = mt_mix(o[i], (i + 1 < kMT) ? o[i + 1] : w[0], w[i - 227]);
+            }
+            __syncthreads();
+            cur ^= 1;
+            pos = 0;
+            avail = kMT;
+        }
+        const uint32_t* mt = buf[cur];
+        const int64_t need = total - done;
+        const int cnt = (int)((int64_t)avail < need ? (int64_t)avail : need);
+        const int off = carry ? 1 : 0;
+        const int have = off + cnt;
+        const int pairs = have / 2;
+        const int64_t d0 = (done - off) / 2;   // uniform index of this block's first pair
+        const int64_t j0 = d0 / n, r0 = d0 - j0 * n;   // its iteration and node (one division per block)
+        const double th0 = thresh[j0];
+        for (int q = tid; q < pairs; q += blockDim.x) {
+            const int w0 = 2 * q - off;        // word of the pair's high half (-1: the carried one)
+            const uint32_t hi = (w0 < 0) ? cval : mt_temper(mt[pos + w0]);
+            const uint32_t lo = mt_temper(mt[pos + w0 + 1]);
+            const uint64_t r = ((uint64_t)hi << 32) | lo;
+            const double u = (double)(r & ((1ull << 53) - 1)) * (1.0 / 9007199254740992.0);
+            const int64_t rq = r0 + q;
+            const double th = (rq < n) ? th0 : thresh[j0 + rq / n];
+            mask[d0 + q] = u < th ? 1 : 0;
+        }
+        carry = (have & 1) != 0;
+        if (carry) cval = mt_temper(mt[pos + cnt - 1]);
+        done += cnt;
+        pos += cnt;
+        avail -= cnt;
+        __syncthreads();                       // the next twist overwrites the other buffer only
+    }
+    for (int i = tid; i < kMT; i += blockDim.x) state[i] = buf[cur][i];
+    if (tid == 0) {
+        // where the CPU engine would be: `pos` words of the current state read
+        // (left + next = 625 after any read; a twist pending when pos = 624)
+        ln[0] = kMT + 1 - pos;
+        ln[1] = pos;
+    }
+}
+}  // namespace
+
+extern "C" int mjx_hpr_refresh_masks(uint32_t* state, int32_t* left_next, int64_t n, int k, const double* thresh,
+                                     uint8_t* mask, void* stream) {
+    if (n < 1 || k < 0 || !state || !left_next || (k > 0 && (!thresh || !mask))) return MJX_EINVAL;
+    if (k == 0) return MJX_OK;
+    k_mt_refresh_masks<<<1, 1024, 0, as_stream(stream)>>>(state, left_next, n, k, thresh, mask);
+    MJX_LAUNCH_CHECK("k_mt_refresh_masks");
+    return MJX_OK;
+}

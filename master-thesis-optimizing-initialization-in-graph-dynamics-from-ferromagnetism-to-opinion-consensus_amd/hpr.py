@@ -348,6 +348,70 @@ class HPRState:
             scales.copy_(torch.tensor([self.decay(t0 + j) for j in range(k + 1)], dtype=self.dtype))
         return {"k": k, "t0": t0, "mask": mask, "scales": scales, "g_state": g_state}
 
+    # -- the reference's CPU random stream continued on the device ---------------
+    def rng_attach(self, generator):
+        """Continue ``generator``'s stream (torch's CPU MT19937) on the device:
+        its 624-word state and left/next counters (get_state(), bytes 8, 16 and
+        24..5016) are copied in; draw_batch_device then produces the same
+        uniforms torch.rand(n) would, on a stream of its own."""
+        b = generator.get_state().numpy()
+        if b.size != 5056:
+            raise _lib.MjxError(f"unexpected CPU generator state size {b.size}")
+        dev = self.s.device
+        words = b[24:24 + 624 * 8].view(np.uint64).astype(np.uint32)
+        left = int(b[8:12].view(np.int32)[0])
+        nxt = int(b[16:24].view(np.uint64)[0])
+        self._mt = torch.from_numpy(words.view(np.int32).copy()).to(dev)
+        self._ln = torch.tensor([left, nxt], dtype=torch.int32, device=dev)
+        self._gen_state_bytes = b.copy()
+        self._gen_stream = torch.cuda.Stream(device=dev)
+        self._gen_done = [torch.cuda.Event(), torch.cuda.Event()]
+        self._mask_free = [torch.cuda.Event(), torch.cuda.Event()]
+        self._gen_slot = 0
+
+    def rng_state_bytes(self, slot=None):
+        """The CPU generator state (uint8 tensor for set_state) at the start of
+        the batch drawn in ``slot`` (None: the current device position)."""
+        if slot is None:
+            mt, ln = self._mt, self._ln
+        else:
+            mt, ln = self._snap[slot]
+        b = self._gen_state_bytes.copy()
+        b[24:24 + 624 * 8] = mt.cpu().numpy().view(np.uint32).astype(np.uint64).view(np.uint8)
+        left, nxt = (int(x) for x in ln.cpu().numpy())
+        b[8:12] = np.array([left], dtype=np.int32).view(np.uint8)
+        b[16:24] = np.array([nxt], dtype=np.uint64).view(np.uint8)
+        return torch.from_numpy(b)
+
+    def draw_batch_device(self, k, t0=None):
+        """draw_batch on the device (mjx_hpr_refresh_masks on the generator's
+        own stream): the same masks, no host work but k thresholds."""
+        if k % 2:
+            raise ValueError("batch size must be even (the message buffers alternate)")
+        self._batch_buffers(k)
+        if getattr(self, "_gmask", None) is None or self._gmask[0].shape != (k, self.plan.n):
+            n, dev = self.plan.n, self.s.device
+            self._gmask = [torch.empty((k, n), dtype=torch.bool, device=dev) for _ in range(2)]
+            self._gthr = [torch.empty(k, dtype=torch.float64, device=dev) for _ in range(2)]
+            self._snap = [(torch.empty_like(self._mt), torch.empty_like(self._ln)) for _ in range(2)]
+        t0 = self.t if t0 is None else t0
+        slot = self._gen_slot
+        self._gen_slot ^= 1
+        thr = torch.tensor([1 - (1 + (t0 + j)) ** (-self.gamma) for j in range(k)], dtype=torch.float64)
+        scales = self._pin[slot][1]
+        if self.layout == "q":
+            scales.copy_(torch.tensor([self.decay(t0 + j) for j in range(k + 1)], dtype=self.dtype))
+        gs = self._gen_stream
+        with torch.cuda.stream(gs):
+            gs.wait_event(self._mask_free[slot])           # the batch two back has copied its masks out
+            self._snap[slot][0].copy_(self._mt)
+            self._snap[slot][1].copy_(self._ln)
+            self._gthr[slot].copy_(thr)
+            _lib.call("mjx_hpr_refresh_masks", _device.ptr(self._mt), _device.ptr(self._ln), self.plan.n, k,
+                      _device.ptr(self._gthr[slot]), _device.ptr(self._gmask[slot]), gs.cuda_stream)
+            self._gen_done[slot].record(gs)
+        return {"k": k, "t0": t0, "slot": slot, "scales": scales, "device": True}
+
     def launch_batch(self, drawn, graph=True):
         """Device half: the batch's masks (and decay scales) copied in, its k
         iterations launched (a hipGraph replay after one eager batch), the sums
@@ -355,7 +419,13 @@ class HPRState:
         k = drawn["k"]
         if drawn["t0"] != self.t:
             raise ValueError("batch drawn for another iteration")
-        self._mask.copy_(drawn["mask"], non_blocking=True)
+        if drawn.get("device"):
+            slot = drawn["slot"]
+            torch.cuda.current_stream().wait_event(self._gen_done[slot])
+            self._mask.copy_(self._gmask[slot])
+            self._mask_free[slot].record()
+        else:
+            self._mask.copy_(drawn["mask"], non_blocking=True)
         if self.layout == "q":
             self._scales.copy_(drawn["scales"], non_blocking=True)
         if graph and self._graph is not None:
@@ -390,7 +460,7 @@ class HPRState:
 
 def hpr_run(d, n, p, c, damppar=0.4, attr_value=1, lmbd_in=None, pie=0.3, gamma=0.1, TT=10000, edges=None,
             nbrs=None, seed=0, dtype=torch.float32, chi0=None, biases0=None, generator=None, batch=16, graph=True,
-            layout=None):
+            layout=None, rng="device"):
     """The HPR experiment of code/HPR_pytorch_RRG.py:224-377 for one graph.
 
     Randomness follows the reference: with ``generator`` a torch CPU generator
@@ -400,7 +470,10 @@ def hpr_run(d, n, p, c, damppar=0.4, attr_value=1, lmbd_in=None, pie=0.3, gamma=
     loop runs in device batches of ``batch`` iterations (one host read each,
     replayed as a hipGraph with ``graph``); on return the generator has made
     exactly the draws the reference makes up to its stop iteration.
-    ``layout``: the message state's layout (HPRState).
+    ``layout``: the message state's layout (HPRState).  ``rng``: "device"
+    continues the generator's stream on the device beside the iterations
+    (mjx_hpr_refresh_masks, bit-identical uniforms), "host" draws torch.rand
+    on the CPU while the previous batch runs.
     Returns the np.savez keys of :377 (mag_reached, conf, num_steps, graphs).
     """
     from .graph import random_regular_edges
@@ -423,7 +496,15 @@ def hpr_run(d, n, p, c, damppar=0.4, attr_value=1, lmbd_in=None, pie=0.3, gamma=
     m_final = total / n
     s_dev = st.s
     B = batch + batch % 2 if batch else 0
-    drawn = st.draw_batch(B, generator) if B > 1 and m_final < 1 else None
+    on_dev = rng == "device"
+    if B > 1 and m_final < 1:
+        if on_dev:
+            st._batch_buffers(B)
+            st.rng_attach(generator)
+            draw = lambda t0=None: st.draw_batch_device(B, t0)  # noqa: E731
+        else:
+            draw = lambda t0=None: st.draw_batch(B, generator, t0)  # noqa: E731
+        drawn = draw()
     while m_final < 1:                                     # code/HPR_pytorch_RRG.py:344-356
         if B > 1:
             # `batch` iterations per host read; the run stops at the first
@@ -432,8 +513,8 @@ def hpr_run(d, n, p, c, damppar=0.4, attr_value=1, lmbd_in=None, pie=0.3, gamma=
             # runs on the device (and discarded if the run stops in it).
             t0 = st.t
             st.launch_batch(drawn, graph=graph)
-            g_state = drawn["g_state"]
-            drawn = st.draw_batch(B, generator, t0=t0 + B)
+            cur = drawn
+            drawn = draw(t0 + B)
             sums, s_hist = st.collect_batch(), st._s_hist
             for j in range(B):
                 t = t0 + j + 1
@@ -445,7 +526,7 @@ def hpr_run(d, n, p, c, damppar=0.4, attr_value=1, lmbd_in=None, pie=0.3, gamma=
                     st.t = t
                     s_dev = s_hist[j]
                     # leave the generator where the reference's would be: j+1 draws
-                    generator.set_state(g_state)
+                    generator.set_state(st.rng_state_bytes(cur["slot"]) if on_dev else cur["g_state"])
                     for _ in range(j + 1):
                         torch.rand(n, dtype=torch.float64, generator=generator)
                     break

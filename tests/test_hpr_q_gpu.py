@@ -163,3 +163,45 @@ def test_marginals_q_precomputed_ii_equals_full_read(mjx_mod):
     assert lib.mjx_hpr_qlayout(F32, a.chi.data_ptr(), ref.data_ptr(), a.chi.shape[0], p, c, 1, 0, 0.6 ** 3, st) == 0
     m_ref = mjx_mod.marginals_comp(ref, plan, p, c)
     assert float((m_ii - m_ref).abs().max()) <= 1e-6
+
+
+@pytest.mark.parametrize("pre,n,k", [(0, 1000, 3), (3, 4097, 2), (1000, 313, 5), (311, 624, 4)])
+def test_device_refresh_masks_equal_torch_cpu_stream(mjx_mod, pre, n, k):
+    """mjx_hpr_refresh_masks continues torch's CPU generator on the device: the
+    masks equal torch.rand(n) < thresh drawn on the CPU (code/HPR_pytorch_RRG.py:
+    142), from a fresh generator and from positions mid-block (odd word
+    counts), and the state handed back is the CPU generator's."""
+    plan, mk = _pair(mjx_mod, 64, 4, 2, 2, seed=1)
+    st = mk("q")
+    g = torch.Generator().manual_seed(7)
+    if pre:
+        torch.rand(pre, dtype=torch.float64, generator=g)
+    h = torch.Generator()
+    h.set_state(g.get_state())
+    st.rng_attach(g)
+    thr = [0.1 * (j + 1) for j in range(k)]
+    lib = mjx_mod.load_library()
+    mask = torch.empty((k, n), dtype=torch.uint8, device="cuda")
+    th = torch.tensor(thr, dtype=torch.float64, device="cuda")
+    assert lib.mjx_hpr_refresh_masks(st._mt.data_ptr(), st._ln.data_ptr(), n, k, th.data_ptr(), mask.data_ptr(),
+                                     torch.cuda.current_stream().cuda_stream) == 0
+    want = torch.stack([torch.rand(n, dtype=torch.float64, generator=h) < thr[j] for j in range(k)])
+    assert torch.equal(mask.cpu().bool(), want)
+    g2 = torch.Generator()
+    g2.set_state(st.rng_state_bytes())
+    assert torch.equal(torch.rand(9, dtype=torch.float64, generator=g2), torch.rand(9, dtype=torch.float64, generator=h))
+
+
+def test_hpr_run_device_rng_equals_host_rng(mjx_mod):
+    """hpr_run with the stream continued on the device and with host draws:
+    same stop iteration, configuration and generator position afterwards."""
+    n, d, p, c = 300, 4, 2, 2
+    edges = mjx_mod.random_regular_edges(d, n, seed=6)
+    out = []
+    for rng in ("device", "host"):
+        g = torch.Generator().manual_seed(11)
+        res = mjx_mod.hpr_run(d, n, p, c, TT=100, edges=edges, dtype=torch.float64, generator=g, rng=rng, batch=8)
+        out.append((res, torch.rand(5, dtype=torch.float64, generator=g)))
+    assert out[0][0]["num_steps"][0] == out[1][0]["num_steps"][0]
+    assert np.array_equal(out[0][0]["conf"], out[1][0]["conf"])
+    assert torch.equal(out[0][1], out[1][1])
