@@ -264,9 +264,13 @@ def bench_er(args, rank, world, dist, dev):
     step()
     el = _timed(lambda: [step() for _ in range(K)], dist, dev)
     nnz = g.nnz
-    dbar = nnz / n
-    # degree-class ELL sweep: int32 neighbours + int32 node order + state rows
-    bytes_per_sweep = 4 * nnz + 4 * n + (W * 8) * n * (dbar + 2)
+    # degree-class ELL sweep: int32 neighbours + int32 node order + state rows:
+    # the deg neighbour rows, the row written, and the node's own row only
+    # where a tie is possible (even degree, always-stay; nb:113-117) -- an
+    # odd-degree class never reads it
+    _, _, classes = g.class_ell()
+    n_even = int(sum(int(cnt) for _, cnt, D, _ in classes.tolist() if D % 2 == 0))
+    bytes_per_sweep = 4 * nnz + 4 * n + (W * 8) * (nnz + n + n_even)
     # sanity: an all-(+1) state is a fixed point of every node (isolated ones included)
     ones = torch.full_like(s0, -1)
     ck = torch.zeros_like(counts)
