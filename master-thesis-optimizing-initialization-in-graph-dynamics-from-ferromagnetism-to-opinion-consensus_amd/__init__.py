@@ -11,7 +11,8 @@ from .graph import (Graph, neighbours, csr_from_networkx, random_regular_graph, 
                     erdos_renyi, erdos_renyi_edges, csr_from_edges, remove_isolated,
                     random_regular_rows_device, random_regular_graph_device, erdos_renyi_device, check_ell)
 from .partition import BinnedPlan, NodeRange, ShardedRRG, pack_host, unpack_host
-from .npz import save_sa_npz, save_hpr_npz, save_bdcm_npz, sa_arrays, hpr_arrays
+from .npz import (save_sa_npz, save_hpr_npz, save_bdcm_npz, sa_arrays, hpr_arrays, neighbour_arrays,
+                  graphs_from_npz)
 from .dynamics import onestep_majority, s_endstate, m, pack, unpack, rollout, popcount, as_graph
 from .sa import SAReplicas, E_delta, sa_run, schedule_constants
 from .hpr import HPRPlan, HPRState, HPr_dp, marginals_comp, new_biases_i, hpr_run
@@ -22,7 +23,7 @@ from .bdcm import converge as bdcm_converge
 from . import drop_in  # reference-signature HPR drop-ins (code/HPR_pytorch_RRG.py)
 
 __all__ = [
-    "MjxError", "lib_path", "BinnedPlan", "Graph", "neighbours", "csr_from_networkx", "random_regular_graph",
+    "MjxError", "lib_path", "BinnedPlan", "neighbour_arrays", "graphs_from_npz", "Graph", "neighbours", "csr_from_networkx", "random_regular_graph",
     "random_regular_edges", "erdos_renyi", "erdos_renyi_device", "erdos_renyi_edges", "csr_from_edges", "remove_isolated",
     "onestep_majority", "s_endstate", "m", "pack", "unpack", "rollout", "popcount", "as_graph",
     "SAReplicas", "E_delta", "sa_run", "schedule_constants",

@@ -39,3 +39,26 @@ def test_hpr_npz_matches_reference_file(mjx_mod, tmp_path):
             assert z[k].dtype == ref[k].dtype, k
             assert np.array_equal(z[k], ref[k]), k
         assert float(z["time"]) == 1.5
+
+
+def test_graphs_round_trip_through_result_files(mjx_mod, tmp_path):
+    """The `graphs` of the reference's own result files (int from SA_RRG.py,
+    float64 from HPR_pytorch_RRG.py) come back as (n, d) int32 neighbour
+    arrays equal to the arrays the scripts used, and survive a write."""
+    for name, key in (("sa_fullscript.npz", "n200_d4_p3"), ("hpr_fullscript.npz", "n40_d4_p1c1")):
+        ref = _ref_arrays(load_golden(name), key)
+        got = mjx_mod.neighbour_arrays({"graphs": ref["graphs"]})
+        assert len(got) == ref["graphs"].shape[0]
+        for a, b in zip(got, ref["graphs"]):
+            assert a.dtype == np.int32 and np.array_equal(a, b)
+        path = tmp_path / f"{key}.npz"
+        np.savez(path, graphs=ref["graphs"])
+        again = mjx_mod.neighbour_arrays(path)
+        assert all(np.array_equal(a, b) for a, b in zip(again, got))
+    bad = {"graphs": np.array([[[0.5, 1.0]]])}
+    try:
+        mjx_mod.neighbour_arrays(bad)
+    except ValueError:
+        pass
+    else:
+        raise AssertionError("non-integral node ids accepted")

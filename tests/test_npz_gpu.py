@@ -56,3 +56,18 @@ def test_bdcm_er_run_to_npz_has_the_notebook_layout(mjx_mod, tmp_path):
         assert np.all((m0 > 0) & (m0 <= 1))
         np.testing.assert_allclose(z["ent1"][:, :, 0], z["ent"][:, :, 0], rtol=0, atol=1e-12)
         assert np.array_equal(z["prob"], np.asarray(deg) / 299)
+
+
+def test_graphs_from_result_file_run_the_dynamics(mjx_mod, tmp_path):
+    """A graph read back from a reference result file drives the device
+    dynamics exactly like the neighbour array the script used."""
+    from oracle import majority as orc
+    full = load_golden("sa_fullscript.npz")
+    adj = full["n200_d4_p3_graphs"]
+    path = tmp_path / "g.npz"
+    np.savez(path, graphs=adj)
+    graphs = mjx_mod.graphs_from_npz(path)
+    s0 = 2 * np.random.default_rng(3).integers(0, 2, (8, adj.shape[1])).astype(np.int64) - 1
+    for g, a in zip(graphs, adj):
+        got = mjx_mod.s_endstate(g, s0, 3, 1)
+        assert np.array_equal(got, orc.s_endstate_batch(a.astype(np.int64), s0, 3, 1))
