@@ -367,6 +367,12 @@ constexpr int LC_MAXD = 16;
 
 struct LcLevels {
     u64* s[LC_MAXT + 1];     // s[0] = current configuration, s[t] = onestep^t(s[0])
+    // word (node v, column col) of level t at s[t] + v * ns + col * cs: ns = W,
+    // cs = 1 for separate level arrays; ns = W * LV, cs = LV for the cone
+    // layout, whose levels of one (node, column) share a 32-B sector
+    int64_t ns;
+    int64_t cs;
+    u64* s0c;                // cone layout: the configuration's own array (level-0 flips mirrored), else null
     int off[LC_MAXT + 2];    // list slot offset of level t; off[T+1] = candidate list
     int tab;                 // slot offset of the ball table (node ids | adjacency rows | candidate entries)
     int ball;                // table capacity: nodes of the radius-T ball (d-regular bound)
@@ -893,6 +899,7 @@ __global__ void __launch_bounds__(64) k_sa_lightcone(const int32_t* __restrict__
     const int64_t r = col * 64 + rl;
     const bool live = lane < per && r < R;
     const u64 bit = 1ull << (rl & 63);
+    const int64_t NS = L.ns, colo = col * L.cs;     // level word addressing (separate arrays or cone)
     uint32_t* lists = lc_lists + lane;
     WaveMT g{st.mt, twist_buf, r, live ? st.mt_idx[r] : MT_N, lane};
     double a = live ? st.a[r] : 0.0, b = live ? st.b[r] : 0.0;
@@ -981,16 +988,16 @@ __global__ void __launch_bounds__(64) k_sa_lightcone(const int32_t* __restrict__
                 bool done_tree = false;
                 if constexpr (D <= 4) {
                     if (pre && simple && T <= 2)
-                        done_tree = lc_tree2<D>(adj, W, col, bit, T, L, lists, (int32_t)i, cnt, &old_i, A0, A1, ds);
+                        done_tree = lc_tree2<D>(adj, NS, colo, bit, T, L, lists, (int32_t)i, cnt, &old_i, A0, A1, ds);
                 }
                 if (done_tree) {
                 } else if (pre && simple)
-                    ds = lc_delta_mlp<D, true>(adj, W, col, bit, T, L, lists, (int32_t)i, cnt, &old_i, A0, A1);
+                    ds = lc_delta_mlp<D, true>(adj, NS, colo, bit, T, L, lists, (int32_t)i, cnt, &old_i, A0, A1);
                 else if (L.tab >= 0)
-                    ds = lc_delta_mlp<D, false>(adj, W, col, bit, T, L, lists, (int32_t)i, cnt, &old_i, A0, A1);
-                else ds = lc_delta<D>(adj, d, W, col, bit, T, L, lists, (int32_t)i, cnt, &old_i);
+                    ds = lc_delta_mlp<D, false>(adj, NS, colo, bit, T, L, lists, (int32_t)i, cnt, &old_i, A0, A1);
+                else ds = lc_delta<D>(adj, d, NS, colo, bit, T, L, lists, (int32_t)i, cnt, &old_i);
             } else {
-                ds = lc_delta<D>(adj, d, W, col, bit, T, L, lists, (int32_t)i, cnt, &old_i);
+                ds = lc_delta<D>(adj, d, NS, colo, bit, T, L, lists, (int32_t)i, cnt, &old_i);
             }
             const int64_t sum_new = sum_end + ds;
             // delta_H (code/SA_RRG.py:37), same operation order, no contraction
@@ -1007,7 +1014,9 @@ __global__ void __launch_bounds__(64) k_sa_lightcone(const int32_t* __restrict__
                     const uint32_t* lst = lists + L.off[lv] * 64;
                     for (int q = 0; q < cnt[lv]; ++q) {
                         const int64_t j = (int64_t)(lst[q * 64] & 0x7fffffffu);
-                        atomicXor((unsigned long long*)(L.s[lv] + j * W + col), (unsigned long long)bit);
+                        atomicXor((unsigned long long*)(L.s[lv] + j * NS + colo), (unsigned long long)bit);
+                        if (lv == 0 && L.s0c)
+                            atomicXor((unsigned long long*)(L.s0c + j * W + col), (unsigned long long)bit);
                     }
                 }
                 sum_end = sum_new;
@@ -1215,14 +1224,11 @@ extern "C" int mjx_sa_lightcone_prepare(const int32_t* adj, int64_t n, int d, in
     return MJX_OK;
 }
 
-extern "C" int mjx_sa_lightcone_steps(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R, uint64_t* s,
-                                      uint64_t* const* levels, mjx_sa_state* stp, int64_t nsteps, double par_a,
-                                      double par_b, double a_cap, double b_cap, int64_t t_cap, void* stream) {
-    const int T = p + c - 1;
-    if (!stp || !adj || !s || !levels || n < 2 || R < 1 || d < 1 || d > LC_MAXD || nsteps < 0) return MJX_EINVAL;
-    if (T < 1 || T > LC_MAXT) return MJX_ERANGE;
-    if (n > (int64_t)INT32_MAX) return MJX_ERANGE;
-    LcLevels L;
+// Shared body of the two light-cone entry points: L.s / ns / cs / s0c set by
+// the caller (separate level arrays or the cone layout).
+static int lc_steps(const int32_t* adj, int64_t n, int d, int T, int64_t R, LcLevels L, mjx_sa_state* stp,
+                    int64_t nsteps, double par_a, double par_b, double a_cap, double b_cap, int64_t t_cap,
+                    void* stream) {
     int slots = -1;
     L.tab = -1;
     L.ball = 0;
@@ -1233,11 +1239,6 @@ extern "C" int mjx_sa_lightcone_steps(const int32_t* adj, int64_t n, int d, int 
     if (L.tab < 0) slots = lc_slots(d, T, L.off);
     const size_t lds = (size_t)slots * 64 * 4;
     if (slots < 0 || lds > kLcLdsMax) return MJX_ERANGE;
-    L.s[0] = (u64*)s;
-    for (int t = 1; t <= T; ++t) {
-        if (!levels[t - 1]) return MJX_EINVAL;
-        L.s[t] = (u64*)levels[t - 1];
-    }
     for (int t = T + 1; t <= LC_MAXT; ++t) L.s[t] = nullptr;
     if (nsteps == 0) return MJX_OK;
     const int64_t W = (R + 63) / 64;
@@ -1278,4 +1279,103 @@ extern "C" int mjx_sa_lightcone_steps(const int32_t* adj, int64_t n, int d, int 
         case 6: return run(k_sa_lightcone<6, false>, k_sa_lightcone<6, true>);
         default: return run(k_sa_lightcone<0, false>, k_sa_lightcone<0, true>);
     }
+}
+
+extern "C" int mjx_sa_lightcone_steps(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R, uint64_t* s,
+                                      uint64_t* const* levels, mjx_sa_state* stp, int64_t nsteps, double par_a,
+                                      double par_b, double a_cap, double b_cap, int64_t t_cap, void* stream) {
+    const int T = p + c - 1;
+    if (!stp || !adj || !s || !levels || n < 2 || R < 1 || d < 1 || d > LC_MAXD || nsteps < 0) return MJX_EINVAL;
+    if (T < 1 || T > LC_MAXT) return MJX_ERANGE;
+    if (n > (int64_t)INT32_MAX) return MJX_ERANGE;
+    LcLevels L;
+    L.s[0] = (u64*)s;
+    for (int t = 1; t <= T; ++t) {
+        if (!levels[t - 1]) return MJX_EINVAL;
+        L.s[t] = (u64*)levels[t - 1];
+    }
+    L.ns = (R + 63) / 64;
+    L.cs = 1;
+    L.s0c = nullptr;
+    return lc_steps(adj, n, d, T, R, L, stp, nsteps, par_a, par_b, a_cap, b_cap, t_cap, stream);
+}
+
+// ---------------------------------------------------------------------------
+// Cone layout: the T+1 level words of one (node, word column) side by side,
+// padded to LV = 2, 4 or 8 words, so the evaluation of a proposal that reads
+// several levels of one node fetches one sector instead of one line per level
+// (configs[1]: ~35 -> ~22 random line fetches per proposal).
+// ---------------------------------------------------------------------------
+static int cone_lv(int T) { return (T + 1 <= 2) ? 2 : (T + 1 <= 4) ? 4 : 8; }
+
+extern "C" int mjx_sa_cone_words(int p, int c) {
+    const int T = p + c - 1;
+    if (T < 1 || T > LC_MAXT) return -1;
+    return cone_lv(T);
+}
+
+struct ConeSrc {
+    const u64* s[LC_MAXT + 1];
+};
+
+template <bool PACK>
+__global__ void __launch_bounds__(kBlock) k_cone_xfer(int64_t words, int T, int LV, ConeSrc src, u64* cone) {
+    for (int64_t w = (int64_t)blockIdx.x * kBlock + threadIdx.x; w < words; w += (int64_t)gridDim.x * kBlock) {
+        u64* dst = cone + w * LV;
+        if constexpr (PACK) {
+            for (int t = 0; t < LV; t += 2) {
+                const u64 a = (t <= T) ? src.s[t][w] : 0ull;
+                const u64 b = (t + 1 <= T) ? src.s[t + 1][w] : 0ull;
+                *reinterpret_cast<ulonglong2*>(dst + t) = make_ulonglong2(a, b);
+            }
+        } else {
+            for (int t = 0; t <= T; ++t) const_cast<u64*>(src.s[t])[w] = dst[t];
+        }
+    }
+}
+
+static int cone_xfer(bool pack, int64_t n, int p, int c, int64_t R, const uint64_t* s, uint64_t* const* levels,
+                     uint64_t* cone, void* stream) {
+    const int T = p + c - 1;
+    if (!s || !levels || !cone || n < 1 || R < 1) return MJX_EINVAL;
+    if (T < 1 || T > LC_MAXT) return MJX_ERANGE;
+    ConeSrc src;
+    src.s[0] = (const u64*)s;
+    for (int t = 1; t <= T; ++t) {
+        if (!levels[t - 1]) return MJX_EINVAL;
+        src.s[t] = (const u64*)levels[t - 1];
+    }
+    for (int t = T + 1; t <= LC_MAXT; ++t) src.s[t] = nullptr;
+    const int64_t words = n * ((R + 63) / 64);
+    const int grid = grid_for(words);
+    if (pack) k_cone_xfer<true><<<grid, kBlock, 0, as_stream(stream)>>>(words, T, cone_lv(T), src, (u64*)cone);
+    else k_cone_xfer<false><<<grid, kBlock, 0, as_stream(stream)>>>(words, T, cone_lv(T), src, (u64*)cone);
+    MJX_LAUNCH_CHECK("k_cone_xfer");
+    return MJX_OK;
+}
+
+extern "C" int mjx_sa_cone_pack(int64_t n, int p, int c, int64_t R, const uint64_t* s, uint64_t* const* levels,
+                                uint64_t* cone, void* stream) {
+    return cone_xfer(true, n, p, c, R, s, levels, cone, stream);
+}
+
+extern "C" int mjx_sa_cone_unpack(int64_t n, int p, int c, int64_t R, const uint64_t* cone, uint64_t* s,
+                                  uint64_t* const* levels, void* stream) {
+    return cone_xfer(false, n, p, c, R, s, levels, const_cast<uint64_t*>(cone), stream);
+}
+
+extern "C" int mjx_sa_cone_steps(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R, uint64_t* s,
+                                 uint64_t* cone, mjx_sa_state* stp, int64_t nsteps, double par_a, double par_b,
+                                 double a_cap, double b_cap, int64_t t_cap, void* stream) {
+    const int T = p + c - 1;
+    if (!stp || !adj || !s || !cone || n < 2 || R < 1 || d < 1 || d > LC_MAXD || nsteps < 0) return MJX_EINVAL;
+    if (T < 1 || T > LC_MAXT) return MJX_ERANGE;
+    if (n > (int64_t)INT32_MAX) return MJX_ERANGE;
+    const int LV = cone_lv(T);
+    LcLevels L;
+    for (int t = 0; t <= T; ++t) L.s[t] = (u64*)cone + t;
+    L.ns = ((R + 63) / 64) * LV;
+    L.cs = LV;
+    L.s0c = (u64*)s;
+    return lc_steps(adj, n, d, T, R, L, stp, nsteps, par_a, par_b, a_cap, b_cap, t_cap, stream);
 }

@@ -47,10 +47,13 @@ class SAReplicas:
     """R bit-packed SA replicas on one random regular graph (device resident)."""
 
     def __init__(self, N, p, c, seeds, par_a=PAR_A, par_b=PAR_B, a0=None, b0=None, mode="auto", tape=1024,
-                 mt_state=None):
+                 mt_state=None, layout="cone"):
         """``mt_state`` = (mt uint32 (R, 624), idx int32 (R,)): continue these
         MT19937 streams instead of seeding (``seeds`` then only fixes R); see
-        ``mt_state()`` and ``sa_run(stream="global")``."""
+        ``mt_state()`` and ``sa_run(stream="global")``.  ``layout`` (light-cone
+        mode): ``"cone"`` keeps the cached levels of one (node, word) side by
+        side (mjx_sa_cone_steps), ``"levels"`` as separate arrays
+        (mjx_sa_lightcone_steps); same results."""
         self.graph = as_graph(N)
         if self.graph.kind != "ell":
             raise ValueError("SA runs on random regular graphs (ELL adjacency), code/SA_RRG.py:59-61")
@@ -118,12 +121,21 @@ class SAReplicas:
         if mode not in ("lightcone", "rollout"):
             raise ValueError(f"unknown SA mode {mode!r}")
         self.mode = mode
+        if layout not in ("cone", "levels"):
+            raise ValueError(f"unknown light-cone layout {layout!r}")
+        self.layout = layout if mode == "lightcone" else None
+        self.cone = None
         if mode == "lightcone":
             # levels s_1..s_T = onestep^t(s); the rollout ping-pong buffers are reused
-            self.levels = [self.tmp1, self.tmp2][:T] + [torch.empty_like(self.s) for _ in range(T - 2)]
-            self._lvl = (_lib.ctypes.c_void_p * T)(*[t.data_ptr() for t in self.levels])
+            self._levels = [self.tmp1, self.tmp2][:T] + [torch.empty_like(self.s) for _ in range(T - 2)]
+            self._lvl = (_lib.ctypes.c_void_p * T)(*[t.data_ptr() for t in self._levels])
             _lib.call("mjx_sa_lightcone_prepare", _device.ptr(self.graph.adj), n, self.graph.d, self.p, self.c, R,
                       _device.ptr(self.s), self._lvl, _device.stream_handle())
+            if layout == "cone":
+                lv = _lib.load().mjx_sa_cone_words(self.p, self.c)
+                self.cone = torch.empty(n * W * lv, dtype=i64, device=dev)
+                _lib.call("mjx_sa_cone_pack", n, self.p, self.c, R, _device.ptr(self.s), self._lvl,
+                          _device.ptr(self.cone), _device.stream_handle())
             # proposal tape: (i, u) of `tape` steps per replica drawn ahead by
             # a wave per replica (0 = draw inside the step kernel)
             self.tape_cap = int(tape) if tape else 0
@@ -154,7 +166,11 @@ class SAReplicas:
         else:
             st.tr_i = st.tr_acc = st.tr_sum = st.tr_dE = None
         T = self.p + self.c - 1
-        if self.mode == "lightcone":
+        if self.mode == "lightcone" and self.cone is not None:
+            _lib.call("mjx_sa_cone_steps", _device.ptr(self.graph.adj), self.n, self.graph.d, self.p, self.c,
+                      self.R, _device.ptr(self.s), _device.ptr(self.cone), _lib.ctypes.byref(st), k, self.par_a,
+                      self.par_b, self.a_cap, self.b_cap, int(self.t_cap), _device.stream_handle())
+        elif self.mode == "lightcone":
             _lib.call("mjx_sa_lightcone_steps", _device.ptr(self.graph.adj), self.n, self.graph.d, self.p, self.c,
                       self.R, _device.ptr(self.s), self._lvl, _lib.ctypes.byref(st), k, self.par_a, self.par_b,
                       self.a_cap, self.b_cap, int(self.t_cap), _device.stream_handle())
@@ -165,6 +181,30 @@ class SAReplicas:
                       int(self.t_cap), _device.stream_handle())
         st.tr_i = st.tr_acc = st.tr_sum = st.tr_dE = None
         return tr
+
+    @property
+    def levels(self):
+        """The cached levels onestep^t(s), t = 1..T, as separate (n*W,) arrays
+        (unpacked from the cone layout when that is in use)."""
+        if self.mode != "lightcone":
+            raise AttributeError("levels exist in the light-cone mode only")
+        self._unpack_cone()
+        return self._levels
+
+    def cone_level0(self):
+        """Level 0 as the cone holds it (equal to ``s`` after every step)."""
+        if self.cone is None:
+            raise AttributeError("no cone layout in use")
+        self._unpack_cone()
+        return self._s0buf
+
+    def _unpack_cone(self):
+        if self.cone is None:
+            return
+        if getattr(self, "_s0buf", None) is None:
+            self._s0buf = torch.empty_like(self.s)
+        _lib.call("mjx_sa_cone_unpack", self.n, self.p, self.c, self.R, _device.ptr(self.cone),
+                  _device.ptr(self._s0buf), self._lvl, _device.stream_handle())
 
     def all_done(self):
         return bool((self.done != 0).all().item())

@@ -100,9 +100,32 @@ def test_sa_lightcone_levels_stay_consistent(mjx_mod, d, p, c):
     for lvl in sa.levels:
         cur = mjx_mod.rollout(g, cur, 1, words=W)
         assert torch.equal(cur, lvl)
+    assert torch.equal(sa.cone_level0(), sa.s)       # level 0 of the cone mirrors s
     cnt = torch.zeros(64 * W, dtype=torch.int64, device="cuda")
     mjx_mod.rollout(g, sa.s, p + c - 1, words=W, counts=cnt)
     assert torch.equal(2 * cnt[:sa.R] - n, sa.sum_end)
+
+
+@pytest.mark.parametrize("d,p,c", [(3, 2, 1), (4, 1, 1), (4, 2, 2), (5, 1, 2), (3, 3, 4)])
+def test_sa_cone_layout_equals_separate_levels(mjx_mod, d, p, c):
+    """The cone layout (levels of one (node, word) side by side) gives the
+    same proposals, accepts, sums and delta_H as separate level arrays, and
+    the same final configuration and levels (LV = 2, 4 and 8 words)."""
+    n = 3000
+    adj = mjx_mod.random_regular_graph(d, n, seed=4)
+    R = 150
+    a = mjx_mod.SAReplicas(adj, p, c, list(range(R)), mode="lightcone", layout="cone")
+    b = mjx_mod.SAReplicas(adj, p, c, list(range(R)), mode="lightcone", layout="levels")
+    assert a.cone is not None and b.cone is None
+    for k in (7, 600, 1500):
+        ta, tb = a.steps(k, trace=True), b.steps(k, trace=True)
+        for key in ("i", "accept", "sum_end", "dE"):
+            assert torch.equal(ta[key], tb[key]), key
+    assert torch.equal(a.s, b.s)
+    for la, lb in zip(a.levels, b.levels):
+        assert torch.equal(la, lb)
+    for f in ("a", "b", "t", "sum_end", "done", "ties"):
+        assert torch.equal(getattr(a, f), getattr(b, f)), f
 
 
 def test_sa_run_matches_full_reference_script(mjx_mod):
