@@ -206,20 +206,24 @@ int mjx_sa_lightcone_steps(const int32_t* adj, int64_t n, int d, int p, int c, i
 
 /* Cone layout of the cached levels: the T+1 words (s, onestep(s), ...,
  * onestep^T(s)) of one (node, word column) side by side, padded to
- * LV = mjx_sa_cone_words(p,c) words (2, 4 or 8; -1 if unsupported), so
- * cone[(v*W + w)*LV + t] = level t, word w of node v (n*W*LV words).  A
+ * LV = mjx_sa_cone_words(p,c) words (2, 4 or 8; -1 if unsupported), word
+ * column major: cone[(w*n + v)*LV + t] = level t, word w of node v (n*W*LV
+ * words).  A
  * proposal reads several levels of the same nodes; here they share one
  * memory sector.  mjx_sa_cone_pack builds the cone from s and the separate
  * levels (after mjx_sa_lightcone_prepare); mjx_sa_cone_steps is
  * mjx_sa_lightcone_steps on the cone (same proposals, accepts and outputs),
  * mirroring every accepted level-0 flip into s so s stays the configuration;
- * mjx_sa_cone_unpack writes the cone back to s and the separate levels. */
+ * mjx_sa_cone_unpack writes the cone back to s and the separate levels.
+ * adj_pad (optional, d = 3): the adjacency with rows padded to 4 int32
+ * (n*4, 16-B aligned); with it, p+c-1 = 2 and a proposal tape, every proposal
+ * costs one memory round trip (rows fetched down the tape ahead of time). */
 int mjx_sa_cone_words(int p, int c);
 int mjx_sa_cone_pack(int64_t n, int p, int c, int64_t R, const uint64_t* s,
                      uint64_t* const* levels, uint64_t* cone, void* stream);
 int mjx_sa_cone_unpack(int64_t n, int p, int c, int64_t R, const uint64_t* cone,
                        uint64_t* s, uint64_t* const* levels, void* stream);
-int mjx_sa_cone_steps(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R,
+int mjx_sa_cone_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d, int p, int c, int64_t R,
                       uint64_t* s, uint64_t* cone, mjx_sa_state* st, int64_t nsteps,
                       double par_a, double par_b, double a_cap, double b_cap, int64_t t_cap,
                       void* stream);

@@ -49,7 +49,7 @@ SIGNATURES = {
     "mjx_sa_cone_words": [c_int, c_int],
     "mjx_sa_cone_pack": [c_i64, c_int, c_int, c_i64, c_vp, c_vp, c_vp, c_vp],
     "mjx_sa_cone_unpack": [c_i64, c_int, c_int, c_i64, c_vp, c_vp, c_vp, c_vp],
-    "mjx_sa_cone_steps": [c_vp, c_i64, c_int, c_int, c_int, c_i64, c_vp, c_vp, c_vp,
+    "mjx_sa_cone_steps": [c_vp, c_vp, c_i64, c_int, c_int, c_int, c_i64, c_vp, c_vp, c_vp,
                           c_i64, c_dbl, c_dbl, c_dbl, c_dbl, c_i64, c_vp],
     "mjx_hpr_update": [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_int,
                        c_dbl, c_dbl, c_dbl, c_vp],

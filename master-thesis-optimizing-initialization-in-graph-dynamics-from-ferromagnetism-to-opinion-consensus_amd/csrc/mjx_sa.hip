@@ -894,8 +894,8 @@ __global__ void __launch_bounds__(64) k_sa_lightcone(const int32_t* __restrict__
     // latency, so more, thinner waves carry more replicas per unit of time
     const int lane = threadIdx.x;
     const int per = 64 / split;
-    const int64_t col = blockIdx.x / split;
-    const int rl = (int)(blockIdx.x % split) * per + lane;    // bit of this lane's replica in the column
+    const int64_t col = blockIdx.x % W;                       // a column's waves on one XCD when W % 8 == 0
+    const int rl = (int)(blockIdx.x / W) * per + lane;        // bit of this lane's replica in the column
     const int64_t r = col * 64 + rl;
     const bool live = lane < per && r < R;
     const u64 bit = 1ull << (rl & 63);
@@ -1063,6 +1063,279 @@ __global__ void __launch_bounds__(64) k_sa_lightcone(const int32_t* __restrict__
 
 // list slots per lane: levels 0..T (ball bounds) + candidate list; with
 // `table` also the ball table of lc_delta_mlp (node ids, rows, candidates)
+// ---------------------------------------------------------------------------
+// Light-cone step on the cone layout with one memory round trip per proposal
+// (p+c-1 = 2, d = 3 and the proposal tape).  Adjacency rows are fetched in a
+// pipeline down the tape -- at step k the row of i_{k+3}, the rows of the
+// neighbours of i_{k+2} and the rows of the children of i_{k+1} -- so when step
+// k starts every node of i_k's radius-3 tree is known, and ONE batch loads the
+// level sectors (s_0, s_1, s_2) of i, its neighbours a_m and their children and
+// the level-1 words of the grandchildren.  The evaluation is lc_tree2's with
+// every value in a register, the change sets are bit masks over the tree's
+// positions (flips straight from registers, no lists), and balls that are not
+// trees fall back to lc_delta_mlp (lists in LDS).  Same accept sequence.
+// ---------------------------------------------------------------------------
+template <int D>
+__global__ void __launch_bounds__(64) k_sa_cone2(const int32_t* __restrict__ adj, const int4* __restrict__ adj_pad,
+                                                 int64_t n, int64_t R, int64_t W,
+                                                 LcLevels L, mjx_sa_state st, int64_t nsteps, double par_a,
+                                                 double par_b, double a_cap, double b_cap, int64_t t_cap,
+                                                 const int32_t* __restrict__ tape_i,
+                                                 const double* __restrict__ tape_u, int split) {
+    extern __shared__ uint32_t lc_lists[];
+    constexpr int T = 2;
+    const int lane = threadIdx.x;
+    const int per = 64 / split;
+    const int64_t col = blockIdx.x % W;                       // a column's waves on one XCD when W % 8 == 0
+    const int rl = (int)(blockIdx.x / W) * per + lane;
+    const int64_t r = col * 64 + rl;
+    const bool live = lane < per && r < R;
+    const u64 bit = 1ull << (rl & 63);
+    const int64_t NS = L.ns, colo = col * L.cs;
+    const u64* cone = L.s[0];                                 // level t of (v, col) at cone + v*NS + colo + t
+    uint32_t* lists = lc_lists + lane;
+    double a = live ? st.a[r] : 0.0, b = live ? st.b[r] : 0.0;
+    int64_t t = live ? st.t[r] : 0, sum_end = live ? st.sum_end[r] : 0;
+    int done = live ? st.done[r] : 1;
+    int ties = 0;
+    const bool run = live && done == 0;
+    static_assert(D == 3, "rows are read as one 16-B load from the padded adjacency");
+    auto row = [&](int32_t v, int32_t (&o)[D]) {
+        const int4 q = adj_pad[(uint32_t)v < (uint32_t)n ? v : 0];             // never out of bounds
+        o[0] = q.x; o[1] = q.y; o[2] = q.z;
+    };
+    auto tape = [&](int64_t k, int32_t& iv, double& uv) {
+        iv = 0; uv = 0.0;
+        if (run && k < nsteps) { iv = tape_i[k * R + r]; uv = tape_u[k * R + r]; }
+    };
+    // pipeline registers: tape (i, u) of k+1..k+3; row of i_{k+1}, i_{k+2};
+    // rows of N(i_{k+1}); current rows of i_k, N(i_k), children of i_k
+    int32_t ti1, ti2, ti3, ti0;
+    double tu1, tu2, tu3, tu0;
+    int32_t Q1[D], Q2[D], N1[D][D], A0[D], A1[D][D], C[D][D][D];
+    tape(0, ti0, tu0); tape(1, ti1, tu1); tape(2, ti2, tu2); tape(3, ti3, tu3);
+    row(ti0, A0); row(ti1, Q1); row(ti2, Q2);
+#pragma unroll
+    for (int m = 0; m < D; ++m) { row(A0[m], A1[m]); row(Q1[m], N1[m]); }
+#pragma unroll
+    for (int m = 0; m < D; ++m)
+#pragma unroll
+        for (int x = 0; x < D; ++x) row(A1[m][x], C[m][x]);
+    // plain (cacheable) loads: a lane's own bit of a word changes only by its
+    // own atomics, which a later load of the same lane sees (the bit-exact
+    // tests re-read just-flipped words constantly); other lanes' bits may be
+    // stale and are never used
+    auto w = [&](int32_t v, int lv) { return cone[(int64_t)v * NS + colo + lv]; };
+    auto sector = [&](int32_t v, u64 (&o)[3]) {
+        const u64* p = cone + (int64_t)v * NS + colo;
+        const ulonglong2 q = *reinterpret_cast<const ulonglong2*>(p);
+        o[0] = q.x; o[1] = q.y; o[2] = p[2];
+    };
+    auto bv = [&](u64 x) -> uint32_t { return (x & bit) ? 1u : 0u; };
+    auto maj = [&](int ones, uint32_t own) -> uint32_t { return (2 * ones > D) ? 1u : ((2 * ones < D) ? 0u : own); };
+    for (int64_t step = 0; step < nsteps; ++step) {
+        const bool active = run && done == 0;
+        const int32_t i = ti0;
+        const double u = tu0;
+        // prefetch stage: tape k+4, row of i_{k+3}, rows of N(i_{k+2}), rows of the children of i_{k+1}
+        int32_t ti4; double tu4;
+        tape(step + 4, ti4, tu4);
+        int32_t Q3[D], N2[D][D], Cn[D][D][D];
+        row(ti3, Q3);
+#pragma unroll
+        for (int m = 0; m < D; ++m) row(Q2[m], N2[m]);
+#pragma unroll
+        for (int m = 0; m < D; ++m)
+#pragma unroll
+            for (int x = 0; x < D; ++x) row(N1[m][x], Cn[m][x]);
+        if (active) {
+            // the tree shape (lc_tree2): i, the a_m and their children all distinct
+            bool ok = true;
+#pragma unroll
+            for (int m = 0; m < D; ++m) {
+                int ci = 0;
+#pragma unroll
+                for (int x = 0; x < D; ++x) ci += (A1[m][x] == i);
+                ok &= (ci == 1) && (A0[m] != i);
+#pragma unroll
+                for (int m2 = m + 1; m2 < D; ++m2) ok &= A0[m] != A0[m2];
+            }
+#pragma unroll
+            for (int m = 0; m < D; ++m)
+#pragma unroll
+                for (int x = 0; x < D; ++x) {
+                    const int32_t cc = A1[m][x];
+                    if (cc == i) continue;
+#pragma unroll
+                    for (int m2 = 0; m2 < D; ++m2) ok &= (cc != A0[m2]);
+#pragma unroll
+                    for (int m2 = m; m2 < D; ++m2)
+#pragma unroll
+                        for (int x2 = 0; x2 < D; ++x2)
+                            if (m2 > m || x2 > x) ok &= (A1[m2][x2] == i) || (A1[m2][x2] != cc);
+                }
+            int old_i = 0;
+            int64_t ds = 0;
+            uint32_t ch1 = 0, nv1 = 0, ch2 = 0;                 // positions: 0 = i, 1+m = a_m, 1+D+m*D+x = child
+            if (ok) {
+                // the one batch: sectors of i, a_m, children; level-1 words of the grandchildren
+                u64 wi[3], wa[D][3], wc[D][D][3], wg[D][D][D];
+                sector(i, wi);
+#pragma unroll
+                for (int m = 0; m < D; ++m) {
+                    sector(A0[m], wa[m]);
+#pragma unroll
+                    for (int x = 0; x < D; ++x) {
+                        const bool child = A1[m][x] != i;
+                        wc[m][x][0] = wc[m][x][1] = wc[m][x][2] = 0ull;
+                        if (child) sector(A1[m][x], wc[m][x]);
+#pragma unroll
+                        for (int y = 0; y < D; ++y)
+                            wg[m][x][y] = (child && C[m][x][y] != A0[m]) ? w(C[m][x][y], 1) : 0ull;
+                    }
+                }
+                // level 1 (lc_tree2)
+                const uint32_t f = bv(wi[0]) ^ 1u;
+                old_i = (int)bv(wi[0]);
+                {
+                    int ones = 0;
+#pragma unroll
+                    for (int m = 0; m < D; ++m) ones += (int)bv(wa[m][0]);
+                    const uint32_t nb = maj(ones, f);
+                    if (nb != bv(wi[1])) { ch1 |= 1u; nv1 |= nb; }
+                }
+#pragma unroll
+                for (int m = 0; m < D; ++m) {
+                    int ones = 0;
+#pragma unroll
+                    for (int x = 0; x < D; ++x) ones += (int)((A1[m][x] == i) ? f : bv(wc[m][x][0]));
+                    const uint32_t nb = maj(ones, bv(wa[m][0]));
+                    if (nb != bv(wa[m][1])) { ch1 |= 2u << m; nv1 |= nb << (1 + m); }
+                }
+                // level 2
+                const bool c0 = ch1 & 1u;
+                const uint32_t vi1 = c0 ? (nv1 & 1u) : bv(wi[1]);
+                int64_t acc = 0;
+                if (ch1 != 0) {
+                    int ones = 0;
+#pragma unroll
+                    for (int m = 0; m < D; ++m) ones += (int)(((ch1 >> (1 + m)) & 1u) ? ((nv1 >> (1 + m)) & 1u) : bv(wa[m][1]));
+                    const uint32_t nb = maj(ones, vi1);
+                    if (nb != bv(wi[2])) { ch2 |= 1u; acc += nb ? 2 : -2; }
+                }
+#pragma unroll
+                for (int m = 0; m < D; ++m) {
+                    const bool cm = (ch1 >> (1 + m)) & 1u;
+                    const uint32_t va1 = cm ? ((nv1 >> (1 + m)) & 1u) : bv(wa[m][1]);
+                    if (c0 || cm) {
+                        int ones = 0;
+#pragma unroll
+                        for (int x = 0; x < D; ++x) ones += (int)((A1[m][x] == i) ? vi1 : bv(wc[m][x][1]));
+                        const uint32_t nb = maj(ones, va1);
+                        if (nb != bv(wa[m][2])) { ch2 |= 2u << m; acc += nb ? 2 : -2; }
+                    }
+                    if (cm) {
+#pragma unroll
+                        for (int x = 0; x < D; ++x) {
+                            if (A1[m][x] == i) continue;
+                            int ones = 0;
+#pragma unroll
+                            for (int y = 0; y < D; ++y) ones += (int)((C[m][x][y] == A0[m]) ? va1 : bv(wg[m][x][y]));
+                            const uint32_t nb = maj(ones, bv(wc[m][x][1]));
+                            if (nb != bv(wc[m][x][2])) { ch2 |= 1u << (1 + D + m * D + x); acc += nb ? 2 : -2; }
+                        }
+                    }
+                }
+                ds = acc;
+            } else {
+                // not a tree: the batched table path (lc_delta_mlp), rows of i and
+                // its neighbours taken from the pipeline when they are distinct
+                bool simple = true;
+#pragma unroll
+                for (int m = 0; m < D; ++m) {
+                    simple &= A0[m] != i;
+#pragma unroll
+                    for (int q = m + 1; q < D; ++q) simple &= A0[m] != A0[q];
+                }
+                int cnt[LC_MAXT + 1];
+                if (simple) ds = lc_delta_mlp<D, true>(adj, NS, colo, bit, T, L, lists, i, cnt, &old_i, A0, A1);
+                else ds = lc_delta_mlp<D, false>(adj, NS, colo, bit, T, L, lists, i, cnt, &old_i, A0, A1);
+                ch1 = (uint32_t)cnt[1] | ((uint32_t)cnt[2] << 8) | 0x80000000u;   // list path marker
+            }
+            const int64_t sum_new = sum_end + ds;
+            // delta_H (code/SA_RRG.py:37), same operation order, no contraction
+            const double si = old_i ? 1.0 : -1.0;
+            const double t1 = (-2.0 * a) * si;
+            const double t2 = b * (double)(sum_end - sum_new);
+            const double dE = (t1 + t2) / (double)n;
+            const double e = exp(-dE);
+            const double prob = (e < 1.0) ? e : 1.0;                 // (code/SA_RRG.py:75)
+            const bool acc = u < prob;                               // (code/SA_RRG.py:76)
+            if (e < 1.0 && fabs(u - e) <= 4.0 * (nextafter(e, 2.0) - e)) ++ties;
+            if (acc) {                                               // (code/SA_RRG.py:77)
+                auto flip = [&](int32_t v, int lv) {
+                    atomicXor((unsigned long long*)(cone + (int64_t)v * NS + colo + lv), (unsigned long long)bit);
+                };
+                flip(i, 0);
+                atomicXor((unsigned long long*)(L.s0c + (int64_t)i * W + col), (unsigned long long)bit);
+                if (ch1 & 0x80000000u) {
+                    const int c1 = (int)(ch1 & 0xffu), c2 = (int)((ch1 >> 8) & 0xffu);
+                    for (int q = 0; q < c1; ++q) flip((int32_t)(lists[(L.off[1] + q) * 64] & 0x7fffffffu), 1);
+                    for (int q = 0; q < c2; ++q) flip((int32_t)(lists[(L.off[2] + q) * 64] & 0x7fffffffu), 2);
+                } else {
+                    if (ch1 & 1u) flip(i, 1);
+                    if (ch2 & 1u) flip(i, 2);
+#pragma unroll
+                    for (int m = 0; m < D; ++m) {
+                        if ((ch1 >> (1 + m)) & 1u) flip(A0[m], 1);
+                        if ((ch2 >> (1 + m)) & 1u) flip(A0[m], 2);
+#pragma unroll
+                        for (int x = 0; x < D; ++x)
+                            if ((ch2 >> (1 + D + m * D + x)) & 1u) flip(A1[m][x], 2);
+                    }
+                }
+                sum_end = sum_new;
+            }
+            if (a < a_cap) a = par_a * a;                            // (code/SA_RRG.py:80-81)
+            if (b < b_cap) b = par_b * b;
+            t += 1;                                                  // (code/SA_RRG.py:82)
+            if (t > t_cap) done = 2;                                 // (code/SA_RRG.py:84)
+            else if (sum_end == n) done = 1;                         // m(s_endstate(s)) == 1
+            if (st.tr_i) st.tr_i[step * R + r] = i;
+            if (st.tr_acc) st.tr_acc[step * R + r] = acc ? 1 : 0;
+            if (st.tr_sum) st.tr_sum[step * R + r] = sum_end;
+            if (st.tr_dE) st.tr_dE[step * R + r] = dE;
+        } else if (live) {
+            if (st.tr_i) st.tr_i[step * R + r] = -1;
+            if (st.tr_acc) st.tr_acc[step * R + r] = -1;
+            if (st.tr_sum) st.tr_sum[step * R + r] = sum_end;
+            if (st.tr_dE) st.tr_dE[step * R + r] = 0.0;
+        }
+        // this wave's flips must land before its next reads of the same words
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // rotate the pipeline
+        ti0 = ti1; tu0 = tu1; ti1 = ti2; tu1 = tu2; ti2 = ti3; tu2 = tu3; ti3 = ti4; tu3 = tu4;
+#pragma unroll
+        for (int m = 0; m < D; ++m) {
+            A0[m] = Q1[m]; Q1[m] = Q2[m]; Q2[m] = Q3[m];
+#pragma unroll
+            for (int x = 0; x < D; ++x) {
+                A1[m][x] = N1[m][x]; N1[m][x] = N2[m][x];
+#pragma unroll
+                for (int y = 0; y < D; ++y) C[m][x][y] = Cn[m][x][y];
+            }
+        }
+    }
+    if (live) {
+        st.a[r] = a;
+        st.b[r] = b;
+        st.t[r] = t;
+        st.sum_end[r] = sum_end;
+        st.done[r] = done;
+        if (st.tr_tie) st.tr_tie[r] += ties;
+    }
+}
+
 static int lc_slots(int d, int T, int* off, bool table = false, int* tab = nullptr, int* ballT = nullptr) {
     int64_t total = 0, ball = 1, shell = 1;
     for (int t = 0; t <= T; ++t) {
@@ -1226,7 +1499,8 @@ extern "C" int mjx_sa_lightcone_prepare(const int32_t* adj, int64_t n, int d, in
 
 // Shared body of the two light-cone entry points: L.s / ns / cs / s0c set by
 // the caller (separate level arrays or the cone layout).
-static int lc_steps(const int32_t* adj, int64_t n, int d, int T, int64_t R, LcLevels L, mjx_sa_state* stp,
+static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d, int T, int64_t R, LcLevels L,
+                    mjx_sa_state* stp,
                     int64_t nsteps, double par_a, double par_b, double a_cap, double b_cap, int64_t t_cap,
                     void* stream) {
     int slots = -1;
@@ -1257,6 +1531,17 @@ static int lc_steps(const int32_t* adj, int64_t n, int d, int T, int64_t R, LcLe
         MJX_LAUNCH_CHECK("k_sa_lightcone");
         return MJX_OK;
     };
+    // cone layout, p+c-1 = 2, d = 3 with the tape: the one-round-trip kernel
+    const bool one_trip = tape && L.s0c && adj_pad && T == 2 && d == 3 && L.tab >= 0 && !getenv("MJX_NO_CONE2");
+    auto launch_one_trip = [&](mjx_sa_state s2, int64_t k) -> int {
+        auto kern = k_sa_cone2<3>;
+        MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+                "cone2 lds");
+        kern<<<(unsigned)(W * split), 64, lds, hs>>>(adj, (const int4*)adj_pad, n, R, W, L, s2, k, par_a, par_b,
+                                                     a_cap, b_cap, t_cap, st.tape_i, st.tape_u, split);
+        MJX_LAUNCH_CHECK("k_sa_cone2");
+        return MJX_OK;
+    };
     auto run = [&](auto kern_plain, auto kern_tape) -> int {
         if (!tape) return launch(kern_plain, st, nsteps);
         for (int64_t k0 = 0; k0 < nsteps; k0 += st.tape_cap) {
@@ -1268,7 +1553,7 @@ static int lc_steps(const int32_t* adj, int64_t n, int d, int T, int64_t R, LcLe
             if (s2.tr_acc) s2.tr_acc += k0 * R;
             if (s2.tr_sum) s2.tr_sum += k0 * R;
             if (s2.tr_dE) s2.tr_dE += k0 * R;
-            const int rc = launch(kern_tape, s2, k);
+            const int rc = one_trip ? launch_one_trip(s2, k) : launch(kern_tape, s2, k);
             if (rc) return rc;
         }
         return MJX_OK;
@@ -1297,14 +1582,15 @@ extern "C" int mjx_sa_lightcone_steps(const int32_t* adj, int64_t n, int d, int 
     L.ns = (R + 63) / 64;
     L.cs = 1;
     L.s0c = nullptr;
-    return lc_steps(adj, n, d, T, R, L, stp, nsteps, par_a, par_b, a_cap, b_cap, t_cap, stream);
+    return lc_steps(adj, nullptr, n, d, T, R, L, stp, nsteps, par_a, par_b, a_cap, b_cap, t_cap, stream);
 }
 
 // ---------------------------------------------------------------------------
 // Cone layout: the T+1 level words of one (node, word column) side by side,
 // padded to LV = 2, 4 or 8 words, so the evaluation of a proposal that reads
-// several levels of one node fetches one sector instead of one line per level
-// (configs[1]: ~35 -> ~22 random line fetches per proposal).
+// several levels of one node fetches one sector instead of one line per level;
+// column-major (word column w's n sectors contiguous), so the waves of one
+// column, all on one XCD, gather from one n*LV*8-byte slab.
 // ---------------------------------------------------------------------------
 static int cone_lv(int T) { return (T + 1 <= 2) ? 2 : (T + 1 <= 4) ? 4 : 8; }
 
@@ -1319,9 +1605,10 @@ struct ConeSrc {
 };
 
 template <bool PACK>
-__global__ void __launch_bounds__(kBlock) k_cone_xfer(int64_t words, int T, int LV, ConeSrc src, u64* cone) {
+__global__ void __launch_bounds__(kBlock) k_cone_xfer(int64_t words, int T, int LV, ConeSrc src, u64* cone,
+                                                      int64_t n, int64_t W) {
     for (int64_t w = (int64_t)blockIdx.x * kBlock + threadIdx.x; w < words; w += (int64_t)gridDim.x * kBlock) {
-        u64* dst = cone + w * LV;
+        u64* dst = cone + ((w % W) * n + w / W) * LV;
         if constexpr (PACK) {
             for (int t = 0; t < LV; t += 2) {
                 const u64 a = (t <= T) ? src.s[t][w] : 0ull;
@@ -1346,10 +1633,10 @@ static int cone_xfer(bool pack, int64_t n, int p, int c, int64_t R, const uint64
         src.s[t] = (const u64*)levels[t - 1];
     }
     for (int t = T + 1; t <= LC_MAXT; ++t) src.s[t] = nullptr;
-    const int64_t words = n * ((R + 63) / 64);
+    const int64_t W = (R + 63) / 64, words = n * W;
     const int grid = grid_for(words);
-    if (pack) k_cone_xfer<true><<<grid, kBlock, 0, as_stream(stream)>>>(words, T, cone_lv(T), src, (u64*)cone);
-    else k_cone_xfer<false><<<grid, kBlock, 0, as_stream(stream)>>>(words, T, cone_lv(T), src, (u64*)cone);
+    if (pack) k_cone_xfer<true><<<grid, kBlock, 0, as_stream(stream)>>>(words, T, cone_lv(T), src, (u64*)cone, n, W);
+    else k_cone_xfer<false><<<grid, kBlock, 0, as_stream(stream)>>>(words, T, cone_lv(T), src, (u64*)cone, n, W);
     MJX_LAUNCH_CHECK("k_cone_xfer");
     return MJX_OK;
 }
@@ -1364,9 +1651,10 @@ extern "C" int mjx_sa_cone_unpack(int64_t n, int p, int c, int64_t R, const uint
     return cone_xfer(false, n, p, c, R, s, levels, const_cast<uint64_t*>(cone), stream);
 }
 
-extern "C" int mjx_sa_cone_steps(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R, uint64_t* s,
-                                 uint64_t* cone, mjx_sa_state* stp, int64_t nsteps, double par_a, double par_b,
-                                 double a_cap, double b_cap, int64_t t_cap, void* stream) {
+extern "C" int mjx_sa_cone_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d, int p, int c,
+                                 int64_t R, uint64_t* s, uint64_t* cone, mjx_sa_state* stp, int64_t nsteps,
+                                 double par_a, double par_b, double a_cap, double b_cap, int64_t t_cap,
+                                 void* stream) {
     const int T = p + c - 1;
     if (!stp || !adj || !s || !cone || n < 2 || R < 1 || d < 1 || d > LC_MAXD || nsteps < 0) return MJX_EINVAL;
     if (T < 1 || T > LC_MAXT) return MJX_ERANGE;
@@ -1374,8 +1662,8 @@ extern "C" int mjx_sa_cone_steps(const int32_t* adj, int64_t n, int d, int p, in
     const int LV = cone_lv(T);
     LcLevels L;
     for (int t = 0; t <= T; ++t) L.s[t] = (u64*)cone + t;
-    L.ns = ((R + 63) / 64) * LV;
-    L.cs = LV;
+    L.ns = LV;
+    L.cs = n * LV;
     L.s0c = (u64*)s;
-    return lc_steps(adj, n, d, T, R, L, stp, nsteps, par_a, par_b, a_cap, b_cap, t_cap, stream);
+    return lc_steps(adj, adj_pad, n, d, T, R, L, stp, nsteps, par_a, par_b, a_cap, b_cap, t_cap, stream);
 }

@@ -125,6 +125,7 @@ class SAReplicas:
             raise ValueError(f"unknown light-cone layout {layout!r}")
         self.layout = layout if mode == "lightcone" else None
         self.cone = None
+        self.adj_pad = None
         if mode == "lightcone":
             # levels s_1..s_T = onestep^t(s); the rollout ping-pong buffers are reused
             self._levels = [self.tmp1, self.tmp2][:T] + [torch.empty_like(self.s) for _ in range(T - 2)]
@@ -136,6 +137,10 @@ class SAReplicas:
                 self.cone = torch.empty(n * W * lv, dtype=i64, device=dev)
                 _lib.call("mjx_sa_cone_pack", n, self.p, self.c, R, _device.ptr(self.s), self._lvl,
                           _device.ptr(self.cone), _device.stream_handle())
+                if self.graph.d == 3:
+                    # rows padded to 16 B: one load per row in the one-round-trip step
+                    self.adj_pad = torch.zeros((n, 4), dtype=torch.int32, device=dev)
+                    self.adj_pad[:, :3] = self.graph.adj.view(n, 3)
             # proposal tape: (i, u) of `tape` steps per replica drawn ahead by
             # a wave per replica (0 = draw inside the step kernel)
             self.tape_cap = int(tape) if tape else 0
@@ -167,7 +172,8 @@ class SAReplicas:
             st.tr_i = st.tr_acc = st.tr_sum = st.tr_dE = None
         T = self.p + self.c - 1
         if self.mode == "lightcone" and self.cone is not None:
-            _lib.call("mjx_sa_cone_steps", _device.ptr(self.graph.adj), self.n, self.graph.d, self.p, self.c,
+            _lib.call("mjx_sa_cone_steps", _device.ptr(self.graph.adj),
+                      _device.ptr(self.adj_pad) if self.adj_pad is not None else None, self.n, self.graph.d, self.p, self.c,
                       self.R, _device.ptr(self.s), _device.ptr(self.cone), _lib.ctypes.byref(st), k, self.par_a,
                       self.par_b, self.a_cap, self.b_cap, int(self.t_cap), _device.stream_handle())
         elif self.mode == "lightcone":
