@@ -1336,6 +1336,343 @@ __global__ void __launch_bounds__(64) k_sa_cone2(const int32_t* __restrict__ adj
     }
 }
 
+// ---------------------------------------------------------------------------
+// Speculative batches (d = 3, p+c-1 = 2, cone layout, proposal tape): the 8
+// lanes of a lane group evaluate the next 8 proposals of ONE replica at once,
+// all against the current configuration, and the batch is then resolved in
+// proposal order.  Proposal j's evaluation reads the words of the nodes R_j of
+// its radius-3 tree; it is the one a sequential run computes unless an earlier
+// proposal of the batch may write one of those nodes, so every proposal's
+// potential writes W_k (i and the positions whose level values it changes) go
+// into a per-replica LDS hash set tagged with the smallest k, and j stands only
+// while no node of R_j carries a tag below j (a ball that is not a tree stands
+// only as the first of a batch).  The batch consumes the proposals before the
+// first that does not stand and ends after the first that finishes the replica;
+// the rest are drawn again as the next batch.  Acceptance needs no ordering
+// (the schedule a, b depends on the step count only; delta_H on the proposal's
+// own change), the stop needs a prefix sum of the accepted changes.  Two random
+// proposals on a 1e6-node graph collide with probability ~1e-4, so batches
+// almost always consume all 8: the replica's serial chain moves 8 proposals per
+// memory round trip instead of one.  Same accept sequence as the serial step.
+// ---------------------------------------------------------------------------
+constexpr int SPEC_K = 8;        // proposals per batch = lanes per replica
+constexpr int SPEC_HS = 512;     // hash slots per replica (<= 8 * 18 keys)
+
+template <int D>
+__global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj, const int4* __restrict__ adj_pad,
+                                                int64_t n, int64_t R, int64_t W, LcLevels L, mjx_sa_state st,
+                                                int64_t nsteps, double par_a, double par_b, double a_cap,
+                                                double b_cap, int64_t t_cap, const int32_t* __restrict__ tape_i,
+                                                const double* __restrict__ tape_u, int hoff) {
+    static_assert(D == 3, "rows are read as one 16-B load from the padded adjacency");
+    extern __shared__ uint32_t lc_lists[];
+    constexpr int T = 2, K = SPEC_K;
+    const int lane = threadIdx.x;
+    const int g = lane / K, k = lane % K;
+    const int64_t col = blockIdx.x % W;                       // a column's waves on one XCD when W % 8 == 0
+    const int rl = (int)(blockIdx.x / W) * (64 / K) + g;
+    const int64_t r = col * 64 + rl;
+    const bool live = r < R;
+    const u64 bit = 1ull << (rl & 63);
+    const int64_t NS = L.ns, colo = col * L.cs;
+    const u64* cone = L.s[0];
+    uint32_t* lists = lc_lists + lane;
+    uint32_t* htab = lc_lists + hoff + g * SPEC_HS;
+    // replica state, identical in the group's 8 lanes
+    double a = live ? st.a[r] : 0.0, b = live ? st.b[r] : 0.0;
+    int64_t t = live ? st.t[r] : 0, sum_end = live ? st.sum_end[r] : 0;
+    int done = live ? st.done[r] : 1;
+    int64_t pos = 0;                                          // proposals of this launch consumed
+    int ties = 0;
+    auto row = [&](int32_t v, int32_t (&o)[D]) {
+        const int4 q = adj_pad[(uint32_t)v < (uint32_t)n ? v : 0];             // never out of bounds
+        o[0] = q.x; o[1] = q.y; o[2] = q.z;
+    };
+    // plain loads: see k_sa_cone2
+    auto w = [&](int32_t v, int lv) { return cone[(int64_t)v * NS + colo + lv]; };
+    auto sector = [&](int32_t v, u64 (&o)[3]) {
+        const u64* p = cone + (int64_t)v * NS + colo;
+        const ulonglong2 q = *reinterpret_cast<const ulonglong2*>(p);
+        o[0] = q.x; o[1] = q.y; o[2] = p[2];
+    };
+    auto bv = [&](u64 x) -> uint32_t { return (x & bit) ? 1u : 0u; };
+    auto maj = [&](int ones, uint32_t own) -> uint32_t { return (2 * ones > D) ? 1u : ((2 * ones < D) ? 0u : own); };
+    auto hslot = [](int32_t v) { return ((uint32_t)v * 0x9E3779B1u) >> 23; };   // 9 bits = SPEC_HS
+    auto hins = [&](int32_t v) {                             // tag v with min(k) over the group's inserts
+        const uint32_t key = ((uint32_t)v << 3) | (uint32_t)k;
+        uint32_t h = hslot(v);
+        for (;;) {
+            const uint32_t old = atomicCAS(&htab[h], 0xffffffffu, key);
+            if (old == 0xffffffffu) break;
+            if ((old >> 3) == (uint32_t)v) { atomicMin(&htab[h], key); break; }
+            h = (h + 1) & (SPEC_HS - 1);
+        }
+    };
+    auto hearlier = [&](int32_t v) -> bool {                 // an earlier proposal may write v
+        uint32_t h = hslot(v);
+        for (;;) {
+            const uint32_t e = htab[h];
+            if (e == 0xffffffffu) return false;
+            if ((e >> 3) == (uint32_t)v) return (e & 7u) < (uint32_t)k;
+            h = (h + 1) & (SPEC_HS - 1);
+        }
+    };
+    for (;;) {
+        const bool going = live && done == 0 && pos < nsteps;
+        if (!__any(going)) break;
+        // empty hash sets (16 KB per wave, 16-B stores)
+        for (int q = lane; q < (64 / K) * SPEC_HS / 4; q += 64)
+            reinterpret_cast<uint4*>(lc_lists + hoff)[q] = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
+        const int64_t kk = pos + k;
+        const bool mine = going && kk < nsteps;
+        int32_t i = 0;
+        double u = 0.0;
+        if (mine) { i = tape_i[kk * R + r]; u = tape_u[kk * R + r]; }
+        // rows of i, of its neighbours, of their children (three round trips per batch)
+        int32_t A0[D], A1[D][D], C[D][D][D];
+        row(i, A0);
+#pragma unroll
+        for (int m = 0; m < D; ++m) row(A0[m], A1[m]);
+#pragma unroll
+        for (int m = 0; m < D; ++m)
+#pragma unroll
+            for (int x = 0; x < D; ++x) row(A1[m][x], C[m][x]);
+        // tree shape (lc_tree2)
+        bool ok = true, simple = true;
+#pragma unroll
+        for (int m = 0; m < D; ++m) {
+            int ci = 0;
+#pragma unroll
+            for (int x = 0; x < D; ++x) ci += (A1[m][x] == i);
+            ok &= (ci == 1) && (A0[m] != i);
+            simple &= A0[m] != i;
+#pragma unroll
+            for (int m2 = m + 1; m2 < D; ++m2) { ok &= A0[m] != A0[m2]; simple &= A0[m] != A0[m2]; }
+        }
+#pragma unroll
+        for (int m = 0; m < D; ++m)
+#pragma unroll
+            for (int x = 0; x < D; ++x) {
+                const int32_t cc = A1[m][x];
+                if (cc == i) continue;
+#pragma unroll
+                for (int m2 = 0; m2 < D; ++m2) ok &= (cc != A0[m2]);
+#pragma unroll
+                for (int m2 = m; m2 < D; ++m2)
+#pragma unroll
+                    for (int x2 = 0; x2 < D; ++x2)
+                        if (m2 > m || x2 > x) ok &= (A1[m2][x2] == i) || (A1[m2][x2] != cc);
+            }
+        int old_i = 0;
+        int64_t ds = 0;
+        uint32_t ch1 = 0, nv1 = 0, ch2 = 0;      // positions: 0 = i, 1+m = a_m, 1+D+m*D+x = child
+        bool listpath = false;
+        int cnt[LC_MAXT + 1] = {0, 0, 0, 0, 0, 0, 0};
+        if (mine && ok) {
+            u64 wi[3], wa[D][3], wc[D][D][3], wg[D][D][D];
+            sector(i, wi);
+#pragma unroll
+            for (int m = 0; m < D; ++m) {
+                sector(A0[m], wa[m]);
+#pragma unroll
+                for (int x = 0; x < D; ++x) {
+                    const bool child = A1[m][x] != i;
+                    wc[m][x][0] = wc[m][x][1] = wc[m][x][2] = 0ull;
+                    if (child) sector(A1[m][x], wc[m][x]);
+#pragma unroll
+                    for (int y = 0; y < D; ++y)
+                        wg[m][x][y] = (child && C[m][x][y] != A0[m]) ? w(C[m][x][y], 1) : 0ull;
+                }
+            }
+            const uint32_t f = bv(wi[0]) ^ 1u;
+            old_i = (int)bv(wi[0]);
+            {
+                int ones = 0;
+#pragma unroll
+                for (int m = 0; m < D; ++m) ones += (int)bv(wa[m][0]);
+                const uint32_t nb = maj(ones, f);
+                if (nb != bv(wi[1])) { ch1 |= 1u; nv1 |= nb; }
+            }
+#pragma unroll
+            for (int m = 0; m < D; ++m) {
+                int ones = 0;
+#pragma unroll
+                for (int x = 0; x < D; ++x) ones += (int)((A1[m][x] == i) ? f : bv(wc[m][x][0]));
+                const uint32_t nb = maj(ones, bv(wa[m][0]));
+                if (nb != bv(wa[m][1])) { ch1 |= 2u << m; nv1 |= nb << (1 + m); }
+            }
+            const bool c0 = ch1 & 1u;
+            const uint32_t vi1 = c0 ? (nv1 & 1u) : bv(wi[1]);
+            int64_t acc = 0;
+            if (ch1 != 0) {
+                int ones = 0;
+#pragma unroll
+                for (int m = 0; m < D; ++m) ones += (int)(((ch1 >> (1 + m)) & 1u) ? ((nv1 >> (1 + m)) & 1u) : bv(wa[m][1]));
+                const uint32_t nb = maj(ones, vi1);
+                if (nb != bv(wi[2])) { ch2 |= 1u; acc += nb ? 2 : -2; }
+            }
+#pragma unroll
+            for (int m = 0; m < D; ++m) {
+                const bool cm = (ch1 >> (1 + m)) & 1u;
+                const uint32_t va1 = cm ? ((nv1 >> (1 + m)) & 1u) : bv(wa[m][1]);
+                if (c0 || cm) {
+                    int ones = 0;
+#pragma unroll
+                    for (int x = 0; x < D; ++x) ones += (int)((A1[m][x] == i) ? vi1 : bv(wc[m][x][1]));
+                    const uint32_t nb = maj(ones, va1);
+                    if (nb != bv(wa[m][2])) { ch2 |= 2u << m; acc += nb ? 2 : -2; }
+                }
+                if (cm) {
+#pragma unroll
+                    for (int x = 0; x < D; ++x) {
+                        if (A1[m][x] == i) continue;
+                        int ones = 0;
+#pragma unroll
+                        for (int y = 0; y < D; ++y) ones += (int)((C[m][x][y] == A0[m]) ? va1 : bv(wg[m][x][y]));
+                        const uint32_t nb = maj(ones, bv(wc[m][x][1]));
+                        if (nb != bv(wc[m][x][2])) { ch2 |= 1u << (1 + D + m * D + x); acc += nb ? 2 : -2; }
+                    }
+                }
+            }
+            ds = acc;
+        } else if (mine && k == 0) {
+            // not a tree: the batched table path, and only as the batch's first proposal
+            listpath = true;
+            if (simple) ds = lc_delta_mlp<D, true>(adj, NS, colo, bit, T, L, lists, i, cnt, &old_i, A0, A1);
+            else ds = lc_delta_mlp<D, false>(adj, NS, colo, bit, T, L, lists, i, cnt, &old_i, A0, A1);
+        }
+        // potential writes of every proposal into the replica's hash set
+        if (mine && (ok || listpath)) {
+            hins(i);
+            if (listpath) {
+                for (int q = 0; q < cnt[1]; ++q) hins((int32_t)(lists[(L.off[1] + q) * 64] & 0x7fffffffu));
+                for (int q = 0; q < cnt[2]; ++q) hins((int32_t)(lists[(L.off[2] + q) * 64] & 0x7fffffffu));
+            } else {
+                const uint32_t chg = ch1 | ch2;
+#pragma unroll
+                for (int m = 0; m < D; ++m) {
+                    if ((chg >> (1 + m)) & 1u) hins(A0[m]);
+#pragma unroll
+                    for (int x = 0; x < D; ++x)
+                        if ((ch2 >> (1 + D + m * D + x)) & 1u) hins(A1[m][x]);
+                }
+            }
+        }
+        // does an earlier proposal of the batch write a node this one read?
+        bool stands = mine && (ok || listpath);
+        if (stands && k > 0) {
+            bool hit = hearlier(i);
+#pragma unroll
+            for (int m = 0; m < D; ++m) {
+                hit |= hearlier(A0[m]);
+#pragma unroll
+                for (int x = 0; x < D; ++x) {
+                    if (A1[m][x] == i) continue;
+                    hit |= hearlier(A1[m][x]);
+#pragma unroll
+                    for (int y = 0; y < D; ++y)
+                        if (C[m][x][y] != A0[m]) hit |= hearlier(C[m][x][y]);
+                }
+            }
+            stands = !hit;
+        }
+        // resolution: J0 = first proposal that does not stand
+        const int gs = g * K;
+        const uint32_t nst = (uint32_t)((__ballot(!stands) >> gs) & 0xffull);
+        const int J0 = nst ? __ffs(nst) - 1 : K;
+        // schedule and acceptance of proposal k (code/SA_RRG.py:37,74-81)
+        double ak = a, bk = b;
+        for (int q = 0; q < k; ++q) {
+            if (ak < a_cap) ak = par_a * ak;
+            if (bk < b_cap) bk = par_b * bk;
+        }
+        const bool inb = k < J0;
+        const double si = old_i ? 1.0 : -1.0;
+        const double t1 = (-2.0 * ak) * si;
+        const double t2 = bk * (double)(-ds);
+        const double dE = (t1 + t2) / (double)n;
+        const double e = exp(-dE);
+        const double prob = (e < 1.0) ? e : 1.0;
+        const bool acc = inb && u < prob;
+        // the stop: sum_end and t after proposal k
+        int64_t pre = acc ? ds : 0;
+#pragma unroll
+        for (int o = 1; o < K; o <<= 1) {
+            const int64_t v = __shfl_up(pre, o, K);
+            if (k >= o) pre += v;
+        }
+        const int64_t sum_after = sum_end + pre;
+        const int dn = (t + k + 1 > t_cap) ? 2 : ((sum_after == n) ? 1 : 0);
+        const uint32_t dm = (uint32_t)((__ballot(inb && dn != 0) >> gs) & 0xffull);
+        const int J = dm ? min(J0, __ffs(dm)) : J0;
+        if (k < J) {
+            if (e < 1.0 && fabs(u - e) <= 4.0 * (nextafter(e, 2.0) - e)) ++ties;
+            if (acc) {
+                auto flip = [&](int32_t v, int lv) {
+                    atomicXor((unsigned long long*)(cone + (int64_t)v * NS + colo + lv), (unsigned long long)bit);
+                };
+                flip(i, 0);
+                atomicXor((unsigned long long*)(L.s0c + (int64_t)i * W + col), (unsigned long long)bit);
+                if (listpath) {
+                    for (int q = 0; q < cnt[1]; ++q) flip((int32_t)(lists[(L.off[1] + q) * 64] & 0x7fffffffu), 1);
+                    for (int q = 0; q < cnt[2]; ++q) flip((int32_t)(lists[(L.off[2] + q) * 64] & 0x7fffffffu), 2);
+                } else {
+                    if (ch1 & 1u) flip(i, 1);
+                    if (ch2 & 1u) flip(i, 2);
+#pragma unroll
+                    for (int m = 0; m < D; ++m) {
+                        if ((ch1 >> (1 + m)) & 1u) flip(A0[m], 1);
+                        if ((ch2 >> (1 + m)) & 1u) flip(A0[m], 2);
+#pragma unroll
+                        for (int x = 0; x < D; ++x)
+                            if ((ch2 >> (1 + D + m * D + x)) & 1u) flip(A1[m][x], 2);
+                    }
+                }
+            }
+            if (st.tr_i) st.tr_i[kk * R + r] = i;
+            if (st.tr_acc) st.tr_acc[kk * R + r] = acc ? 1 : 0;
+            if (st.tr_sum) st.tr_sum[kk * R + r] = sum_after;
+            if (st.tr_dE) st.tr_dE[kk * R + r] = dE;
+        }
+        // the replica's state after the J consumed proposals (lane J-1's)
+        if (going) {
+            const int src = gs + J - 1;
+            sum_end = __shfl(sum_after, src, 64);
+            done = __shfl(dn, src, 64);
+            for (int q = 0; q < J; ++q) {
+                if (a < a_cap) a = par_a * a;
+                if (b < b_cap) b = par_b * b;
+            }
+            t += J;
+            pos += J;
+        } else {
+            (void)__shfl(sum_after, lane, 64);                // keep the shuffles wave-uniform
+            (void)__shfl(dn, lane, 64);
+        }
+        // flips land before the next batch reads
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    // steps of this launch after the replica finished
+    if (live && (st.tr_i || st.tr_acc || st.tr_sum || st.tr_dE)) {
+        for (int64_t q = pos + k; q < nsteps; q += K) {
+            if (st.tr_i) st.tr_i[q * R + r] = -1;
+            if (st.tr_acc) st.tr_acc[q * R + r] = -1;
+            if (st.tr_sum) st.tr_sum[q * R + r] = sum_end;
+            if (st.tr_dE) st.tr_dE[q * R + r] = 0.0;
+        }
+    }
+#pragma unroll
+    for (int o = K / 2; o >= 1; o >>= 1) ties += __shfl_xor(ties, o, K);
+    if (live && k == 0) {
+        st.a[r] = a;
+        st.b[r] = b;
+        st.t[r] = t;
+        st.sum_end[r] = sum_end;
+        st.done[r] = done;
+        if (st.tr_tie) st.tr_tie[r] += ties;
+    }
+}
+
 static int lc_slots(int d, int T, int* off, bool table = false, int* tab = nullptr, int* ballT = nullptr) {
     int64_t total = 0, ball = 1, shell = 1;
     for (int t = 0; t <= T; ++t) {
@@ -1542,6 +1879,20 @@ static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d
         MJX_LAUNCH_CHECK("k_sa_cone2");
         return MJX_OK;
     };
+    // ... and its speculative form: the 8 lanes of a group take 8 proposals of one replica
+    const bool spec = one_trip && n < (int64_t(1) << 28) && !getenv("MJX_NO_SPEC");
+    const int hoff = slots * 64;
+    const size_t lds_spec = lds + (size_t)64 / SPEC_K * SPEC_HS * 4;
+    auto launch_spec = [&](mjx_sa_state s2, int64_t k) -> int {
+        auto kern = k_sa_spec<3>;
+        MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_spec),
+                "spec lds");
+        kern<<<(unsigned)(W * (64 / SPEC_K)), 64, lds_spec, hs>>>(adj, (const int4*)adj_pad, n, R, W, L, s2, k,
+                                                                  par_a, par_b, a_cap, b_cap, t_cap, st.tape_i,
+                                                                  st.tape_u, hoff);
+        MJX_LAUNCH_CHECK("k_sa_spec");
+        return MJX_OK;
+    };
     auto run = [&](auto kern_plain, auto kern_tape) -> int {
         if (!tape) return launch(kern_plain, st, nsteps);
         for (int64_t k0 = 0; k0 < nsteps; k0 += st.tape_cap) {
@@ -1553,7 +1904,7 @@ static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d
             if (s2.tr_acc) s2.tr_acc += k0 * R;
             if (s2.tr_sum) s2.tr_sum += k0 * R;
             if (s2.tr_dE) s2.tr_dE += k0 * R;
-            const int rc = one_trip ? launch_one_trip(s2, k) : launch(kern_tape, s2, k);
+            const int rc = spec ? launch_spec(s2, k) : one_trip ? launch_one_trip(s2, k) : launch(kern_tape, s2, k);
             if (rc) return rc;
         }
         return MJX_OK;
