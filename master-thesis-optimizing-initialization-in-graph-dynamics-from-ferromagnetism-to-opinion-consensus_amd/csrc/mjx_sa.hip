@@ -1428,15 +1428,12 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
         int32_t i = 0;
         double u = 0.0;
         if (mine) { i = tape_i[kk * R + r]; u = tape_u[kk * R + r]; }
-        // rows of i, of its neighbours, of their children (three round trips per batch)
+        // rows of i and of its neighbours (two round trips per batch); the rows
+        // of the children only where level 2 needs them (below)
         int32_t A0[D], A1[D][D], C[D][D][D];
         row(i, A0);
 #pragma unroll
         for (int m = 0; m < D; ++m) row(A0[m], A1[m]);
-#pragma unroll
-        for (int m = 0; m < D; ++m)
-#pragma unroll
-            for (int x = 0; x < D; ++x) row(A1[m][x], C[m][x]);
         // tree shape (lc_tree2)
         bool ok = true, simple = true;
 #pragma unroll
@@ -1469,6 +1466,13 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
         bool listpath = false;
         int cnt[LC_MAXT + 1] = {0, 0, 0, 0, 0, 0, 0};
         if (mine && ok) {
+            // rows of the children and the level sectors of i, the a_m and the
+            // children in one batch
+#pragma unroll
+            for (int m = 0; m < D; ++m)
+#pragma unroll
+                for (int x = 0; x < D; ++x)
+                    if (A1[m][x] != i) row(A1[m][x], C[m][x]);
             u64 wi[3], wa[D][3], wc[D][D][3], wg[D][D][D];
             sector(i, wi);
 #pragma unroll
@@ -1476,12 +1480,8 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
                 sector(A0[m], wa[m]);
 #pragma unroll
                 for (int x = 0; x < D; ++x) {
-                    const bool child = A1[m][x] != i;
                     wc[m][x][0] = wc[m][x][1] = wc[m][x][2] = 0ull;
-                    if (child) sector(A1[m][x], wc[m][x]);
-#pragma unroll
-                    for (int y = 0; y < D; ++y)
-                        wg[m][x][y] = (child && C[m][x][y] != A0[m]) ? w(C[m][x][y], 1) : 0ull;
+                    if (A1[m][x] != i) sector(A1[m][x], wc[m][x]);
                 }
             }
             const uint32_t f = bv(wi[0]) ^ 1u;
@@ -1501,6 +1501,16 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
                 const uint32_t nb = maj(ones, bv(wa[m][0]));
                 if (nb != bv(wa[m][1])) { ch1 |= 2u << m; nv1 |= nb << (1 + m); }
             }
+            // the level-1 words of the children's other neighbours, only for the
+            // branches level 2 re-evaluates (one more round trip)
+#pragma unroll
+            for (int m = 0; m < D; ++m)
+#pragma unroll
+                for (int x = 0; x < D; ++x)
+#pragma unroll
+                    for (int y = 0; y < D; ++y)
+                        wg[m][x][y] = (((ch1 >> (1 + m)) & 1u) && A1[m][x] != i && C[m][x][y] != A0[m])
+                                          ? w(C[m][x][y], 1) : 0ull;
             const bool c0 = ch1 & 1u;
             const uint32_t vi1 = c0 ? (nv1 & 1u) : bv(wi[1]);
             int64_t acc = 0;
@@ -1569,6 +1579,7 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
                 for (int x = 0; x < D; ++x) {
                     if (A1[m][x] == i) continue;
                     hit |= hearlier(A1[m][x]);
+                    if (listpath || !((ch1 >> (1 + m)) & 1u)) continue;      // grandchildren read only here
 #pragma unroll
                     for (int y = 0; y < D; ++y)
                         if (C[m][x][y] != A0[m]) hit |= hearlier(C[m][x][y]);
