@@ -86,7 +86,8 @@ def main():
             "k_sweep_cls_rp": lambda b: b.startswith("k_sweep_cls"),
             "k_hpr_node_marg": lambda b: b == "k_hpr_node_marg",
             "k_bin_msg": lambda b: b == "k_bin_msg",
-            "k_bin_apply": lambda b: b.startswith("k_bin_apply")}
+            "k_bin_apply": lambda b: b.startswith("k_bin_apply"),
+            "k_sa_spec": lambda b: b == "k_sa_spec"}
     entries = {k: v for k, v in res.items() if isinstance(v, dict) and "fetch_kib" in v}
     for fam, match in fams.items():
         ks = [v for k, v in entries.items() if match(base(k))]

@@ -5,7 +5,8 @@ Runs, on cuda:0, exactly the bench.py sweep (d=4 RRG, N=1e6, R=4096
 replica-packed, 2 sweeps per rollout, fused count on the last one) a few
 times, then (unless --no-hpr) the C3 HPR iteration (d=4 RRG, N=1e5,
 p=c=2, fp32: HPr_dp + marginals_comp, in the reference layout and in the
-loop state's decay-split layout) and (unless --no-giant) a few sweeps
+loop state's decay-split layout), (unless --no-sa) 1000 light-cone SA steps
+at configs[1] (the speculative batches), and (unless --no-giant) a few sweeps
 of the C5 partitioned N=1e9 d=6 graph on one rank, preceded by a calibration copy of a known byte count (torch's
 vectorised copy, 16 B per lane) that tools/pmc_parse.py uses to check the
 gfx950 FETCH_SIZE correction (MI355X_MICROARCH.md, HBM section).
@@ -29,6 +30,8 @@ def main():
     ap.add_argument("--no-hpr", action="store_true")
     ap.add_argument("--no-giant", action="store_true")
     ap.add_argument("--giant-n", type=int, default=1_000_000_000)
+    ap.add_argument("--no-sa", action="store_true")
+    ap.add_argument("--sa-steps", type=int, default=1000)
     args = ap.parse_args()
     import torch
     import mjx
@@ -76,6 +79,15 @@ def main():
         torch.cuda.synchronize()
         del chi, hout, plan, st
         print("pmc_run hpr done", flush=True)
+    if not args.no_sa:
+        # configs[1] light-cone SA (d=3, N=1e6, p=2, c=1, 4096 replicas): the
+        # speculative batches on the cone layout; one launch per 1024-step tape chunk
+        import numpy as np
+        sa = mjx.SAReplicas(mjx.random_regular_graph(3, 1_000_000, seed=7), 2, 1, np.arange(4096), mode="lightcone")
+        sa.steps(args.sa_steps)
+        torch.cuda.synchronize()
+        del sa
+        print("pmc_run sa done", flush=True)
     if not args.no_giant:
         sh = mjx.ShardedRRG(6, args.giant_n, seed=12345, mode="binned")
         sh.drop_adjacency()
