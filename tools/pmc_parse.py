@@ -68,8 +68,9 @@ def main():
             "read_factor": calib_bytes / max(1.0, fk * 1024),
             "write_factor": calib_bytes / max(1.0, wk * 1024),
         }
-    # bench.py key: the fused-count sweep and the plain sweep of the rollout
-    sweeps = [v for k, v in res.items() if k.startswith("mjx::k_sweep_ell_rp") or "k_sweep_ell_rp" in k]
+    # bench.py key: the fused-count sweep and the plain sweep of the d=4 rollout
+    # (the SA section's d=3 level sweeps are other launches)
+    sweeps = [v for k, v in res.items() if "k_sweep_ell_rp<4," in k]
     if sweeps:
         tot = sum(v["bytes_per_launch"] * v["dispatches"] for v in sweeps)
         cnt = sum(v["dispatches"] for v in sweeps)
