@@ -1358,15 +1358,16 @@ __global__ void __launch_bounds__(64) k_sa_cone2(const int32_t* __restrict__ adj
 constexpr int SPEC_K = 8;        // proposals per batch = lanes per replica
 constexpr int SPEC_HS = 512;     // hash slots per replica (<= 8 * 18 keys)
 
-template <int D>
+template <int D, int TT>
 __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj, const int4* __restrict__ adj_pad,
                                                 int64_t n, int64_t R, int64_t W, LcLevels L, mjx_sa_state st,
                                                 int64_t nsteps, double par_a, double par_b, double a_cap,
                                                 double b_cap, int64_t t_cap, const int32_t* __restrict__ tape_i,
                                                 const double* __restrict__ tape_u, int hoff) {
-    static_assert(D == 3, "rows are read as one 16-B load from the padded adjacency");
+    // rows as one 16-B load: the padded adjacency (d = 3) or the adjacency itself (d = 4)
+    static_assert((D == 3 && (TT == 1 || TT == 2)) || (D == 4 && TT == 1), "speculative batches: d=3 T<=2, d=4 T=1");
     extern __shared__ uint32_t lc_lists[];
-    constexpr int T = 2, K = SPEC_K;
+    constexpr int T = TT, K = SPEC_K;
     const int lane = threadIdx.x;
     const int g = lane / K, k = lane % K;
     const int64_t col = blockIdx.x % W;                       // a column's waves on one XCD when W % 8 == 0
@@ -1387,13 +1388,14 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
     auto row = [&](int32_t v, int32_t (&o)[D]) {
         const int4 q = adj_pad[(uint32_t)v < (uint32_t)n ? v : 0];             // never out of bounds
         o[0] = q.x; o[1] = q.y; o[2] = q.z;
+        if constexpr (D == 4) o[3] = q.w;
     };
     // plain loads: see k_sa_cone2
     auto w = [&](int32_t v, int lv) { return cone[(int64_t)v * NS + colo + lv]; };
-    auto sector = [&](int32_t v, u64 (&o)[3]) {
+    auto sector = [&](int32_t v, u64 (&o)[3]) {      // levels 0..T of v
         const u64* p = cone + (int64_t)v * NS + colo;
         const ulonglong2 q = *reinterpret_cast<const ulonglong2*>(p);
-        o[0] = q.x; o[1] = q.y; o[2] = p[2];
+        o[0] = q.x; o[1] = q.y; o[2] = (TT == 2) ? p[2] : 0ull;
     };
     auto bv = [&](u64 x) -> uint32_t { return (x & bit) ? 1u : 0u; };
     auto maj = [&](int ones, uint32_t own) -> uint32_t { return (2 * ones > D) ? 1u : ((2 * ones < D) ? 0u : own); };
@@ -1466,13 +1468,15 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
         bool listpath = false;
         int cnt[LC_MAXT + 1] = {0, 0, 0, 0, 0, 0, 0};
         if (mine && ok) {
-            // rows of the children and the level sectors of i, the a_m and the
-            // children in one batch
+            // rows of the children (T = 2) and the level sectors of i, the a_m and
+            // the children in one batch
+            if constexpr (TT == 2) {
 #pragma unroll
-            for (int m = 0; m < D; ++m)
+                for (int m = 0; m < D; ++m)
 #pragma unroll
-                for (int x = 0; x < D; ++x)
-                    if (A1[m][x] != i) row(A1[m][x], C[m][x]);
+                    for (int x = 0; x < D; ++x)
+                        if (A1[m][x] != i) row(A1[m][x], C[m][x]);
+            }
             u64 wi[3], wa[D][3], wc[D][D][3], wg[D][D][D];
             sector(i, wi);
 #pragma unroll
@@ -1501,6 +1505,14 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
                 const uint32_t nb = maj(ones, bv(wa[m][0]));
                 if (nb != bv(wa[m][1])) { ch1 |= 2u << m; nv1 |= nb << (1 + m); }
             }
+            if constexpr (TT == 1) {
+                // T = 1: the sum over the level-1 changes (lc_tree2)
+                int64_t acc = 0;
+#pragma unroll
+                for (int e = 0; e <= D; ++e)
+                    if ((ch1 >> e) & 1u) acc += ((nv1 >> e) & 1u) ? 2 : -2;
+                ds = acc;
+            } else {
             // the level-1 words of the children's other neighbours, only for the
             // branches level 2 re-evaluates (one more round trip)
 #pragma unroll
@@ -1545,6 +1557,7 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
                 }
             }
             ds = acc;
+            }
         } else if (mine && k == 0) {
             // not a tree: the batched table path, and only as the batch's first proposal
             listpath = true;
@@ -1555,8 +1568,9 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
         if (mine && (ok || listpath)) {
             hins(i);
             if (listpath) {
-                for (int q = 0; q < cnt[1]; ++q) hins((int32_t)(lists[(L.off[1] + q) * 64] & 0x7fffffffu));
-                for (int q = 0; q < cnt[2]; ++q) hins((int32_t)(lists[(L.off[2] + q) * 64] & 0x7fffffffu));
+#pragma unroll
+                for (int lv = 1; lv <= T; ++lv)
+                    for (int q = 0; q < cnt[lv]; ++q) hins((int32_t)(lists[(L.off[lv] + q) * 64] & 0x7fffffffu));
             } else {
                 const uint32_t chg = ch1 | ch2;
 #pragma unroll
@@ -1579,7 +1593,7 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
                 for (int x = 0; x < D; ++x) {
                     if (A1[m][x] == i) continue;
                     hit |= hearlier(A1[m][x]);
-                    if (listpath || !((ch1 >> (1 + m)) & 1u)) continue;      // grandchildren read only here
+                    if (TT == 1 || listpath || !((ch1 >> (1 + m)) & 1u)) continue;   // grandchildren read only here
 #pragma unroll
                     for (int y = 0; y < D; ++y)
                         if (C[m][x][y] != A0[m]) hit |= hearlier(C[m][x][y]);
@@ -1625,8 +1639,9 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
                 flip(i, 0);
                 atomicXor((unsigned long long*)(L.s0c + (int64_t)i * W + col), (unsigned long long)bit);
                 if (listpath) {
-                    for (int q = 0; q < cnt[1]; ++q) flip((int32_t)(lists[(L.off[1] + q) * 64] & 0x7fffffffu), 1);
-                    for (int q = 0; q < cnt[2]; ++q) flip((int32_t)(lists[(L.off[2] + q) * 64] & 0x7fffffffu), 2);
+#pragma unroll
+                    for (int lv = 1; lv <= T; ++lv)
+                        for (int q = 0; q < cnt[lv]; ++q) flip((int32_t)(lists[(L.off[lv] + q) * 64] & 0x7fffffffu), lv);
                 } else {
                     if (ch1 & 1u) flip(i, 1);
                     if (ch2 & 1u) flip(i, 2);
@@ -1891,18 +1906,23 @@ static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d
         return MJX_OK;
     };
     // ... and its speculative form: the 8 lanes of a group take 8 proposals of one replica
-    const bool spec = one_trip && n < (int64_t(1) << 28) && !getenv("MJX_NO_SPEC");
+    const int4* rows4 = (d == 4) ? (const int4*)adj : (const int4*)adj_pad;   // 16-B rows
+    const bool spec = tape && L.s0c && rows4 && L.tab >= 0 && n < (int64_t(1) << 28) && !getenv("MJX_NO_SPEC") &&
+                      ((d == 3 && (T == 1 || T == 2)) || (d == 4 && T == 1));
     const int hoff = slots * 64;
     const size_t lds_spec = lds + (size_t)64 / SPEC_K * SPEC_HS * 4;
     auto launch_spec = [&](mjx_sa_state s2, int64_t k) -> int {
-        auto kern = k_sa_spec<3>;
-        MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_spec),
-                "spec lds");
-        kern<<<(unsigned)(W * (64 / SPEC_K)), 64, lds_spec, hs>>>(adj, (const int4*)adj_pad, n, R, W, L, s2, k,
-                                                                  par_a, par_b, a_cap, b_cap, t_cap, st.tape_i,
-                                                                  st.tape_u, hoff);
-        MJX_LAUNCH_CHECK("k_sa_spec");
-        return MJX_OK;
+        auto go = [&](auto kern) {
+            MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)lds_spec), "spec lds");
+            kern<<<(unsigned)(W * (64 / SPEC_K)), 64, lds_spec, hs>>>(adj, rows4, n, R, W, L, s2, k, par_a, par_b,
+                                                                      a_cap, b_cap, t_cap, st.tape_i, st.tape_u,
+                                                                      hoff);
+            MJX_LAUNCH_CHECK("k_sa_spec");
+            return MJX_OK;
+        };
+        if (d == 4) return go(k_sa_spec<4, 1>);
+        return (T == 2) ? go(k_sa_spec<3, 2>) : go(k_sa_spec<3, 1>);
     };
     auto run = [&](auto kern_plain, auto kern_tape) -> int {
         if (!tape) return launch(kern_plain, st, nsteps);
