@@ -1355,10 +1355,9 @@ __global__ void __launch_bounds__(64) k_sa_cone2(const int32_t* __restrict__ adj
 // almost always consume all 8: the replica's serial chain moves 8 proposals per
 // memory round trip instead of one.  Same accept sequence as the serial step.
 // ---------------------------------------------------------------------------
-constexpr int SPEC_K = 8;        // proposals per batch = lanes per replica
-constexpr int SPEC_HS = 512;     // hash slots per replica (<= 8 * 18 keys)
+constexpr int SPEC_LDS = 16384;  // bytes of hash sets per wave: 64 * K slots per replica (<= K * 18 keys)
 
-template <int D, int TT>
+template <int D, int TT, int K>
 __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj, const int4* __restrict__ adj_pad,
                                                 int64_t n, int64_t R, int64_t W, LcLevels L, mjx_sa_state st,
                                                 int64_t nsteps, double par_a, double par_b, double a_cap,
@@ -1367,7 +1366,12 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
     // rows as one 16-B load: the padded adjacency (d = 3) or the adjacency itself (d = 4)
     static_assert((D == 3 && (TT == 1 || TT == 2)) || (D == 4 && TT == 1), "speculative batches: d=3 T<=2, d=4 T=1");
     extern __shared__ uint32_t lc_lists[];
-    constexpr int T = TT, K = SPEC_K;
+    static_assert(K == 8 || K == 16, "8 or 16 proposals per batch");
+    constexpr int T = TT;
+    constexpr int KB = (K == 8) ? 3 : 4;                     // tag bits
+    constexpr int SPEC_HS = 64 * K;                          // hash slots per replica
+    constexpr int HB = (K == 8) ? 9 : 10;                    // log2(SPEC_HS)
+    constexpr u64 GM = (1ull << K) - 1;
     const int lane = threadIdx.x;
     const int g = lane / K, k = lane % K;
     const int64_t col = blockIdx.x % W;                       // a column's waves on one XCD when W % 8 == 0
@@ -1399,14 +1403,14 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
     };
     auto bv = [&](u64 x) -> uint32_t { return (x & bit) ? 1u : 0u; };
     auto maj = [&](int ones, uint32_t own) -> uint32_t { return (2 * ones > D) ? 1u : ((2 * ones < D) ? 0u : own); };
-    auto hslot = [](int32_t v) { return ((uint32_t)v * 0x9E3779B1u) >> 23; };   // 9 bits = SPEC_HS
+    auto hslot = [](int32_t v) { return ((uint32_t)v * 0x9E3779B1u) >> (32 - HB); };
     auto hins = [&](int32_t v) {                             // tag v with min(k) over the group's inserts
-        const uint32_t key = ((uint32_t)v << 3) | (uint32_t)k;
+        const uint32_t key = ((uint32_t)v << KB) | (uint32_t)k;
         uint32_t h = hslot(v);
         for (;;) {
             const uint32_t old = atomicCAS(&htab[h], 0xffffffffu, key);
             if (old == 0xffffffffu) break;
-            if ((old >> 3) == (uint32_t)v) { atomicMin(&htab[h], key); break; }
+            if ((old >> KB) == (uint32_t)v) { atomicMin(&htab[h], key); break; }
             h = (h + 1) & (SPEC_HS - 1);
         }
     };
@@ -1415,7 +1419,7 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
         for (;;) {
             const uint32_t e = htab[h];
             if (e == 0xffffffffu) return false;
-            if ((e >> 3) == (uint32_t)v) return (e & 7u) < (uint32_t)k;
+            if ((e >> KB) == (uint32_t)v) return (e & (uint32_t)(K - 1)) < (uint32_t)k;
             h = (h + 1) & (SPEC_HS - 1);
         }
     };
@@ -1603,7 +1607,7 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
         }
         // resolution: J0 = first proposal that does not stand
         const int gs = g * K;
-        const uint32_t nst = (uint32_t)((__ballot(!stands) >> gs) & 0xffull);
+        const uint32_t nst = (uint32_t)((__ballot(!stands) >> gs) & GM);
         const int J0 = nst ? __ffs(nst) - 1 : K;
         // schedule and acceptance of proposal k (code/SA_RRG.py:37,74-81)
         double ak = a, bk = b;
@@ -1628,7 +1632,7 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
         }
         const int64_t sum_after = sum_end + pre;
         const int dn = (t + k + 1 > t_cap) ? 2 : ((sum_after == n) ? 1 : 0);
-        const uint32_t dm = (uint32_t)((__ballot(inb && dn != 0) >> gs) & 0xffull);
+        const uint32_t dm = (uint32_t)((__ballot(inb && dn != 0) >> gs) & GM);
         const int J = dm ? min(J0, __ffs(dm)) : J0;
         if (k < J) {
             if (e < 1.0 && fabs(u - e) <= 4.0 * (nextafter(e, 2.0) - e)) ++ties;
@@ -1907,22 +1911,30 @@ static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d
     };
     // ... and its speculative form: the 8 lanes of a group take 8 proposals of one replica
     const int4* rows4 = (d == 4) ? (const int4*)adj : (const int4*)adj_pad;   // 16-B rows
-    const bool spec = tape && L.s0c && rows4 && L.tab >= 0 && n < (int64_t(1) << 28) && !getenv("MJX_NO_SPEC") &&
-                      ((d == 3 && (T == 1 || T == 2)) || (d == 4 && T == 1));
+    // 8 proposals per batch; 16 when 8 would leave CUs without a wave (few word columns):
+    // configs[1] at R = 1024 3.05 -> 1.78 us per step, at R = 4096 16 is slower (3.76 vs 4.10)
+    int spec_k = (W * 8 < kCUs) ? 16 : 8;
+    if (const char* e = getenv("MJX_SPEC_K")) spec_k = (atoi(e) == 16) ? 16 : 8;   // tuning override
+    const bool spec = tape && L.s0c && rows4 && L.tab >= 0 && n < (int64_t(1) << (spec_k == 16 ? 27 : 28)) &&
+                      !getenv("MJX_NO_SPEC") && ((d == 3 && (T == 1 || T == 2)) || (d == 4 && T == 1));
     const int hoff = slots * 64;
-    const size_t lds_spec = lds + (size_t)64 / SPEC_K * SPEC_HS * 4;
+    const size_t lds_spec = lds + SPEC_LDS;
     auto launch_spec = [&](mjx_sa_state s2, int64_t k) -> int {
-        auto go = [&](auto kern) {
+        auto go = [&](auto kern, int K) {      // K waves per word column (64 / K replicas per wave)
             MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         (int)lds_spec), "spec lds");
-            kern<<<(unsigned)(W * (64 / SPEC_K)), 64, lds_spec, hs>>>(adj, rows4, n, R, W, L, s2, k, par_a, par_b,
+            kern<<<(unsigned)(W * K), 64, lds_spec, hs>>>(adj, rows4, n, R, W, L, s2, k, par_a, par_b,
                                                                       a_cap, b_cap, t_cap, st.tape_i, st.tape_u,
                                                                       hoff);
             MJX_LAUNCH_CHECK("k_sa_spec");
             return MJX_OK;
         };
-        if (d == 4) return go(k_sa_spec<4, 1>);
-        return (T == 2) ? go(k_sa_spec<3, 2>) : go(k_sa_spec<3, 1>);
+        if (spec_k == 16) {
+            if (d == 4) return go(k_sa_spec<4, 1, 16>, 16);
+            return (T == 2) ? go(k_sa_spec<3, 2, 16>, 16) : go(k_sa_spec<3, 1, 16>, 16);
+        }
+        if (d == 4) return go(k_sa_spec<4, 1, 8>, 8);
+        return (T == 2) ? go(k_sa_spec<3, 2, 8>, 8) : go(k_sa_spec<3, 1, 8>, 8);
     };
     auto run = [&](auto kern_plain, auto kern_tape) -> int {
         if (!tape) return launch(kern_plain, st, nsteps);

@@ -106,17 +106,22 @@ def test_sa_lightcone_levels_stay_consistent(mjx_mod, d, p, c):
     assert torch.equal(2 * cnt[:sa.R] - n, sa.sum_end)
 
 
-@pytest.mark.parametrize("d,p,c,kernel", [(3, 2, 1, "spec"), (3, 2, 1, "one_trip"), (3, 2, 1, "lightcone"),
-                                          (3, 1, 1, "spec"), (4, 1, 1, "spec"), (4, 1, 1, "lightcone"),
+@pytest.mark.parametrize("d,p,c,kernel", [(3, 2, 1, "spec8"), (3, 2, 1, "spec16"), (3, 2, 1, "one_trip"),
+                                          (3, 2, 1, "lightcone"), (3, 1, 1, "spec8"), (3, 1, 1, "spec16"),
+                                          (4, 1, 1, "spec8"), (4, 1, 1, "spec16"), (4, 1, 1, "lightcone"),
                                           (4, 2, 2, ""), (5, 1, 2, ""), (3, 3, 4, "")])
 def test_sa_cone_layout_equals_separate_levels(mjx_mod, d, p, c, kernel, monkeypatch):
     """The cone layout (levels of one (node, word) side by side) gives the
     same proposals, accepts, sums and delta_H as separate level arrays, and
     the same final configuration and levels (LV = 2, 4 and 8 words).  At
     d=3, p+c-1=2 three kernels run on the cone: the speculative 8-proposal
-    batches (default; also d=3 and d=4 at p+c-1=1), the one-round-trip step
+    batches of 8 or 16 proposals (default; also d=3 and d=4 at p+c-1=1), the one-round-trip step
     (MJX_NO_SPEC) and the general light-cone step (MJX_NO_CONE2)."""
-    if kernel == "one_trip":
+    if kernel == "spec16":
+        monkeypatch.setenv("MJX_SPEC_K", "16")
+    elif kernel == "spec8":
+        monkeypatch.setenv("MJX_SPEC_K", "8")
+    elif kernel == "one_trip":
         monkeypatch.setenv("MJX_NO_SPEC", "1")
     elif kernel == "lightcone":
         monkeypatch.setenv("MJX_NO_SPEC", "1")
