@@ -1337,8 +1337,9 @@ __global__ void __launch_bounds__(64) k_sa_cone2(const int32_t* __restrict__ adj
 }
 
 // ---------------------------------------------------------------------------
-// Speculative batches (d = 3, p+c-1 = 2, cone layout, proposal tape): the 8
-// lanes of a lane group evaluate the next 8 proposals of ONE replica at once,
+// Speculative batches (cone layout, proposal tape; d = 3 at p+c-1 <= 2, d = 4 at
+// p+c-1 = 1): the K = 8 or 16 lanes of a lane group evaluate the next K
+// proposals of ONE replica at once,
 // all against the current configuration, and the batch is then resolved in
 // proposal order.  Proposal j's evaluation reads the words of the nodes R_j of
 // its radius-3 tree; it is the one a sequential run computes unless an earlier
@@ -1352,8 +1353,10 @@ __global__ void __launch_bounds__(64) k_sa_cone2(const int32_t* __restrict__ adj
 // (the schedule a, b depends on the step count only; delta_H on the proposal's
 // own change), the stop needs a prefix sum of the accepted changes.  Two random
 // proposals on a 1e6-node graph collide with probability ~1e-4, so batches
-// almost always consume all 8: the replica's serial chain moves 8 proposals per
-// memory round trip instead of one.  Same accept sequence as the serial step.
+// almost always consume all K: the replica's serial chain moves K proposals per
+// batch of round trips instead of one.  Same accept sequence as the serial step.
+// (Two-hop adjacency records -- a node's row and its neighbours' rows in one
+// line -- measured no faster: the 16 MB adjacency is served on-die.)
 // ---------------------------------------------------------------------------
 constexpr int SPEC_LDS = 16384;  // bytes of hash sets per wave: 64 * K slots per replica (<= K * 18 keys)
 
