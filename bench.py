@@ -78,7 +78,84 @@ def parse():
     ap.add_argument("--no-hpr", action="store_true")
     ap.add_argument("--bdcm-iters", type=int, default=100)
     ap.add_argument("--no-bdcm", action="store_true")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check without a GPU: the ranks join a gloo group, time an empty step and "
+                         "rank 0 prints the merged JSON line (tests/test_bench_launch.py)")
     return ap.parse_args()
+
+
+# ---------------------------------------------------------------------------
+# Launcher: --gpus N > 1 without a torch.distributed.run environment
+# ---------------------------------------------------------------------------
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args, argv):
+    """Start one fresh rank process per GPU (RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_* set, rendezvous on 127.0.0.1) and wait for them.  This process
+    never touches the GPU (device_count() does not initialise it) and never
+    re-execs; it exits with the first failing rank's status, stopping the
+    others, and fails when fewer than N devices are visible."""
+    import subprocess
+    n = args.gpus
+    if not args.dry_run:
+        import torch
+        avail = torch.cuda.device_count()
+        if avail < n:
+            print(f"bench.py: --gpus {n} but only {avail} GPU(s) visible", file=sys.stderr, flush=True)
+            return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                print(f"bench.py: rank {procs.index(p)} exited with status {code}; stopping the others",
+                      file=sys.stderr, flush=True)
+                for q in live:
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
+
+
+def dry_run(args, rank, world):
+    """The launch path without a GPU: gloo group, an empty timed step between
+    barriers, max over ranks, one merged JSON line from rank 0."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+    t0 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    pids = [os.getpid()]
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+        pids = [None] * world
+        dist.all_gather_object(pids, os.getpid())
+    if rank == 0:
+        print(json.dumps({"metric": "dry-run", "value": 0.0, "unit": "none", "n_gpus": world, "ranks": world,
+                          "rank_pids": pids, "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * el,
+                          "dry_run": True}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 # ---------------------------------------------------------------------------
@@ -559,9 +636,20 @@ def rocprof_traffic(kernel_prefix="k_sweep_ell_rp"):
 
 def main():
     args = parse()
+    if args.gpus < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr)
+        sys.exit(2)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
+    if args.dry_run:
+        dry_run(args, rank, world)
+        return
     n, d, R = args.n, args.d, args.replicas
     T = args.p + args.c - 1
     W = (R + 63) // 64
@@ -658,6 +746,10 @@ def main():
     if not args.no_giant and args.giant_n > 0:
         giant = bench_giant(args, rank, world, dist, dev)
 
+    for leg in (sa_res, c1, er, hpr, bdcm, giant):
+        if leg is not None:
+            leg["n_gpus"] = world
+            leg["ranks"] = world
     if rank == 0:
         line = {
             "metric": "node-updates/s, d=4 RRG majority rollout (s_endstate + m of bit-packed replicas)",

@@ -1,0 +1,63 @@
+"""bench.py's launcher: `--gpus N` without a
+torch.distributed.run environment starts N rank processes; the dry-run mode
+drives the same path over gloo without a GPU.  `--gpus 1` stays one process."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _run(argv, env_extra=None, timeout=120):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, BENCH] + argv, capture_output=True, text=True, timeout=timeout,
+                          env=env, cwd=ROOT)
+
+
+def _json_lines(out):
+    return [json.loads(x) for x in out.splitlines() if x.strip().startswith("{")]
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_gpus_n_starts_n_ranks_and_prints_one_line(n):
+    p = _run(["--gpus", str(n), "--dry-run", "--steps", "3", "--warmup", "1"])
+    assert p.returncode == 0, p.stderr
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1, p.stdout
+    line = lines[0]
+    assert line["n_gpus"] == n and line["ranks"] == n
+    pids = line["rank_pids"]
+    assert len(pids) == n and len(set(pids)) == n           # n distinct processes
+    assert os.getpid() not in pids
+    assert line["steps"] == 3 and line["warmup"] == 1
+
+
+def test_gpus_1_is_one_process():
+    p = _run(["--gpus", "1", "--dry-run"])
+    assert p.returncode == 0, p.stderr
+    (line,) = _json_lines(p.stdout)
+    assert line["n_gpus"] == 1 and len(line["rank_pids"]) == 1
+
+
+def test_world_size_mismatch_fails():
+    p = _run(["--gpus", "4", "--dry-run"], env_extra={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert p.returncode != 0
+    assert "WORLD_SIZE" in p.stderr
+    assert not _json_lines(p.stdout)
+
+
+def test_too_few_gpus_fails_loudly():
+    """No GPU in this container: --gpus 2 must refuse instead of reporting n_gpus 1."""
+    import torch
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("two GPUs visible")
+    p = _run(["--gpus", "2", "--steps", "1", "--warmup", "0"])
+    assert p.returncode != 0
+    assert "visible" in p.stderr
+    assert not _json_lines(p.stdout)
