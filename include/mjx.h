@@ -56,6 +56,9 @@ extern "C" {
 #define MJX_F64  108
 
 int         mjx_abi_version(void);            /* bumps on any signature change */
+/* Content hash of the sources (csrc/, include/mjx.h) the library was built
+ * from; the Python loader refuses a library whose id differs from its tree. */
+const char* mjx_build_id(void);
 const char* mjx_strerror(int status);
 const char* mjx_last_hip_error(void);         /* text of the last failing HIP call */
 

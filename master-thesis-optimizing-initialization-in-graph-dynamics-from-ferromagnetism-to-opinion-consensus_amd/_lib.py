@@ -20,6 +20,7 @@ c_u64 = ctypes.c_uint64
 # name -> argtypes (restype is c_int unless listed in _RESTYPES)
 SIGNATURES = {
     "mjx_abi_version": [],
+    "mjx_build_id": [],
     "mjx_strerror": [c_int],
     "mjx_last_hip_error": [],
     "mjx_pack_np": [c_vp, c_int, c_i64, c_vp, c_vp],
@@ -89,7 +90,7 @@ SIGNATURES = {
     "mjx_bdcm_edge_obs": [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_dbl, c_vp, c_vp, c_vp],
     "mjx_sum_f64": [c_vp, c_i64, c_int, c_vp, c_vp, c_vp],
 }
-_RESTYPES = {"mjx_strerror": ctypes.c_char_p, "mjx_last_hip_error": ctypes.c_char_p,
+_RESTYPES = {"mjx_strerror": ctypes.c_char_p, "mjx_build_id": ctypes.c_char_p, "mjx_last_hip_error": ctypes.c_char_p,
              "mjx_sa_lightcone_lds": c_i64, "mjx_bdcm_lds_bytes": c_i64, "mjx_bdcm_scratch_bytes": c_i64,
              "mjx_rrg_partner_host": c_i64, "mjx_er_work_bytes": c_i64, "mjx_hpr_er_scratch_bytes": c_i64}
 
@@ -117,26 +118,44 @@ def lib_path():
     return _build.LIB
 
 
+def verify_build_id(lib, csrc=None, include=None):
+    """Raise MjxError unless the library's mjx_build_id() is the content hash
+    of the source tree (default: the csrc/ and include/ next to this file)."""
+    got = lib.mjx_build_id().decode()
+    want = _build.source_hash(csrc or _build.CSRC, include or _build.INCLUDE)
+    if got != want:
+        raise MjxError(f"libmjx.so was built from other sources (build id {got}, source tree {want}): "
+                       "rebuild it with __graft_entry__.build()")
+
+
+def open_library(path, verify=True):
+    """dlopen a build of libmjx.so and declare every entry point; with
+    ``verify`` the build id must match the source tree (verify_build_id)."""
+    lib = ctypes.CDLL(path)
+    for name, argtypes in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = _RESTYPES.get(name, c_int)
+    if verify:
+        verify_build_id(lib)
+    return lib
+
+
 def load(build_if_missing=False):
-    """Load libmjx.so and declare every entry point.  Raises if it is absent."""
+    """Load the in-tree libmjx.so (its build id checked against the sources)
+    and declare every entry point.  Raises if it is absent or stale."""
     global _LIB
     if _LIB is not None:
         return _LIB
-    # MJX_LIB: an alternative build of the same library (profiling variants)
-    path = os.environ.get("MJX_LIB") or _build.LIB
+    path = _build.LIB
     if not os.path.exists(path):
         if build_if_missing:
             _build.build()
         else:
             raise MjxError(f"libmjx.so not found at {path}: run __graft_entry__.build() "
                            "(there is no CPU fallback for the majority-dynamics kernels)")
-    lib = ctypes.CDLL(path)
-    for name, argtypes in SIGNATURES.items():
-        fn = getattr(lib, name)
-        fn.argtypes = argtypes
-        fn.restype = _RESTYPES.get(name, c_int)
-    _LIB = lib
-    return lib
+    _LIB = open_library(path)
+    return _LIB
 
 
 def check(rc, what):

@@ -88,3 +88,26 @@ def test_product_path_fails_loudly_without_gpu(mjx_mod):
         mjx_mod.onestep_majority(adj, np.ones(64, dtype=np.int64))
     with pytest.raises(mjx_mod.MjxError):
         mjx_mod.SAReplicas(adj, 1, 1, [0])
+
+
+def test_build_id_binds_library_to_its_sources(mjx_mod, tmp_path):
+    """libmjx.so embeds the content hash of csrc/ + include/mjx.h; the loader
+    refuses a library whose id differs from the tree."""
+    import shutil
+    lib = mjx_mod.load_library()            # the in-tree library matches its own tree
+    _lib, _build = mjx_mod._lib, mjx_mod._lib._build
+    assert lib.mjx_build_id().decode() == _build.source_hash()
+    csrc, inc = tmp_path / "csrc", tmp_path / "include"
+    shutil.copytree(_build.CSRC, csrc, ignore=shutil.ignore_patterns("*.o"))
+    shutil.copytree(os.path.dirname(HEADER), inc)
+    _lib.verify_build_id(lib, str(csrc), str(inc))          # an identical copy passes
+    victim = csrc / "mjx_sa.hip"
+    victim.write_text(victim.read_text() + "\n// changed\n")
+    with pytest.raises(mjx_mod.MjxError, match="other sources"):
+        _lib.verify_build_id(lib, str(csrc), str(inc))
+    hdr = inc / "mjx.h"
+    victim.write_text(victim.read_text().replace("\n// changed\n", ""))
+    _lib.verify_build_id(lib, str(csrc), str(inc))
+    hdr.write_text(hdr.read_text().replace("MJX_H", "MJX_H_"))
+    with pytest.raises(mjx_mod.MjxError):
+        _lib.verify_build_id(lib, str(csrc), str(inc))
