@@ -59,6 +59,11 @@ def parse():
     ap.add_argument("--sa-warmin", type=int, default=10000,
                     help="proposals every SA replica makes before the timed region (steady state, not t=0)")
     ap.add_argument("--c1-steps", type=int, default=10000)
+    ap.add_argument("--c1-cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--consensus-replicas", type=int, default=64)
+    ap.add_argument("--consensus-max-s", type=float, default=90.0,
+                    help="wall-time cap of the run-to-consensus leg (reported, not hidden, if hit)")
+    ap.add_argument("--no-consensus", action="store_true")
     ap.add_argument("--no-sa", action="store_true")
     ap.add_argument("--giant-n", type=int, default=1_000_000_000)
     ap.add_argument("--giant-d", type=int, default=6)
@@ -161,8 +166,27 @@ def dry_run(args, rank, world):
 # ---------------------------------------------------------------------------
 # CPU baseline (runs BEFORE the GPU is touched: forked workers, no exec)
 # ---------------------------------------------------------------------------
+def cpu_share():
+    """Host cores this process may use: the CPUs in its affinity mask, capped by
+    the cgroup CPU quota (cpu.max) when one is set -- the GPU box lists 256 CPUs
+    in the mask but grants a 16-CPU share (cpu.max 1600000 100000)."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return (min(avail, quota) if quota else avail), avail, quota
+
+
 def host_info():
-    """CPU model, os.cpu_count() and library versions."""
+    """CPU model, os.cpu_count(), the CPU share and library versions."""
     model = None
     try:
         with open("/proc/cpuinfo") as f:
@@ -172,7 +196,9 @@ def host_info():
                     break
     except OSError:
         pass
-    info = {"cpu_model": model, "os_cpu_count": os.cpu_count(), "numpy": np.__version__}
+    cores, affinity, quota = cpu_share()
+    info = {"cpu_model": model, "os_cpu_count": os.cpu_count(), "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
+            "cpu_share": cores, "numpy": np.__version__}
     try:
         import torch
         info["torch"] = torch.__version__
@@ -195,15 +221,16 @@ def _cpu_worker(args):
     return done, time.perf_counter() - t0
 
 
-def cpu_baseline(adj, T, seconds):
-    import multiprocessing as mp
-    try:
-        avail = len(os.sched_getaffinity(0))
-    except AttributeError:
-        avail = os.cpu_count() or 1
-    cores = max(1, min(16, avail, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
+def _single_thread_numpy():
     for k in ("OMP_NUM_THREADS", "MKL_NUM_THREADS", "OPENBLAS_NUM_THREADS"):
         os.environ[k] = "1"
+
+
+def cpu_baseline(adj, T, seconds):
+    """One process per core of the CPU share (cpu_share()), numpy single-threaded."""
+    import multiprocessing as mp
+    cores = cpu_share()[0]
+    _single_thread_numpy()
     ctx = mp.get_context("fork")
     t0 = time.perf_counter()
     with ctx.Pool(cores) as pool:
@@ -278,36 +305,111 @@ def bench_sa(args, rank, world, dist, dev):
     return out
 
 
-def bench_sa_c1(args, rank, world, dist, dev):
-    """configs[0] literally: SA_RRG.py's own case, d=4 RRG, N=1e4, p=c=1,
-    64 replicas (numpy seeds), light-cone SA on the GPU after a warm-in, timed
-    beside the numpy restatement of the reference's SA step (oracle/majority.py
-    sa_loop: three full rollouts per proposal, code/SA_RRG.py:63-88) on one
-    host core, on the same graph and seed."""
+def _sa_cpu_worker(args):
+    """numpy restatement of the reference's SA loop (three rollouts per
+    proposal, code/SA_RRG.py:63-88) on the replicas given, ~seconds in all:
+    a short calibration run, then an equal proposal budget per replica."""
+    graphs, p, c, seeds, seconds = args
+    from oracle import majority as orc
+    t0 = time.perf_counter()
+    done = orc.sa_loop(graphs[0], p, c, seeds[0], max_steps=50)["num_steps"]
+    per = (time.perf_counter() - t0) / max(1, done)
+    budget = max(50, int((seconds - (time.perf_counter() - t0)) / per / len(graphs)))
+    for g, sd in zip(graphs, seeds):
+        done += orc.sa_loop(g, p, c, sd, max_steps=budget)["num_steps"]
+    return done, time.perf_counter() - t0
+
+
+def sa_cpu_baseline(graphs, p, c, seeds, seconds):
+    """configs[0]'s CPU reference: the replicas spread over one process per
+    core of the CPU share, each running the numpy SA loop."""
+    import multiprocessing as mp
+    cores = min(cpu_share()[0], len(seeds))
+    _single_thread_numpy()
+    parts = [([], []) for _ in range(cores)]
+    for k, (g, sd) in enumerate(zip(graphs, seeds)):
+        parts[k % cores][0].append(g)
+        parts[k % cores][1].append(sd)
+    with mp.get_context("fork").Pool(cores) as pool:
+        res = pool.map(_sa_cpu_worker, [(gs, p, c, sds, seconds) for gs, sds in parts])
+    props = sum(r[0] for r in res)
+    wall = max(r[1] for r in res)
+    return {"proposals_per_s": props / wall, "cores": cores, "kind": "port", "host": host_info(),
+            "sample": f"oracle/majority.py sa_loop (numpy, code/SA_RRG.py:63-88, three rollouts per proposal), "
+                      f"{len(seeds)} replicas each on its own graph spread over {cores} processes, {props} "
+                      f"proposals in {wall:.1f} s"}
+
+
+def bench_sa_c1(args, rank, world, dist, dev, c1_cpu=None):
+    """configs[0] literally: SA_RRG.py's own case, d=4 RRG, N=1e4, p=c=1, 64
+    replicas, each on its OWN graph as the script draws them
+    (code/SA_RRG.py:58-62), all 64 run together (graphs stacked in HBM),
+    light-cone SA after a warm-in; the same replicas on one shared graph
+    beside it; the numpy restatement of the reference's SA loop on the host
+    cores (measured before the GPU was touched) as the CPU baseline."""
     import torch
     import mjx
     n, d, p, c, R = 10_000, 4, 1, 1, 64
-    adj = mjx.random_regular_graph(d, n, seed=args.seed + 1000 + rank)
+    graphs = c1_graphs(args, rank)
     seeds = list(range(rank * R, (rank + 1) * R))
-    sa = mjx.SAReplicas(adj, p, c, seeds)
-    sa.steps(args.sa_warmin)
     K = args.c1_steps
-    el = _timed(lambda: sa.steps(K), dist, dev)
-    props = world * R * K / el
-    res = {"config": "configs[0]: SA_RRG.py case, d=4 RRG N=1e4, p=c=1, 64 replicas per GPU (numpy seeds), "
-                     f"{K} proposals per replica after {args.sa_warmin} warm-in proposals",
-           "mode": sa.mode, "proposals_per_s": props, "sweeps_per_s": props / n, "ms_per_step": 1e3 * el / K}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        from oracle import majority as orc
-        t0 = time.perf_counter()
-        o = orc.sa_loop(adj, p, c, seeds[0], max_steps=2000)
-        cpu_s = time.perf_counter() - t0
-        res["cpu_baseline"] = {"proposals_per_s": o["num_steps"] / cpu_s, "cores": 1, "kind": "port", "host": host_info(),
-                               "sample": f"oracle/majority.py sa_loop (numpy, code/SA_RRG.py:63-88, three rollouts "
-                                         f"per proposal) on the same graph, seed {seeds[0]}, {o['num_steps']} "
-                                         f"proposals in {cpu_s:.1f} s, one core (the reference runs its replicas "
-                                         f"one after another on one core)"}
-        res["speedup_vs_cpu"] = props / res["cpu_baseline"]["proposals_per_s"]
+    res = {"config": "configs[0]: SA_RRG.py case, d=4 RRG N=1e4, p=c=1, 64 replicas per GPU (numpy seeds), each on "
+                     f"its own graph (code/SA_RRG.py:58-62), {K} proposals per replica after {args.sa_warmin} "
+                     "warm-in proposals"}
+    for tag, src in (("distinct_graphs", graphs), ("shared_graph", graphs[0])):
+        sa = mjx.SAReplicas(src, p, c, seeds)
+        sa.steps(args.sa_warmin)
+        el = _timed(lambda: sa.steps(K), dist, dev)
+        props = world * R * K / el
+        res[tag] = {"mode": sa.mode, "proposals_per_s": props, "sweeps_per_s": props / n, "ms_per_step": 1e3 * el / K}
+        del sa
+    res["proposals_per_s"] = res["distinct_graphs"]["proposals_per_s"]
+    if c1_cpu is not None:
+        res["cpu_baseline"] = c1_cpu
+        res["speedup_vs_cpu"] = res["proposals_per_s"] / c1_cpu["proposals_per_s"]
+    return res
+
+
+def c1_graphs(args, rank):
+    import mjx
+    return [mjx.random_regular_graph(4, 10_000, seed=args.seed + 1000 + 64 * rank + k) for k in range(64)]
+
+
+def bench_sa_consensus(args, rank, world, dist, dev):
+    """SA_RRG.py's own configuration run to the end: n=1e4, d=4, p=3, c=1
+    (code/SA_RRG.py:44-52), every replica on its own fresh graph, until
+    m(s_endstate(s)) = 1 or t > 2n^3 (code/SA_RRG.py:72-85); 64 replicas per
+    GPU run together.  Reports the wall time to consensus and the num_steps /
+    mag_reached distributions (the script's np.savez keys)."""
+    import torch
+    import mjx
+    n, d, p, c, R = 10_000, 4, 3, 1, args.consensus_replicas
+    graphs = [mjx.random_regular_graph(d, n, seed=args.seed + 5000 + R * rank + k) for k in range(R)]
+    seeds = list(range(10_000 + rank * R, 10_000 + (rank + 1) * R))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    sa = mjx.SAReplicas(graphs, p, c, seeds)
+    torch.cuda.synchronize()
+    init_s = time.perf_counter() - t0
+    chunk, t0, taken = 4096, time.perf_counter(), 0
+    while not sa.all_done() and time.perf_counter() - t0 < args.consensus_max_s:
+        sa.steps(chunk)
+        taken += chunk
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    out = sa.results()
+    steps, mag, done = out["num_steps"], out["mag_reached"], out["done"]
+    res = {"config": f"SA_RRG.py's configuration: d={d} RRG N={n}, p={p} c={c}, {R} replicas per GPU each on its own "
+                     "graph, run to consensus (m_final = 1) or t > 2n^3",
+           "mode": sa.mode, "replicas": R, "init_s": init_s, "wall_s_to_consensus": wall,
+           "all_done": bool((done != 0).all()), "replicas_done": int((done != 0).sum()),
+           "proposals_launched_per_replica": taken,
+           "num_steps": {"min": float(steps.min()), "median": float(np.median(steps)), "mean": float(steps.mean()),
+                         "max": float(steps.max())},
+           "mag_reached": {"min": float(mag.min()), "mean": float(mag.mean()), "max": float(mag.max())},
+           "proposals_per_s": float(steps.sum()) / wall,
+           "time_cap_s": args.consensus_max_s}
+    del sa
     return res
 
 
@@ -554,11 +656,7 @@ def bench_hpr(args, rank, world, dist, dev):
         chi_h = chi.double().cpu()
         b_h = b.double().cpu()
         rows = np.random.default_rng(0).choice(msgs, size=2048, replace=False)
-        try:
-            avail = len(os.sched_getaffinity(0))
-        except AttributeError:
-            avail = os.cpu_count() or 1
-        cores = max(1, min(16, avail))
+        cores = cpu_share()[0]
         old_threads = torch.get_num_threads()
         torch.set_num_threads(cores)
         hpr_torch.HPr_dp(chi_h, b_h, inr, src, n, d, p, c, 1, lmbd, 0.4, rows[:64])      # warm-up
@@ -657,9 +755,11 @@ def main():
     import mjx
     adj = mjx.random_regular_graph(d, n, seed=args.seed + 1000 * rank)
 
-    cpu = None
+    cpu = c1_cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(adj, T, args.cpu_seconds)
+        if not args.no_sa and args.c1_steps > 0:
+            c1_cpu = sa_cpu_baseline(c1_graphs(args, 0), 1, 1, list(range(64)), args.c1_cpu_seconds)
 
     import torch
     torch.cuda.set_device(local_rank)
@@ -727,7 +827,10 @@ def main():
         sa_res = bench_sa(args, rank, world, dist, dev)
     c1 = None
     if not args.no_sa and args.c1_steps > 0:
-        c1 = bench_sa_c1(args, rank, world, dist, dev)
+        c1 = bench_sa_c1(args, rank, world, dist, dev, c1_cpu)
+    cons = None
+    if not args.no_sa and not args.no_consensus and args.consensus_replicas > 0:
+        cons = bench_sa_consensus(args, rank, world, dist, dev)
 
     del s0, out, tmp, counts, chk, o2
     torch.cuda.empty_cache()
@@ -746,7 +849,7 @@ def main():
     if not args.no_giant and args.giant_n > 0:
         giant = bench_giant(args, rank, world, dist, dev)
 
-    for leg in (sa_res, c1, er, hpr, bdcm, giant):
+    for leg in (sa_res, c1, cons, er, hpr, bdcm, giant):
         if leg is not None:
             leg["n_gpus"] = world
             leg["ranks"] = world
@@ -784,6 +887,7 @@ def main():
             "cpu_baseline": cpu,
             "sa": sa_res,
             "sa_c1": c1,
+            "sa_consensus": cons,
             "er": er,
             "hpr": hpr,
             "bdcm": bdcm,

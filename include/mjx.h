@@ -86,6 +86,15 @@ int mjx_rollout_ell_np(const int32_t* adj, int64_t n, int d,
 int mjx_rollout_ell_rp(const int32_t* adj, int64_t n, int d, int64_t words,
                        const uint64_t* s_in, uint64_t* s_out, uint64_t* tmp,
                        int steps, unsigned long long* counts, void* stream);
+/* mjx_rollout_ell_rp with a graph per replica: R replicas in W = ceil(R/64)
+ * words per node; replica r (bit r&63 of word column r>>6) runs on graph
+ * rep_graph[r] (device int32[R]) of a stack of graphs, graph g's rows at
+ * adj + g*n*d; padding replicas (r >= R) are written as -1 (bit 0).  counts
+ * (nullable): [R], added.  The reference's SA draws one graph per replica
+ * (code/SA_RRG.py:58-62). */
+int mjx_rollout_ell_rp_multi(const int32_t* adj, int64_t n, int d, int64_t R, const int32_t* rep_graph,
+                             const uint64_t* s_in, uint64_t* s_out, uint64_t* tmp,
+                             int steps, unsigned long long* counts, void* stream);
 /* The replica-packed rollout run slice by slice: slice q of S covers word units
  * [q*U/S, (q+1)*U/S) of every node (U = words/2 16-byte units, or words if
  * odd); replicas never interact, so the result is identical for every S.
@@ -160,11 +169,26 @@ typedef struct mjx_sa_state {
     int32_t*  tape_i;    /* [tape_cap*R] */
     double*   tape_u;    /* [tape_cap*R] */
     int64_t   tape_cap;
+    /* distinct graphs (nullable = every replica on the one graph `adj`):
+     * replica r runs on graph rep_graph[r] (device int32[R]) of a stack of
+     * graphs with the same n and d, graph g's rows at adj + g*n*d (and at
+     * adj_pad + g*n*4 for the padded d = 3 rows).  The reference draws a
+     * fresh graph per replica (code/SA_RRG.py:58-62). */
+    const int32_t* rep_graph;
+    /* light-cone kernel selection, 0 = the library's choice (tests and tuning
+     * set them; nothing is read from the environment) */
+    int32_t   opt_split;   /* waves per 64-replica word column: 1, 2, 4, ..., 64 */
+    int32_t   opt_spec_k;  /* speculative batch width: 8 or 16 */
+    uint32_t  opt_flags;   /* MJX_SA_NO_SPEC | MJX_SA_NO_CONE2 */
 } mjx_sa_state;
+
+#define MJX_SA_NO_SPEC   1u   /* no speculative batches (k_sa_spec) */
+#define MJX_SA_NO_CONE2  2u   /* no one-round-trip step (k_sa_cone2) */
 
 /* Seed replica r with seeds[r] (device uint32[R]), draw s0 into the
  * replica-packed spins s[n*W], set a=a0, b=b0, t=0, done=0, and
- * sum_end = sum(s_endstate(s0)) using tmp1/tmp2 ([n*W] each). */
+ * sum_end = sum(s_endstate(s0)) using tmp1/tmp2 ([n*W] each); with
+ * st->rep_graph each replica's rollout runs on its own graph. */
 int mjx_sa_init(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R,
                 const uint32_t* seeds, double a0, double b0,
                 uint64_t* s, uint64_t* tmp1, uint64_t* tmp2,
@@ -198,10 +222,12 @@ int mjx_sa_steps(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R,
  * Supported: 1 <= T <= 6, d <= 16 and mjx_sa_lightcone_lds(d,p,c) <= 150 KiB
  * (bytes of LDS per 64 replicas; -1 if unsupported).  The step kernel runs
  * several waves per 64-replica word column when the column count is small
- * (environment MJX_LC_SPLIT = 1, 2, 4, ..., 64 overrides the choice). */
+ * (st->opt_split overrides the choice).  rep_graph (nullable): as in
+ * mjx_sa_state, for the levels of replicas on distinct graphs. */
 int64_t mjx_sa_lightcone_lds(int d, int p, int c);
 int mjx_sa_lightcone_prepare(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R,
-                             const uint64_t* s, uint64_t* const* levels, void* stream);
+                             const int32_t* rep_graph, const uint64_t* s, uint64_t* const* levels,
+                             void* stream);
 int mjx_sa_lightcone_steps(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R,
                            uint64_t* s, uint64_t* const* levels, mjx_sa_state* st, int64_t nsteps,
                            double par_a, double par_b, double a_cap, double b_cap, int64_t t_cap,
@@ -230,6 +256,21 @@ int mjx_sa_cone_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int
                       uint64_t* s, uint64_t* cone, mjx_sa_state* st, int64_t nsteps,
                       double par_a, double par_b, double a_cap, double b_cap, int64_t t_cap,
                       void* stream);
+
+/* LDS-resident light-cone SA (small graphs, the reference's own sizes: n = 1e4,
+ * d = 4, code/SA_RRG.py:44-52): a workgroup per replica keeps its graph (uint16
+ * rows), the rollout levels onestep^t(s) (t = 0..p+c-1, bit arrays) and its
+ * MT19937 state in LDS for the whole call; levels are rebuilt from s at the
+ * start of every call, the changed configuration bits XORed back into s and
+ * the stream state written back at its end (exactly numpy's position: nothing
+ * is drawn ahead).  Same proposals, accepts and outputs as mjx_sa_steps;
+ * honours st->rep_graph and the trace pointers; no tape, no level arrays.
+ * mjx_sa_lds_bytes: LDS bytes per replica, -1 if (n, d, p, c) does not fit
+ * (n <= 65535, d <= 16, 1 <= p+c-1 <= 6, <= 160 KiB). */
+int64_t mjx_sa_lds_bytes(int64_t n, int d, int p, int c);
+int mjx_sa_lds_steps(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R, uint64_t* s,
+                     mjx_sa_state* st, int64_t nsteps, double par_a, double par_b, double a_cap, double b_cap,
+                     int64_t t_cap, void* stream);
 
 /* ---- history-passing reinforcement on d-regular graphs ------------------ */
 /*
@@ -363,10 +404,12 @@ int mjx_sweep_ell_np_range(const int32_t* adj, int64_t n, int d, int64_t row_lo,
 int mjx_binned_plan_shape(int64_t n, int d, int64_t row_lo, int64_t row_hi, int64_t* sizes);
 int mjx_binned_build(const int32_t* adj, int64_t n, int d, int64_t row_lo, int64_t row_hi, uint16_t* src_lo,
                      uint16_t* src_hi, uint16_t* off, long long* index, void* work, int64_t work_bytes, void* stream);
+/* apply_form: 0 = the library's choice, 1 = flat tile stream (K <= 960 source
+ * blocks, MJX_ERANGE beyond), 2 = per-segment form. */
 int mjx_sweep_binned(const uint16_t* src_lo, const uint16_t* src_hi, const uint16_t* off, const long long* index,
                      int64_t n, int d,
                      int64_t row_lo, int64_t row_hi, const uint64_t* s_in, uint64_t* msg, uint64_t* s_out,
-                     unsigned long long* counts, void* stream);
+                     unsigned long long* counts, int apply_form, void* stream);
 
 /* Device Erdos-Renyi G(n, p) into CSR, replacing
  * nx.erdos_renyi_graph + isolate removal + relabelling of

@@ -29,6 +29,7 @@ SIGNATURES = {
     "mjx_unpack_rp": [c_vp, c_i64, c_i64, c_vp, c_int, c_vp],
     "mjx_rollout_ell_np": [c_vp, c_i64, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp],
     "mjx_rollout_ell_rp": [c_vp, c_i64, c_int, c_i64, c_vp, c_vp, c_vp, c_int, c_vp, c_vp],
+    "mjx_rollout_ell_rp_multi": [c_vp, c_i64, c_int, c_i64, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp],
     "mjx_rollout_ell_rp_sliced": [c_vp, c_i64, c_int, c_i64, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp],
     "mjx_rollout_csr_rp_ordered": [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_int, c_vp, c_vp],
     "mjx_rollout_csr_np": [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_int, c_vp, c_vp],
@@ -44,9 +45,12 @@ SIGNATURES = {
     "mjx_sa_steps": [c_vp, c_i64, c_int, c_int, c_int, c_i64, c_vp, c_vp, c_vp, c_vp,
                      c_i64, c_dbl, c_dbl, c_dbl, c_dbl, c_i64, c_vp],
     "mjx_sa_lightcone_lds": [c_int, c_int, c_int],
-    "mjx_sa_lightcone_prepare": [c_vp, c_i64, c_int, c_int, c_int, c_i64, c_vp, c_vp, c_vp],
+    "mjx_sa_lightcone_prepare": [c_vp, c_i64, c_int, c_int, c_int, c_i64, c_vp, c_vp, c_vp, c_vp],
     "mjx_sa_lightcone_steps": [c_vp, c_i64, c_int, c_int, c_int, c_i64, c_vp, c_vp, c_vp,
                                c_i64, c_dbl, c_dbl, c_dbl, c_dbl, c_i64, c_vp],
+    "mjx_sa_lds_bytes": [c_i64, c_int, c_int, c_int],
+    "mjx_sa_lds_steps": [c_vp, c_i64, c_int, c_int, c_int, c_i64, c_vp, c_vp, c_i64, c_dbl, c_dbl, c_dbl, c_dbl,
+                         c_i64, c_vp],
     "mjx_sa_cone_words": [c_int, c_int],
     "mjx_sa_cone_pack": [c_i64, c_int, c_int, c_i64, c_vp, c_vp, c_vp, c_vp],
     "mjx_sa_cone_unpack": [c_i64, c_int, c_int, c_i64, c_vp, c_vp, c_vp, c_vp],
@@ -78,7 +82,7 @@ SIGNATURES = {
     "mjx_er_generate": [c_i64, c_dbl, c_u64, c_int, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp],
     "mjx_binned_plan_shape": [c_i64, c_int, c_i64, c_i64, c_vp],
     "mjx_binned_build": [c_vp, c_i64, c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp],
-    "mjx_sweep_binned": [c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "mjx_sweep_binned": [c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_int, c_vp],
     "mjx_bdcm_lds_bytes": [c_int, c_int, c_int],
     "mjx_bdcm_scratch_bytes": [c_int, c_int, c_int],
     "mjx_bdcm_update_class": [c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_int, c_dbl, c_dbl, c_dbl, c_vp,
@@ -91,7 +95,7 @@ SIGNATURES = {
     "mjx_sum_f64": [c_vp, c_i64, c_int, c_vp, c_vp, c_vp],
 }
 _RESTYPES = {"mjx_strerror": ctypes.c_char_p, "mjx_build_id": ctypes.c_char_p, "mjx_last_hip_error": ctypes.c_char_p,
-             "mjx_sa_lightcone_lds": c_i64, "mjx_bdcm_lds_bytes": c_i64, "mjx_bdcm_scratch_bytes": c_i64,
+             "mjx_sa_lightcone_lds": c_i64, "mjx_sa_lds_bytes": c_i64, "mjx_bdcm_lds_bytes": c_i64, "mjx_bdcm_scratch_bytes": c_i64,
              "mjx_rrg_partner_host": c_i64, "mjx_er_work_bytes": c_i64, "mjx_hpr_er_scratch_bytes": c_i64}
 
 MJX_OK, MJX_EINVAL, MJX_EHIP, MJX_ERANGE = 0, 1, 2, 3      # status codes (include/mjx.h)
@@ -107,7 +111,12 @@ class MjxSaState(ctypes.Structure):
         ("prop_u", c_vp), ("cnt", c_vp),
         ("tr_i", c_vp), ("tr_acc", c_vp), ("tr_sum", c_vp), ("tr_dE", c_vp), ("tr_tie", c_vp),
         ("tape_i", c_vp), ("tape_u", c_vp), ("tape_cap", c_i64),
+        ("rep_graph", c_vp), ("opt_split", ctypes.c_int32), ("opt_spec_k", ctypes.c_int32),
+        ("opt_flags", ctypes.c_uint32),
     ]
+
+
+MJX_SA_NO_SPEC, MJX_SA_NO_CONE2 = 1, 2          # mjx_sa_state.opt_flags (include/mjx.h)
 
 
 class MjxError(RuntimeError):

@@ -124,6 +124,7 @@ class BDCMPlan:
         if need and getattr(self, "_scratch_key", None) != key:
             self._scratch = torch.empty(need, dtype=torch.uint8, device=self.device)
             self._scratch_key = key
+            self._drop_graphs()            # a captured loop holds the old slab's address
         return self._scratch if need else None
 
     def check_sizes(self, p, c):
@@ -135,7 +136,12 @@ class BDCMPlan:
         need = max((m for _, _, _, m in self.edge_classes), default=0) * nc
         if self._upd is None or self._upd.numel() < need:
             self._upd = torch.empty(max(need, 1), dtype=torch.float64, device=self.device)
+            self._drop_graphs()            # a captured loop holds the old buffer's address
         return self._upd
+
+    def _drop_graphs(self):
+        if getattr(self, "_graphs", None):
+            self._graphs.clear()
 
     @classmethod
     def from_networkx(cls, G, n_total=None, n_iso=0):
@@ -217,8 +223,8 @@ def converge(chi, plan, p, c, attr_value, lmbd_in, damppar, eps, T_max, epsilon=
     reference's loop; chi ends in the state after sweep t exactly (the sweeps
     past the stop are no-ops)."""
     ch = _chi2d(chi, plan, p, c)
-    plan.check_sizes(p, c)
-    plan.upd(ch.shape[1])                    # every buffer exists before a capture
+    sc = plan.scratch(p, c)
+    upd = plan.upd(ch.shape[1])              # every buffer exists before a capture
     ctl = plan._ctl
     ctl.zero_()
     g = None
@@ -227,8 +233,9 @@ def converge(chi, plan, p, c, attr_value, lmbd_in, damppar, eps, T_max, epsilon=
         import math
         w_dev = plan._w
         w_dev.copy_(torch.tensor([math.exp(-lmbd_in), math.exp(lmbd_in)], dtype=torch.float64))
-        key = (ch.data_ptr(), int(p), int(c), int(attr_value), float(damppar), float(eps),
-               int(T_max), float(epsilon), int(batch))
+        # every address the capture bakes in is part of the key
+        key = (ch.data_ptr(), upd.data_ptr(), sc.data_ptr() if sc is not None else None, int(p), int(c),
+               int(attr_value), float(damppar), float(eps), int(T_max), float(epsilon), int(batch))
         cache = getattr(plan, "_graphs", None)
         if cache is None:
             cache = plan._graphs = {}

@@ -10,6 +10,7 @@
 // HBM-bound by design: per node and sweep the kernels read d int32 indices,
 // gather d neighbour state rows, read the node's own row and write one row.
 #include "mjx_common.h"
+#include <algorithm>
 #include <string.h>
 #include <stdio.h>
 #include <mutex>
@@ -698,7 +699,7 @@ __global__ void __launch_bounds__(kBlock) k_popcount_rp(const u64* __restrict__ 
 // ===========================================================================
 using namespace mjx;
 
-extern "C" int mjx_abi_version(void) { return 1; }
+extern "C" int mjx_abi_version(void) { return 2; }
 
 extern "C" const char* mjx_strerror(int status) {
     switch (status) {
@@ -993,6 +994,64 @@ extern "C" int mjx_rollout_ell_rp_sliced(const int32_t* adj, int64_t n, int d, i
         if (rc) return rc;
     }
     return MJX_OK;
+}
+
+// One synchronous sweep with a graph per replica (code/SA_RRG.py:58-62 draws a
+// graph per replica; the sweep itself is code/SA_RRG.py:18-20).  Lane = replica
+// r of word column w = blockIdx.y, each wave strides over nodes; a lane gathers
+// the d neighbour words of ITS graph and keeps its own bit, the wave's 64 new
+// bits are one ballot.  Setup-path kernel (initial levels of distinct-graph SA
+// replicas): d random 8-B loads per replica-node, not the bit-parallel sweep.
+template <bool COUNT>
+__global__ void __launch_bounds__(kBlock) k_sweep_multi_rp(const int32_t* __restrict__ adj, int64_t n, int d,
+                                                           int64_t R, int64_t W, const int32_t* __restrict__ rep_graph,
+                                                           const u64* __restrict__ s_in, u64* __restrict__ s_out,
+                                                           unsigned long long* __restrict__ counts) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w = blockIdx.y;
+    const int64_t r = w * 64 + lane;
+    const bool live = r < R;
+    const int32_t* a = adj + (live ? (int64_t)rep_graph[r] : 0) * n * d;
+    const u64 bit = 1ull << lane;
+    const int64_t waves = (int64_t)gridDim.x * (kBlock / 64);
+    unsigned long long cnt = 0;
+    for (int64_t v = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); v < n; v += waves) {
+        bool nb = false;
+        if (live) {
+            int ones = 0;
+            for (int j = 0; j < d; ++j) ones += (s_in[(int64_t)a[v * d + j] * W + w] & bit) ? 1 : 0;
+            const bool own = (s_in[v * W + w] & bit) != 0;
+            nb = (2 * ones > d) ? true : ((2 * ones < d) ? false : own);     // always-stay majority
+        }
+        const u64 word = __ballot(nb);
+        if (lane == 0) s_out[v * W + w] = word;
+        if constexpr (COUNT) cnt += nb ? 1 : 0;
+    }
+    if constexpr (COUNT) {
+        if (live && cnt) atomicAdd(&counts[r], cnt);
+    }
+}
+
+extern "C" int mjx_rollout_ell_rp_multi(const int32_t* adj, int64_t n, int d, int64_t R, const int32_t* rep_graph,
+                                        const uint64_t* s_in, uint64_t* s_out, uint64_t* tmp, int steps,
+                                        unsigned long long* counts, void* stream) {
+    if (n < 1 || d < 1 || d > 255 || R < 1 || !adj || !rep_graph || !s_in || !s_out || steps < 1) return MJX_EINVAL;
+    if (n > (int64_t)INT32_MAX) return MJX_ERANGE;
+    if (overlaps(s_in, s_out) || overlaps(s_in, tmp) || overlaps(s_out, tmp)) return MJX_EINVAL;
+    const int64_t W = (R + 63) / 64;
+    if (W > 65535) return MJX_ERANGE;
+    hipStream_t st = as_stream(stream);
+    int64_t gx = (n + 3) / 4;
+    const int64_t cap = std::max<int64_t>(1, (int64_t)kCUs * 8 / W);
+    if (gx > cap) gx = cap;
+    const dim3 grid((unsigned)gx, (unsigned)W);
+    auto sweep = [&](const u64* a, u64* b, unsigned long long* c) -> int {
+        if (c) k_sweep_multi_rp<true><<<grid, kBlock, 0, st>>>(adj, n, d, R, W, rep_graph, a, b, c);
+        else k_sweep_multi_rp<false><<<grid, kBlock, 0, st>>>(adj, n, d, R, W, rep_graph, a, b, nullptr);
+        MJX_LAUNCH_CHECK("k_sweep_multi_rp");
+        return MJX_OK;
+    };
+    return run_rollout(steps, (const u64*)s_in, (u64*)s_out, (u64*)tmp, counts, sweep);
 }
 
 extern "C" int mjx_rollout_ell_rp(const int32_t* adj, int64_t n, int d, int64_t words, const uint64_t* s_in,

@@ -949,10 +949,11 @@ extern "C" int mjx_binned_build(const int32_t* adj, int64_t n, int d, int64_t ro
 extern "C" int mjx_sweep_binned(const uint16_t* src_lo, const uint16_t* src_hi, const uint16_t* off,
                                 const long long* index, int64_t n, int d,
                                 int64_t row_lo, int64_t row_hi, const uint64_t* s_in, uint64_t* msg, uint64_t* s_out,
-                                unsigned long long* counts, void* stream) {
+                                unsigned long long* counts, int apply_form, void* stream) {
     using namespace mjx::binned;
     const int rc = check_range(n, d, row_lo, row_hi);
     if (rc) return rc;
+    if (apply_form < 0 || apply_form > 2) return MJX_EINVAL;
     if (row_hi == row_lo) return MJX_OK;
     if (!src_lo || !src_hi || !off || !index || !s_in || !msg || !s_out || s_in == s_out) return MJX_EINVAL;
     const Shape s = shape(n, d, row_hi - row_lo);
@@ -973,10 +974,10 @@ extern "C" int mjx_sweep_binned(const uint16_t* src_lo, const uint16_t* src_hi, 
         src_lo, src_hi, blk, n, split, (const uint32_t*)s_in, (mjx::u64*)msg);
     MJX_LAUNCH_CHECK("k_bin_msg");
     // the flat form streams the tile contiguously; it needs the tile's
-    // segment table in LDS (K <= kFlatMaxK: n <= ~1e9); MJX_BIN_APPLY=segments
-    // forces the per-segment form (tests)
-    const char* form = getenv("MJX_BIN_APPLY");
-    const bool flat = s.K <= kFlatMaxK && !(form && form[0] == 's');
+    // segment table in LDS (K <= kFlatMaxK: n <= ~1e9); apply_form 2 asks for
+    // the per-segment form (tests run both)
+    if (apply_form == 1 && s.K > kFlatMaxK) return MJX_ERANGE;
+    const bool flat = s.K <= kFlatMaxK && apply_form != 2;
     if (flat) {
         MJX_HIP(hipFuncSetAttribute((const void*)k_bin_apply_flat<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     kCntWords * (int)sizeof(uint32_t)), "k_bin_apply_flat lds");

@@ -925,12 +925,8 @@ static int launch_update(const void* chi_in, void* chi_out, const void* biases, 
         const int64_t tiles = (n + C::NT - 1) / C::NT;
         if (tiles > INT32_MAX) return MJX_ERANGE;
         if constexpr (std::is_same<S, float>::value && T == 4) {
-            // 1 KB rows: the software-pipelined persistent form (MJX_HPR_PIPE=0 selects the other)
-            static const bool pipe = [] {
-                const char* e = getenv("MJX_HPR_PIPE");
-                return !(e && e[0] == '0');
-            }();
-            if (pipe) {
+            // 1 KB rows: the software-pipelined persistent form
+            {
                 using PC = PipeCfg<T, P, D>;
                 auto pk = k_hpr_update_pipe<T, P, D>;
                 static bool pattr = false;

@@ -19,6 +19,7 @@
 // evaluated as ((-2*a)*s_i + b*D)/n with separately rounded operations, as
 // numpy does (code/SA_RRG.py:37).
 #include "mjx_common.h"
+#include "mjx_mt.h"
 #include <math.h>
 #include <stdlib.h>
 #include <algorithm>
@@ -26,29 +27,6 @@
 #pragma clang fp contract(off)
 
 namespace mjx {
-
-constexpr int MT_N = 624;
-constexpr int MT_M = 397;
-constexpr uint32_t MT_MATRIX_A = 0x9908b0dfu;
-constexpr uint32_t MT_UPPER = 0x80000000u;
-constexpr uint32_t MT_LOWER = 0x7fffffffu;
-
-__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
-    y ^= (y >> 11);
-    y ^= (y << 7) & 0x9d2c5680u;
-    y ^= (y << 15) & 0xefc60000u;
-    y ^= (y >> 18);
-    return y;
-}
-
-__device__ __forceinline__ uint32_t mt_mix(uint32_t cur, uint32_t nxt, uint32_t far) {
-    uint32_t y = (cur & MT_UPPER) | (nxt & MT_LOWER);
-    return far ^ (y >> 1) ^ ((y & 1u) ? MT_MATRIX_A : 0u);
-}
-
-__device__ __forceinline__ double mt_double(uint32_t w1, uint32_t w2) {
-    return ((double)(w1 >> 5) * 67108864.0 + (double)(w2 >> 6)) / 9007199254740992.0;
-}
 
 // ---------------------------------------------------------------------------
 // init: 64 replicas per block (one wave); their MT states live in LDS laid out
@@ -110,33 +88,6 @@ __global__ void __launch_bounds__(64) k_sa_init_draw(int64_t n, int64_t R, int64
 // transpose per (word column, node word) writes the replica-packed layout.
 // Same stream, same spins as k_sa_init_draw, with 64x the parallelism.
 // ---------------------------------------------------------------------------
-__device__ void lds_twist(uint32_t* buf, int lane) {
-    for (int k = lane; k < MT_N - MT_M; k += 64) {
-        const uint32_t v = mt_mix(buf[k], buf[k + 1], buf[k + MT_M]);
-        __builtin_amdgcn_wave_barrier();
-        buf[k] = v;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-    }
-    for (int k = MT_N - MT_M + lane; k < 2 * (MT_N - MT_M); k += 64) {
-        const uint32_t v = mt_mix(buf[k], buf[k + 1], buf[k + MT_M - MT_N]);
-        __builtin_amdgcn_wave_barrier();
-        buf[k] = v;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-    }
-    for (int k = 2 * (MT_N - MT_M) + lane; k < MT_N - 1; k += 64) {
-        const uint32_t v = mt_mix(buf[k], buf[k + 1], buf[k + MT_M - MT_N]);
-        __builtin_amdgcn_wave_barrier();
-        buf[k] = v;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-    }
-    if (lane == 0) buf[MT_N - 1] = mt_mix(buf[MT_N - 1], buf[0], buf[MT_M - 1]);
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-}
-
 __global__ void __launch_bounds__(64) k_sa_init_np(int64_t n, int64_t R, int64_t r0, const uint32_t* __restrict__ seeds,
                                                    u64* __restrict__ np_bits, uint32_t* __restrict__ mt_out,
                                                    int32_t* __restrict__ idx_out) {
@@ -886,7 +837,8 @@ __global__ void __launch_bounds__(64) k_sa_lightcone(const int32_t* __restrict__
                                                      int64_t W, LcLevels L, int T, mjx_sa_state st, int64_t nsteps,
                                                      double par_a, double par_b, double a_cap, double b_cap,
                                                      int64_t t_cap, const int32_t* __restrict__ tape_i,
-                                                     const double* __restrict__ tape_u, int split) {
+                                                     const double* __restrict__ tape_u, int split,
+                                                     const int32_t* __restrict__ rep_graph) {
     extern __shared__ uint32_t lc_lists[];
     __shared__ uint32_t twist_buf[MT_N];
     // `split` waves share one 64-replica word column, each taking 64/split
@@ -900,6 +852,7 @@ __global__ void __launch_bounds__(64) k_sa_lightcone(const int32_t* __restrict__
     const bool live = lane < per && r < R;
     const u64 bit = 1ull << (rl & 63);
     const int64_t NS = L.ns, colo = col * L.cs;     // level word addressing (separate arrays or cone)
+    if (rep_graph && live) adj += (int64_t)rep_graph[r] * n * d;   // this replica's graph of the stack
     uint32_t* lists = lc_lists + lane;
     WaveMT g{st.mt, twist_buf, r, live ? st.mt_idx[r] : MT_N, lane};
     double a = live ? st.a[r] : 0.0, b = live ? st.b[r] : 0.0;
@@ -1075,13 +1028,53 @@ __global__ void __launch_bounds__(64) k_sa_lightcone(const int32_t* __restrict__
 // positions (flips straight from registers, no lists), and balls that are not
 // trees fall back to lc_delta_mlp (lists in LDS).  Same accept sequence.
 // ---------------------------------------------------------------------------
+// Cone-word loads of the one-trip and speculative kernels: sc1 loads (served
+// by L2, around the CU's vector L1) through a buffer descriptor over the wave's
+// word-column slab.  A lane re-reads words that its own atomicXor flips have
+// just changed; global atomics are performed in L2, and the gfx950 memory model
+// gives no rule by which a line already held in this CU's L1 would see them, so
+// plain (L1-cacheable) loads could return the lane's own bit stale.  sc1 loads
+// cost 0-3 % against plain ones at 16 B (MI355X_MICROARCH.md, visibility
+// table); the general kernels use agent-scope atomic loads (ld_word), the same
+// sc1 instruction at 8 B.  The slab base is wave-uniform (the column comes from
+// blockIdx), so the descriptor lives in SGPRs; offsets are 32-bit (the host
+// checks n*LV*8 < 2^31).
+typedef unsigned int v4u32_t __attribute__((ext_vector_type(4)));
+typedef unsigned int v2u32_t __attribute__((ext_vector_type(2)));
+constexpr int kSc1 = 16;        // buffer cache-policy bits: sc1
+
+struct ConeRd {
+    __amdgpu_buffer_rsrc_t rs;
+    // the inputs are wave-uniform; readfirstlane makes that provable, so the
+    // descriptor sits in SGPRs (no waterfall loop around each load)
+    __device__ __forceinline__ static __amdgpu_buffer_rsrc_t make(const u64* slab, int64_t bytes) {
+        const uint64_t a = (uint64_t)(uintptr_t)slab;
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+        const int nb = __builtin_amdgcn_readfirstlane((int)bytes);
+        return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), (short)0, nb,
+                                                 0x00020000);
+    }
+    __device__ __forceinline__ ConeRd(const u64* slab, int64_t bytes) : rs(make(slab, bytes)) {}
+    __device__ __forceinline__ u64 word(uint32_t idx) const {          // idx in 8-B words
+        const v2u32_t x = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(idx * 8u), 0, kSc1);
+        return (u64)x.x | ((u64)x.y << 32);
+    }
+    __device__ __forceinline__ void pair(uint32_t idx, u64& a, u64& b) const {   // 16-B aligned pair
+        const v4u32_t x = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(idx * 8u), 0, kSc1);
+        a = (u64)x.x | ((u64)x.y << 32);
+        b = (u64)x.z | ((u64)x.w << 32);
+    }
+};
+
 template <int D>
 __global__ void __launch_bounds__(64) k_sa_cone2(const int32_t* __restrict__ adj, const int4* __restrict__ adj_pad,
                                                  int64_t n, int64_t R, int64_t W,
                                                  LcLevels L, mjx_sa_state st, int64_t nsteps, double par_a,
                                                  double par_b, double a_cap, double b_cap, int64_t t_cap,
                                                  const int32_t* __restrict__ tape_i,
-                                                 const double* __restrict__ tape_u, int split) {
+                                                 const double* __restrict__ tape_u, int split,
+                                                 const int32_t* __restrict__ rep_graph) {
     extern __shared__ uint32_t lc_lists[];
     constexpr int T = 2;
     const int lane = threadIdx.x;
@@ -1100,6 +1093,11 @@ __global__ void __launch_bounds__(64) k_sa_cone2(const int32_t* __restrict__ adj
     int ties = 0;
     const bool run = live && done == 0;
     static_assert(D == 3, "rows are read as one 16-B load from the padded adjacency");
+    if (rep_graph && live) {                                  // this replica's graph of the stack
+        const int64_t g = rep_graph[r];
+        adj += g * n * D;
+        adj_pad += g * n;
+    }
     auto row = [&](int32_t v, int32_t (&o)[D]) {
         const int4 q = adj_pad[(uint32_t)v < (uint32_t)n ? v : 0];             // never out of bounds
         o[0] = q.x; o[1] = q.y; o[2] = q.z;
@@ -1121,15 +1119,14 @@ __global__ void __launch_bounds__(64) k_sa_cone2(const int32_t* __restrict__ adj
     for (int m = 0; m < D; ++m)
 #pragma unroll
         for (int x = 0; x < D; ++x) row(A1[m][x], C[m][x]);
-    // plain (cacheable) loads: a lane's own bit of a word changes only by its
-    // own atomics, which a later load of the same lane sees (the bit-exact
-    // tests re-read just-flipped words constantly); other lanes' bits may be
-    // stale and are never used
-    auto w = [&](int32_t v, int lv) { return cone[(int64_t)v * NS + colo + lv]; };
+    // sc1 loads (ConeRd): a lane's own bit of a word changes only by its own
+    // atomics; other lanes' bits may be stale and are never used
+    const ConeRd crd(cone + colo, n * NS * 8);
+    auto w = [&](int32_t v, int lv) { return crd.word((uint32_t)v * (uint32_t)NS + (uint32_t)lv); };
     auto sector = [&](int32_t v, u64 (&o)[3]) {
-        const u64* p = cone + (int64_t)v * NS + colo;
-        const ulonglong2 q = *reinterpret_cast<const ulonglong2*>(p);
-        o[0] = q.x; o[1] = q.y; o[2] = p[2];
+        const uint32_t q = (uint32_t)v * (uint32_t)NS;
+        crd.pair(q, o[0], o[1]);
+        o[2] = crd.word(q + 2);
     };
     auto bv = [&](u64 x) -> uint32_t { return (x & bit) ? 1u : 0u; };
     auto maj = [&](int ones, uint32_t own) -> uint32_t { return (2 * ones > D) ? 1u : ((2 * ones < D) ? 0u : own); };
@@ -1365,7 +1362,8 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
                                                 int64_t n, int64_t R, int64_t W, LcLevels L, mjx_sa_state st,
                                                 int64_t nsteps, double par_a, double par_b, double a_cap,
                                                 double b_cap, int64_t t_cap, const int32_t* __restrict__ tape_i,
-                                                const double* __restrict__ tape_u, int hoff) {
+                                                const double* __restrict__ tape_u, int hoff,
+                                                const int32_t* __restrict__ rep_graph) {
     // rows as one 16-B load: the padded adjacency (d = 3) or the adjacency itself (d = 4)
     static_assert((D == 3 && (TT == 1 || TT == 2)) || (D == 4 && TT == 1), "speculative batches: d=3 T<=2, d=4 T=1");
     extern __shared__ uint32_t lc_lists[];
@@ -1386,6 +1384,11 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
     const u64* cone = L.s[0];
     uint32_t* lists = lc_lists + lane;
     uint32_t* htab = lc_lists + hoff + g * SPEC_HS;
+    if (rep_graph && live) {                                  // this replica's graph of the stack
+        const int64_t gi = rep_graph[r];
+        adj += gi * n * D;
+        adj_pad += gi * n;
+    }
     // replica state, identical in the group's 8 lanes
     double a = live ? st.a[r] : 0.0, b = live ? st.b[r] : 0.0;
     int64_t t = live ? st.t[r] : 0, sum_end = live ? st.sum_end[r] : 0;
@@ -1397,12 +1400,13 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
         o[0] = q.x; o[1] = q.y; o[2] = q.z;
         if constexpr (D == 4) o[3] = q.w;
     };
-    // plain loads: see k_sa_cone2
-    auto w = [&](int32_t v, int lv) { return cone[(int64_t)v * NS + colo + lv]; };
+    // sc1 loads: see ConeRd
+    const ConeRd crd(cone + colo, n * NS * 8);
+    auto w = [&](int32_t v, int lv) { return crd.word((uint32_t)v * (uint32_t)NS + (uint32_t)lv); };
     auto sector = [&](int32_t v, u64 (&o)[3]) {      // levels 0..T of v
-        const u64* p = cone + (int64_t)v * NS + colo;
-        const ulonglong2 q = *reinterpret_cast<const ulonglong2*>(p);
-        o[0] = q.x; o[1] = q.y; o[2] = (TT == 2) ? p[2] : 0ull;
+        const uint32_t q = (uint32_t)v * (uint32_t)NS;
+        crd.pair(q, o[0], o[1]);
+        o[2] = (TT == 2) ? crd.word(q + 2) : 0ull;
     };
     auto bv = [&](u64 x) -> uint32_t { return (x & bit) ? 1u : 0u; };
     auto maj = [&](int ones, uint32_t own) -> uint32_t { return (2 * ones > D) ? 1u : ((2 * ones < D) ? 0u : own); };
@@ -1429,9 +1433,12 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
     for (;;) {
         const bool going = live && done == 0 && pos < nsteps;
         if (!__any(going)) break;
-        // empty hash sets (16 KB per wave, 16-B stores)
+        // empty hash sets (16 KB per wave, 16-B stores); lanes then insert into
+        // and read slots other lanes wrote: wave-scope fences at each hand-off
         for (int q = lane; q < (64 / K) * SPEC_HS / 4; q += 64)
             reinterpret_cast<uint4*>(lc_lists + hoff)[q] = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
         const int64_t kk = pos + k;
         const bool mine = going && kk < nsteps;
         int32_t i = 0;
@@ -1589,6 +1596,8 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
                 }
             }
         }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
         // does an earlier proposal of the batch write a node this one read?
         bool stands = mine && (ok || listpath);
         if (stands && k > 0) {
@@ -1682,8 +1691,10 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
             (void)__shfl(sum_after, lane, 64);                // keep the shuffles wave-uniform
             (void)__shfl(dn, lane, 64);
         }
-        // flips land before the next batch reads
+        // flips land before the next batch reads; the hash reads end before the next clear
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
     }
     // steps of this launch after the replica finished
     if (live && (st.tr_i || st.tr_acc || st.tr_sum || st.tr_dE)) {
@@ -1750,7 +1761,8 @@ static int sa_init_finish(const int32_t* adj, int64_t n, int d, int T, int64_t R
                           uint64_t* s, uint64_t* tmp1, uint64_t* tmp2, const mjx_sa_state& st, void* stream) {
     hipStream_t hs = as_stream(stream);
     MJX_HIP(hipMemsetAsync(st.cnt, 0, (size_t)R * sizeof(unsigned long long), hs), "sa_init memset");
-    int rc = mjx_rollout_ell_rp(adj, n, d, W, s, tmp1, tmp2, T, st.cnt, stream);
+    int rc = st.rep_graph ? mjx_rollout_ell_rp_multi(adj, n, d, R, st.rep_graph, s, tmp1, tmp2, T, st.cnt, stream)
+                          : mjx_rollout_ell_rp(adj, n, d, W, s, tmp1, tmp2, T, st.cnt, stream);
     if (rc) return rc;
     k_sa_init_state<<<(unsigned)((R + 255) / 256), 256, 0, hs>>>(n, R, a0, b0, st.cnt, st);
     MJX_LAUNCH_CHECK("k_sa_init_state");
@@ -1830,7 +1842,8 @@ extern "C" int mjx_sa_steps(const int32_t* adj, int64_t n, int d, int p, int c, 
         k_sa_propose<<<gridR, kBlock, 0, hs>>>(n, R, W, (u64*)s, st, k);
         MJX_LAUNCH_CHECK("k_sa_propose");
         MJX_HIP(hipMemsetAsync(st.cnt, 0, (size_t)R * sizeof(unsigned long long), hs), "sa_steps memset");
-        int rc = mjx_rollout_ell_rp(adj, n, d, W, s, tmp1, tmp2, T, st.cnt, stream);
+        int rc = st.rep_graph ? mjx_rollout_ell_rp_multi(adj, n, d, R, st.rep_graph, s, tmp1, tmp2, T, st.cnt, stream)
+                              : mjx_rollout_ell_rp(adj, n, d, W, s, tmp1, tmp2, T, st.cnt, stream);
         if (rc) return rc;
         k_sa_accept<<<gridR, kBlock, 0, hs>>>(n, R, W, (u64*)s, st, k, par_a, par_b, a_cap, b_cap, t_cap);
         MJX_LAUNCH_CHECK("k_sa_accept");
@@ -1853,14 +1866,16 @@ extern "C" int64_t mjx_sa_lightcone_lds(int d, int p, int c) {
 }
 
 extern "C" int mjx_sa_lightcone_prepare(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R,
-                                        const uint64_t* s, uint64_t* const* levels, void* stream) {
+                                        const int32_t* rep_graph, const uint64_t* s, uint64_t* const* levels,
+                                        void* stream) {
     const int T = p + c - 1;
     if (!adj || !s || !levels || n < 2 || R < 1 || d < 1 || T < 1 || T > LC_MAXT) return MJX_EINVAL;
     const int64_t W = (R + 63) / 64;
     const uint64_t* src = s;
     for (int t = 0; t < T; ++t) {
         if (!levels[t]) return MJX_EINVAL;
-        int rc = mjx_rollout_ell_rp(adj, n, d, W, src, levels[t], nullptr, 1, nullptr, stream);
+        int rc = rep_graph ? mjx_rollout_ell_rp_multi(adj, n, d, R, rep_graph, src, levels[t], nullptr, 1, nullptr, stream)
+                           : mjx_rollout_ell_rp(adj, n, d, W, src, levels[t], nullptr, 1, nullptr, stream);
         if (rc) return rc;
         src = levels[t];
     }
@@ -1889,26 +1904,31 @@ static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d
     hipStream_t hs = as_stream(stream);
     const mjx_sa_state st = *stp;
     const bool tape = st.tape_i && st.tape_u && st.tape_cap > 0;
-    int split = lc_split(W, lds);
-    if (const char* e = getenv("MJX_LC_SPLIT")) split = atoi(e);   // tuning experiment
+    const int split = st.opt_split ? st.opt_split : lc_split(W, lds);
     if (split < 1 || split > 64 || (64 % split)) return MJX_EINVAL;
+    if (st.opt_spec_k != 0 && st.opt_spec_k != 8 && st.opt_spec_k != 16) return MJX_EINVAL;
+    if (st.opt_flags & ~(MJX_SA_NO_SPEC | MJX_SA_NO_CONE2)) return MJX_EINVAL;
+    // the one-trip and speculative kernels address a word column's cone slab
+    // with 32-bit byte offsets (ConeRd)
+    const bool slab32 = L.s0c && n * L.ns * 8 < (int64_t(1) << 31);
     // one launch per tape chunk (the tape kernel fills the chunk's (i, u) first)
     auto launch = [&](auto kern, mjx_sa_state s2, int64_t k) -> int {
         MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
                 "lightcone lds");
         kern<<<(unsigned)(W * split), 64, lds, hs>>>(adj, d, n, R, W, L, T, s2, k, par_a, par_b, a_cap, b_cap,
-                                                     t_cap, st.tape_i, st.tape_u, split);
+                                                     t_cap, st.tape_i, st.tape_u, split, st.rep_graph);
         MJX_LAUNCH_CHECK("k_sa_lightcone");
         return MJX_OK;
     };
     // cone layout, p+c-1 = 2, d = 3 with the tape: the one-round-trip kernel
-    const bool one_trip = tape && L.s0c && adj_pad && T == 2 && d == 3 && L.tab >= 0 && !getenv("MJX_NO_CONE2");
+    const bool one_trip = tape && slab32 && adj_pad && T == 2 && d == 3 && L.tab >= 0 &&
+                          !(st.opt_flags & MJX_SA_NO_CONE2);
     auto launch_one_trip = [&](mjx_sa_state s2, int64_t k) -> int {
         auto kern = k_sa_cone2<3>;
         MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
                 "cone2 lds");
         kern<<<(unsigned)(W * split), 64, lds, hs>>>(adj, (const int4*)adj_pad, n, R, W, L, s2, k, par_a, par_b,
-                                                     a_cap, b_cap, t_cap, st.tape_i, st.tape_u, split);
+                                                     a_cap, b_cap, t_cap, st.tape_i, st.tape_u, split, st.rep_graph);
         MJX_LAUNCH_CHECK("k_sa_cone2");
         return MJX_OK;
     };
@@ -1916,10 +1936,9 @@ static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d
     const int4* rows4 = (d == 4) ? (const int4*)adj : (const int4*)adj_pad;   // 16-B rows
     // 8 proposals per batch; 16 when 8 would leave CUs without a wave (few word columns):
     // configs[1] at R = 1024 3.05 -> 1.78 us per step, at R = 4096 16 is slower (3.76 vs 4.10)
-    int spec_k = (W * 8 < kCUs) ? 16 : 8;
-    if (const char* e = getenv("MJX_SPEC_K")) spec_k = (atoi(e) == 16) ? 16 : 8;   // tuning override
-    const bool spec = tape && L.s0c && rows4 && L.tab >= 0 && n < (int64_t(1) << (spec_k == 16 ? 27 : 28)) &&
-                      !getenv("MJX_NO_SPEC") && ((d == 3 && (T == 1 || T == 2)) || (d == 4 && T == 1));
+    const int spec_k = st.opt_spec_k ? st.opt_spec_k : ((W * 8 < kCUs) ? 16 : 8);
+    const bool spec = tape && slab32 && rows4 && L.tab >= 0 && n < (int64_t(1) << (spec_k == 16 ? 27 : 28)) &&
+                      !(st.opt_flags & MJX_SA_NO_SPEC) && ((d == 3 && (T == 1 || T == 2)) || (d == 4 && T == 1));
     const int hoff = slots * 64;
     const size_t lds_spec = lds + SPEC_LDS;
     auto launch_spec = [&](mjx_sa_state s2, int64_t k) -> int {
@@ -1928,7 +1947,7 @@ static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d
                                         (int)lds_spec), "spec lds");
             kern<<<(unsigned)(W * K), 64, lds_spec, hs>>>(adj, rows4, n, R, W, L, s2, k, par_a, par_b,
                                                                       a_cap, b_cap, t_cap, st.tape_i, st.tape_u,
-                                                                      hoff);
+                                                                      hoff, st.rep_graph);
             MJX_LAUNCH_CHECK("k_sa_spec");
             return MJX_OK;
         };

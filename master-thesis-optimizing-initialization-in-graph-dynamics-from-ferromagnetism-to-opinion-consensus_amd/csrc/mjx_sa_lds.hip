@@ -1,0 +1,379 @@
+// LDS-resident light-cone SA for the reference's own graph sizes
+// (code/SA_RRG.py:44-52: n = 1e4, d = 4; configs[0]).
+//
+// A workgroup (one wave) owns one replica for a whole launch: its graph's
+// adjacency as uint16 rows, the cached rollout levels s_t = onestep^t(s),
+// t = 0..T (T = p+c-1), as bit arrays, and its MT19937 state all live in LDS
+// (n = 1e4, d = 4, T = 3: 94 KB), so a proposal's light-cone evaluation makes
+// LDS round trips only.  The HBM/L2-resident kernels (mjx_sa.hip) pay one
+// memory round trip per dependent load -- about 90 us per step at p = 3 --
+// which is what makes SA_RRG.py's run to consensus (1e5-1e8+ proposals per
+// replica) slow there.
+//
+// Per step (code/SA_RRG.py:73-85), wave-uniform:
+//   * i = randint(0, n), u = rand() from the replica's numpy stream (legacy
+//     MT19937: masked rejection over tempered words, 53-bit doubles); the words
+//     of one randint are tested 64 at a time with one ballot, the state is
+//     twisted in LDS exactly when numpy would twist it, so the stream position
+//     after the launch is numpy's (no draw-ahead);
+//   * the change sets C_t of the levels (C_0 = {i flipped}): candidates of
+//     level t are C_{t-1} and its neighbours, one lane each; a candidate's
+//     level-(t-1) inputs come from C_{t-1} (an LDS hash of node -> new value)
+//     or from the cached bit; it joins C_t when the always-stay majority
+//     (code/SA_RRG.py:19-20) differs from its cached level-t bit (inserted
+//     once: the hash dedups);
+//   * sum(s_end(flipped)) - sum(s_end) = sum over C_T of +-2; delta_H in float64
+//     in the reference's operation order (this unit is built with
+//     -ffp-contract=off), Metropolis test, schedule, stop tests;
+//   * an accepted proposal XORs its change sets into the level bit arrays.
+// At the end of the launch the changed level-0 bits go back to the
+// replica-packed configuration s (atomicXor of the replica's bit: the other
+// 63 replicas of a word are other workgroups) and the MT state, a, b, t,
+// sum_end, done back to the state arrays.  Same proposals, accepts and outputs
+// as every other SA mode.
+#include "mjx_common.h"
+#include "mjx_mt.h"
+#include <math.h>
+
+#pragma clang fp contract(off)
+
+namespace mjx {
+namespace salds {
+
+constexpr int kMaxT = 6;
+constexpr size_t kLdsMax = 160 * 1024;
+
+struct Geo {
+    int rw;          // uint16 entries per adjacency row (4, 8 or 16)
+    int nw;          // uint32 words per level bit array (even)
+    int lc;          // change-list capacity per level (>= the radius-T ball)
+    int hs;          // hash slots per level (power of 2, >= 2 lc)
+    int hshift;      // 32 - log2(hs)
+    int off_lev;     // byte offsets into the dynamic LDS
+    int off_lev0;
+    int off_mt;
+    int off_hash;
+    int off_list;
+    int off_cnt;
+    int bytes;
+};
+
+static int64_t ball(int d, int T) {
+    int64_t b = 1, shell = 1;
+    for (int t = 1; t <= T; ++t) {
+        shell = (t == 1) ? d : shell * (d - 1);
+        b += shell;
+        if (b > (1 << 20)) return b;
+    }
+    return b;
+}
+
+static bool geometry(int64_t n, int d, int T, Geo* g) {
+    if (n < 2 || n > 65535 || d < 1 || d > 16 || T < 1 || T > kMaxT) return false;
+    g->rw = (d <= 4) ? 4 : (d <= 8) ? 8 : 16;
+    g->nw = (int)(((n + 63) / 64) * 2);
+    int64_t lc = ball(d, T);
+    if (lc > n) lc = n;
+    lc = ((lc + 63) / 64) * 64;
+    if (lc > 4096) return false;
+    g->lc = (int)lc;
+    int hs = 64, lg = 6;
+    while (hs < 2 * lc) { hs *= 2; ++lg; }
+    g->hs = hs;
+    g->hshift = 32 - lg;
+    int64_t off = ((int64_t)n * g->rw * 2 + 15) / 16 * 16;
+    g->off_lev = (int)off;   off += (int64_t)(T + 1) * g->nw * 4;
+    g->off_lev0 = (int)off;  off += (int64_t)g->nw * 4;
+    g->off_mt = (int)off;    off += MT_N * 4;
+    g->off_hash = (int)off;  off += (int64_t)(T + 1) * hs * 4;
+    g->off_list = (int)off;  off += (int64_t)(T + 1) * lc * 4;
+    g->off_cnt = (int)off;   off += 16 * 4;
+    g->bytes = (int)off;
+    return (size_t)off <= kLdsMax;
+}
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ int64_t wave_sum(int64_t x) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
+    return x;
+}
+
+template <int D>
+__global__ void __launch_bounds__(64) k_sa_lds(const int32_t* __restrict__ adj, int dd, int64_t n, int T, int64_t R,
+                                               int64_t W, u64* __restrict__ s, mjx_sa_state st, int64_t nsteps,
+                                               double par_a, double par_b, double a_cap, double b_cap, int64_t t_cap,
+                                               Geo geo) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int d = (D > 0) ? D : dd;
+    const int lane = threadIdx.x;
+    const int64_t r = blockIdx.x;
+    const int64_t col = r >> 6;
+    const u64 rbit = 1ull << (r & 63);
+    const int nw = geo.nw, rw = geo.rw, hs = geo.hs, lc = geo.lc;
+    uint16_t* rows = reinterpret_cast<uint16_t*>(smem);
+    uint32_t* lev = reinterpret_cast<uint32_t*>(smem + geo.off_lev);      // level t at lev + t*nw
+    uint32_t* lev0s = reinterpret_cast<uint32_t*>(smem + geo.off_lev0);   // level 0 at launch start
+    uint32_t* mt = reinterpret_cast<uint32_t*>(smem + geo.off_mt);
+    uint32_t* hsh = reinterpret_cast<uint32_t*>(smem + geo.off_hash);     // level t at hsh + t*hs
+    uint32_t* lst = reinterpret_cast<uint32_t*>(smem + geo.off_list);     // level t at lst + t*lc
+    int* cnts = reinterpret_cast<int*>(smem + geo.off_cnt);
+    const int32_t* g = adj + (st.rep_graph ? (int64_t)st.rep_graph[r] : 0) * n * d;
+
+    // ---- launch setup: rows, level 0, MT state; then levels 1..T by sweeps in LDS
+    for (int64_t q = lane; q < n * d; q += 64) {
+        const int64_t v = q / d;
+        rows[v * rw + (q - v * d)] = (uint16_t)g[q];
+    }
+    for (int64_t v0 = 0; v0 < (int64_t)nw * 32; v0 += 64) {
+        const int64_t v = v0 + lane;
+        const bool b = v < n && (s[v * W + col] & rbit);
+        const u64 m = __ballot(b);
+        if (lane < 2) {
+            const uint32_t x = (uint32_t)(m >> (32 * lane));
+            lev[(v0 >> 5) + lane] = x;
+            lev0s[(v0 >> 5) + lane] = x;
+        }
+    }
+    for (int k = lane; k < MT_N; k += 64) mt[k] = st.mt[r * MT_N + k];
+    for (int k = lane; k < (T + 1) * hs; k += 64) hsh[k] = 0u;
+    wave_sync();
+    auto bitof = [&](const uint32_t* L, int v) -> uint32_t { return (L[v >> 5] >> (v & 31)) & 1u; };
+    auto maj = [&](int ones, uint32_t own) -> uint32_t {       // always-stay majority (code/SA_RRG.py:19-20)
+        return (2 * ones > d) ? 1u : ((2 * ones < d) ? 0u : own);
+    };
+    for (int t = 1; t <= T; ++t) {
+        const uint32_t* lp = lev + (t - 1) * nw;
+        uint32_t* lt = lev + t * nw;
+        for (int64_t v0 = 0; v0 < (int64_t)nw * 32; v0 += 64) {
+            const int v = (int)(v0 + lane);
+            uint32_t nb = 0;
+            if (v < n) {
+                int ones = 0;
+                for (int q = 0; q < d; ++q) ones += (int)bitof(lp, rows[v * rw + q]);
+                nb = maj(ones, bitof(lp, v));
+            }
+            const u64 m = __ballot(nb != 0);
+            if (lane < 2) lt[(v0 >> 5) + lane] = (uint32_t)(m >> (32 * lane));
+        }
+        wave_sync();
+    }
+
+    // ---- the steps
+    double a = st.a[r], b = st.b[r];
+    int64_t t = st.t[r], sum_end = st.sum_end[r];
+    int done = st.done[r];
+    int idx = st.mt_idx[r];
+    int ties = 0;
+    const uint32_t rng = (uint32_t)(n - 1);
+    uint32_t mask = rng;
+    mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+    auto hslot = [&](int v) -> uint32_t { return ((uint32_t)(v + 1) * 0x9E3779B1u) >> geo.hshift; };
+    // value of node v at level l as the proposal sees it: C_l's new value, else the cached bit
+    auto val_at = [&](int l, int v) -> uint32_t {
+        const uint32_t* H = hsh + l * hs;
+        uint32_t h = hslot(v);
+        for (;;) {
+            const uint32_t e = H[h];
+            if (e == 0u) return bitof(lev + l * nw, v);
+            if ((e >> 1) == (uint32_t)(v + 1)) return e & 1u;
+            h = (h + 1) & (uint32_t)(hs - 1);
+        }
+    };
+    auto hins = [&](int l, int v, uint32_t val) -> bool {     // true: first insert of v at level l
+        uint32_t* H = hsh + l * hs;
+        const uint32_t key = ((uint32_t)(v + 1) << 1) | val;
+        uint32_t h = hslot(v);
+        for (;;) {
+            const uint32_t old = atomicCAS(&H[h], 0u, key);
+            if (old == 0u) return true;
+            if ((old >> 1) == (uint32_t)(v + 1)) return false;
+            h = (h + 1) & (uint32_t)(hs - 1);
+        }
+    };
+    auto next_word = [&]() -> uint32_t {                          // wave-uniform
+        if (idx >= MT_N) {
+            lds_twist(mt, lane);
+            idx = 0;
+        }
+        return mt_temper(mt[idx++]);
+    };
+    int64_t k = 0;
+    for (; k < nsteps && done == 0; ++k) {
+        // randint(low=0, high=n) (code/SA_RRG.py:73): numpy's masked rejection, 64 words per ballot
+        int iv = -1;
+        while (iv < 0) {
+            if (idx >= MT_N) {
+                lds_twist(mt, lane);
+                idx = 0;
+            }
+            const int q = idx + lane;
+            uint32_t y = 0;
+            bool ok = false;
+            if (q < MT_N) {
+                y = mt_temper(mt[q]) & mask;
+                ok = y <= rng;
+            }
+            const u64 bal = __ballot(ok);
+            if (bal) {
+                const int f = __ffsll((unsigned long long)bal) - 1;
+                iv = __shfl((int)y, f, 64);
+                idx += f + 1;
+            } else {
+                idx += (MT_N - idx < 64) ? MT_N - idx : 64;
+            }
+        }
+        // rand() (code/SA_RRG.py:76)
+        const uint32_t w1 = next_word();
+        const uint32_t w2 = next_word();
+        const double u = mt_double(w1, w2);
+        // level 0: i flipped
+        const uint32_t old_i = bitof(lev, iv);
+        if (lane == 0) {
+            hsh[hslot(iv)] = ((uint32_t)(iv + 1) << 1) | (old_i ^ 1u);     // empty table: the home slot
+            lst[0] = (uint32_t)iv | ((old_i ^ 1u) << 31);
+            cnts[0] = 1;
+        }
+        wave_sync();
+        int last = 0;                          // deepest level with a change
+        for (int l = 1; l <= T; ++l) {
+            const uint32_t* prev = lst + (l - 1) * lc;
+            uint32_t* cur = lst + l * lc;
+            const int np = cnts[l - 1];
+            const int m = np * (d + 1);
+            int nc = 0;
+            for (int base = 0; base < m; base += 64) {
+                const int q = base + lane;
+                bool add = false;
+                int cand = 0;
+                uint32_t nb = 0;
+                if (q < m) {
+                    const int slot = q / (d + 1), j = q - slot * (d + 1);
+                    const int v = (int)(prev[slot] & 0x7fffffffu);
+                    cand = (j == 0) ? v : (int)rows[v * rw + j - 1];
+                    int ones = 0;
+                    for (int e = 0; e < d; ++e) ones += (int)val_at(l - 1, rows[cand * rw + e]);
+                    nb = maj(ones, val_at(l - 1, cand));
+                    if (nb != bitof(lev + l * nw, cand)) add = hins(l, cand, nb);
+                }
+                const u64 bal = __ballot(add);
+                if (add) cur[nc + __popcll(bal & ((1ull << lane) - 1ull))] = (uint32_t)cand | (nb << 31);
+                nc += __popcll(bal);
+            }
+            if (lane == 0) cnts[l] = nc;
+            wave_sync();
+            if (nc == 0) break;
+            last = l;
+        }
+        int64_t ds = 0;
+        if (last == T) {
+            const uint32_t* lt = lst + T * lc;
+            for (int q = lane; q < cnts[T]; q += 64) ds += (lt[q] >> 31) ? 2 : -2;
+            ds = wave_sum(ds);
+        }
+        const int64_t sum_new = sum_end + ds;
+        // delta_H (code/SA_RRG.py:37), same operation order, no contraction
+        const double si = old_i ? 1.0 : -1.0;
+        const double t1 = (-2.0 * a) * si;
+        const double t2 = b * (double)(sum_end - sum_new);
+        const double dE = (t1 + t2) / (double)n;
+        const double e = exp(-dE);
+        const double prob = (e < 1.0) ? e : 1.0;                    // (code/SA_RRG.py:75)
+        const bool acc = u < prob;                                  // (code/SA_RRG.py:76)
+        if (e < 1.0 && fabs(u - e) <= 4.0 * (nextafter(e, 2.0) - e)) ++ties;
+        if (acc) {                                                  // (code/SA_RRG.py:77)
+            for (int l = 0; l <= last; ++l) {
+                const uint32_t* cl = lst + l * lc;
+                for (int q = lane; q < cnts[l]; q += 64) {
+                    const uint32_t v = cl[q] & 0x7fffffffu;
+                    atomicXor(&lev[l * nw + (v >> 5)], 1u << (v & 31));
+                }
+            }
+            sum_end = sum_new;
+        }
+        if (a < a_cap) a = par_a * a;                               // (code/SA_RRG.py:80-81)
+        if (b < b_cap) b = par_b * b;
+        t += 1;                                                     // (code/SA_RRG.py:82)
+        if (t > t_cap) done = 2;                                    // (code/SA_RRG.py:84)
+        else if (sum_end == n) done = 1;                            // m(s_endstate(s)) == 1
+        if (lane == 0) {
+            if (st.tr_i) st.tr_i[k * R + r] = iv;
+            if (st.tr_acc) st.tr_acc[k * R + r] = acc ? 1 : 0;
+            if (st.tr_sum) st.tr_sum[k * R + r] = sum_end;
+            if (st.tr_dE) st.tr_dE[k * R + r] = dE;
+        }
+        // empty the hash levels this step used (a level past `last` got no insert)
+        for (int l = 0; l <= last + 1 && l <= T; ++l)
+            for (int q = lane; q < hs; q += 64) hsh[l * hs + q] = 0u;
+        wave_sync();
+    }
+    // steps of this launch after the replica finished
+    if (lane == 0) {
+        for (; k < nsteps; ++k) {
+            if (st.tr_i) st.tr_i[k * R + r] = -1;
+            if (st.tr_acc) st.tr_acc[k * R + r] = -1;
+            if (st.tr_sum) st.tr_sum[k * R + r] = sum_end;
+            if (st.tr_dE) st.tr_dE[k * R + r] = 0.0;
+        }
+    }
+    // ---- write back: changed configuration bits, the stream, the replica state
+    for (int64_t v0 = 0; v0 < n; v0 += 64) {
+        const int v = (int)(v0 + lane);
+        if (v < n && (bitof(lev, v) ^ bitof(lev0s, v)))
+            atomicXor((unsigned long long*)&s[(int64_t)v * W + col], (unsigned long long)rbit);
+    }
+    for (int q = lane; q < MT_N; q += 64) st.mt[r * MT_N + q] = mt[q];
+    if (lane == 0) {
+        st.mt_idx[r] = idx;
+        st.a[r] = a;
+        st.b[r] = b;
+        st.t[r] = t;
+        st.sum_end[r] = sum_end;
+        st.done[r] = done;
+        if (st.tr_tie) st.tr_tie[r] += ties;
+    }
+}
+
+}  // namespace salds
+}  // namespace mjx
+
+using namespace mjx;
+
+extern "C" int64_t mjx_sa_lds_bytes(int64_t n, int d, int p, int c) {
+    salds::Geo g;
+    if (p < 0 || c < 0 || !salds::geometry(n, d, p + c - 1, &g)) return -1;
+    return g.bytes;
+}
+
+extern "C" int mjx_sa_lds_steps(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R, uint64_t* s,
+                                mjx_sa_state* stp, int64_t nsteps, double par_a, double par_b, double a_cap,
+                                double b_cap, int64_t t_cap, void* stream) {
+    if (!stp || !adj || !s || R < 1 || nsteps < 0 || p < 0 || c < 0) return MJX_EINVAL;
+    const int T = p + c - 1;
+    salds::Geo g;
+    if (!salds::geometry(n, d, T, &g)) return MJX_ERANGE;
+    const mjx_sa_state st = *stp;
+    if (!st.mt || !st.mt_idx || !st.a || !st.b || !st.t || !st.sum_end || !st.done) return MJX_EINVAL;
+    if (nsteps == 0) return MJX_OK;
+    if (R > INT32_MAX) return MJX_ERANGE;
+    const int64_t W = (R + 63) / 64;
+    hipStream_t hs = as_stream(stream);
+    auto go = [&](auto kern) -> int {
+        MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, g.bytes),
+                "sa_lds lds");
+        kern<<<(unsigned)R, 64, (size_t)g.bytes, hs>>>(adj, d, n, T, R, W, (u64*)s, st, nsteps, par_a, par_b, a_cap,
+                                                       b_cap, t_cap, g);
+        MJX_LAUNCH_CHECK("k_sa_lds");
+        return MJX_OK;
+    };
+    switch (d) {
+        case 3: return go(salds::k_sa_lds<3>);
+        case 4: return go(salds::k_sa_lds<4>);
+        case 6: return go(salds::k_sa_lds<6>);
+        default: return go(salds::k_sa_lds<0>);
+    }
+}

@@ -104,11 +104,15 @@ class BinnedPlan:
                       work.numel(), _device.stream_handle())
             del work
 
-    def sweep(self, s_in, s_out, counts=None):
+    APPLY_FORMS = {"auto": 0, "flat": 1, "segments": 2}
+
+    def sweep(self, s_in, s_out, counts=None, apply_form="auto"):
+        """apply_form: phase-2 kernel, "auto" (the library's choice), "flat" or "segments"."""
         _lib.call("mjx_sweep_binned", _device.ptr(self.src_lo), _device.ptr(self.src_hi), _device.ptr(self.off),
                   _device.ptr(self.index),
                   self.n, self.d, self.lo, self.hi, _device.ptr(s_in), _device.ptr(self.msg), _device.ptr(s_out),
-                  _device.ptr(counts) if counts is not None else None, _device.stream_handle())
+                  _device.ptr(counts) if counts is not None else None, self.APPLY_FORMS[apply_form],
+                  _device.stream_handle())
 
 
 class ShardedRRG:

@@ -1,8 +1,11 @@
 """Simulated annealing for strategic initialisations (code/SA_RRG.py:44-92).
 
-``SAReplicas`` runs R independent replicas of the reference's SA loop on one
-graph, all replicas bit-packed into one spin array (64 per 64-bit word).
-Replica r is bit-identical to the reference run
+``SAReplicas`` runs R independent replicas of the reference's SA loop, all
+replicas bit-packed into one spin array (64 per 64-bit word), on one graph or
+on a graph per replica (the reference draws a fresh graph for each of its
+N_stat replicas, code/SA_RRG.py:58-62: the graphs are stacked in HBM and
+replica r reads the rows of its own).  Replica r is bit-identical to the
+reference run
 
     np.random.seed(seeds[r])
     s = 2*np.random.binomial(n=1, p=0.5, size=[n]) - 1      # code/SA_RRG.py:65
@@ -43,29 +46,78 @@ def schedule_constants(n):
     return 0.015 * n, 0.01 * n, 4.5 * n, float(5 * n), 2 * n ** 3
 
 
+KERNEL_FLAGS = {"no_spec": _lib.MJX_SA_NO_SPEC, "no_cone2": _lib.MJX_SA_NO_CONE2}
+
+
+def _graph_stack(N, R, graph_of):
+    """(device int32 (G*n, d) rows, n, d, device int32 rep_graph or None) for
+    one neighbour array or a sequence of them (stacked, replica r on graph
+    graph_of[r], default r)."""
+    multi = isinstance(N, (list, tuple)) or (isinstance(N, np.ndarray) and N.ndim == 3) or \
+        (isinstance(N, torch.Tensor) and N.dim() == 3)
+    if not multi:
+        if graph_of is not None:
+            raise ValueError("graph_of needs a sequence of graphs")
+        g = as_graph(N)
+        if g.kind != "ell":
+            raise ValueError("SA runs on random regular graphs (ELL adjacency), code/SA_RRG.py:59-61")
+        return g, g.adj, g.n, g.d, None
+    gl = [x.adj if isinstance(x, Graph) else x for x in N]
+    if not gl:
+        raise ValueError("no graphs")
+    G = len(gl)
+    gof = np.arange(R) if graph_of is None else np.asarray(graph_of, dtype=np.int64).reshape(-1)
+    if gof.size != R or gof.min() < 0 or gof.max() >= G:
+        raise ValueError(f"graph_of: one graph index in [0, {G}) per replica ({R})")
+    if graph_of is None and G != R:
+        raise ValueError(f"one graph per replica: {G} graphs for {R} replicas (or pass graph_of)")
+    shapes = {tuple(x.shape) for x in gl}
+    if len(shapes) != 1 or len(next(iter(shapes))) != 2:
+        raise ValueError("every graph must be an (n, d) neighbour array of the same n and d")
+    n, d = next(iter(shapes))
+    if all(isinstance(x, torch.Tensor) and x.is_cuda for x in gl):
+        stack = torch.stack([x.to(torch.int32) for x in gl]).reshape(G * n, d).contiguous()
+    else:
+        a = np.stack([x.cpu().numpy() if isinstance(x, torch.Tensor) else np.asarray(x) for x in gl])
+        if a.size and (a.min() < 0 or a.max() >= n):
+            raise ValueError("adjacency index out of range")
+        stack = _device.to_device(np.ascontiguousarray(a.astype(np.int32).reshape(G * n, d)))
+    rep = torch.from_numpy(gof.astype(np.int32)).to(stack.device)
+    return None, stack, int(n), int(d), rep
+
+
 class SAReplicas:
-    """R bit-packed SA replicas on one random regular graph (device resident)."""
+    """R bit-packed SA replicas on one random regular graph or on a graph per
+    replica (device resident)."""
 
     def __init__(self, N, p, c, seeds, par_a=PAR_A, par_b=PAR_B, a0=None, b0=None, mode="auto", tape=1024,
-                 mt_state=None, layout="cone"):
-        """``mt_state`` = (mt uint32 (R, 624), idx int32 (R,)): continue these
-        MT19937 streams instead of seeding (``seeds`` then only fixes R); see
-        ``mt_state()`` and ``sa_run(stream="global")``.  ``layout`` (light-cone
-        mode): ``"cone"`` keeps the cached levels of one (node, word) side by
-        side (mjx_sa_cone_steps), ``"levels"`` as separate arrays
-        (mjx_sa_lightcone_steps); same results."""
-        self.graph = as_graph(N)
-        if self.graph.kind != "ell":
-            raise ValueError("SA runs on random regular graphs (ELL adjacency), code/SA_RRG.py:59-61")
-        dev = _device.require_gpu()
-        self.p, self.c = int(p), int(c)
-        self.n = n = self.graph.n
-        if n < 2:
-            raise ValueError("n must be >= 2")
+                 mt_state=None, layout="auto", graph_of=None, kernel=None):
+        """``N``: one (n, d) neighbour array (or Graph) for every replica, or a
+        sequence of them (or a (G, n, d) array): replica r runs on graph r, or
+        on graph ``graph_of[r]``.  ``mt_state`` = (mt uint32 (R, 624), idx
+        int32 (R,)): continue these MT19937 streams instead of seeding
+        (``seeds`` then only fixes R); see ``mt_state()`` and
+        ``sa_run(stream="global")``.  ``layout`` (light-cone mode): ``"lds"``
+        keeps each replica's graph, levels and stream in LDS for a whole call
+        (mjx_sa_lds_steps; n <= 65535, the reference's own sizes), ``"cone"``
+        keeps the cached levels of one (node, word) side by side in HBM
+        (mjx_sa_cone_steps), ``"levels"`` as separate arrays
+        (mjx_sa_lightcone_steps); ``"auto"``: lds where it fits, else cone;
+        same results in every layout.  ``kernel``: light-cone kernel
+        selection passed to the ABI (tests, tuning): ``split`` (waves per word
+        column), ``spec_k`` (8 or 16), ``no_spec``, ``no_cone2``; the results
+        never depend on it."""
         seeds = np.asarray(seeds, dtype=np.int64).reshape(-1)
         if seeds.size == 0 or seeds.min() < 0 or seeds.max() > 0xFFFFFFFF:
             raise ValueError("seeds must be in [0, 2**32)")  # np.random.seed's range
         self.R = R = int(seeds.size)
+        self.graph, self.adj, n, d, self.rep_graph = _graph_stack(N, R, graph_of)
+        self.d = d
+        dev = _device.require_gpu()
+        self.p, self.c = int(p), int(c)
+        self.n = n
+        if n < 2:
+            raise ValueError("n must be >= 2")
         self.W = W = _device.words_for(R)
         a0d, b0d, self.a_cap, self.b_cap, self.t_cap = schedule_constants(n)
         self.a0 = a0d if a0 is None else float(a0)
@@ -94,9 +146,20 @@ class SAReplicas:
         for f in ("mt", "mt_idx", "a", "b", "t", "sum_end", "done", "prop_i", "prop_s", "prop_u", "cnt"):
             setattr(self._state, f, getattr(self, f).data_ptr())
         self._state.tr_tie = self.ties.data_ptr()
+        self._state.rep_graph = self.rep_graph.data_ptr() if self.rep_graph is not None else None
+        kernel = dict(kernel or {})
+        self._state.opt_split = int(kernel.pop("split", 0) or 0)
+        self._state.opt_spec_k = int(kernel.pop("spec_k", 0) or 0)
+        flags = 0
+        for key, bit in KERNEL_FLAGS.items():
+            if kernel.pop(key, False):
+                flags |= bit
+        if kernel:
+            raise ValueError(f"unknown kernel options {sorted(kernel)}")
+        self._state.opt_flags = flags
         T = self.p + self.c - 1
         if mt_state is None:
-            _lib.call("mjx_sa_init", _device.ptr(self.graph.adj), n, self.graph.d, self.p, self.c, R,
+            _lib.call("mjx_sa_init", _device.ptr(self.adj), n, self.d, self.p, self.c, R,
                       _device.ptr(self.seeds), self.a0, self.b0, _device.ptr(self.s), _device.ptr(self.tmp1),
                       _device.ptr(self.tmp2) if T >= 2 else None, _lib.ctypes.byref(self._state),
                       _device.stream_handle())
@@ -107,40 +170,51 @@ class SAReplicas:
                 raise ValueError("MT19937 word index must be in [0, 624]")
             mt_d = torch.from_numpy(mt_in.view(np.int32)).to(dev)
             idx_d = torch.from_numpy(idx_in).to(dev)
-            _lib.call("mjx_sa_init_mt", _device.ptr(self.graph.adj), n, self.graph.d, self.p, self.c, R,
+            _lib.call("mjx_sa_init_mt", _device.ptr(self.adj), n, self.d, self.p, self.c, R,
                       _device.ptr(mt_d), _device.ptr(idx_d), self.a0, self.b0, _device.ptr(self.s),
                       _device.ptr(self.tmp1), _device.ptr(self.tmp2) if T >= 2 else None,
                       _lib.ctypes.byref(self._state), _device.stream_handle())
             torch.cuda.current_stream().synchronize()       # mt_d / idx_d are freed on return
-        lds = _lib.load().mjx_sa_lightcone_lds(self.graph.d, self.p, self.c)
+        lds = _lib.load().mjx_sa_lightcone_lds(self.d, self.p, self.c)
         fits = T >= 1 and 0 < lds <= 150 * 1024
         if mode == "auto":
             mode = "lightcone" if fits else "rollout"
         if mode == "lightcone" and not fits:
-            raise ValueError(f"light-cone SA unsupported for d={self.graph.d}, p+c-1={T}")
+            raise ValueError(f"light-cone SA unsupported for d={self.d}, p+c-1={T}")
         if mode not in ("lightcone", "rollout"):
             raise ValueError(f"unknown SA mode {mode!r}")
         self.mode = mode
-        if layout not in ("cone", "levels"):
+        if layout not in ("auto", "lds", "cone", "levels"):
             raise ValueError(f"unknown light-cone layout {layout!r}")
+        lds_fits = 0 < _lib.load().mjx_sa_lds_bytes(n, self.d, self.p, self.c) <= 160 * 1024
+        if layout == "auto":
+            layout = "lds" if lds_fits else "cone"
+        if mode == "lightcone" and layout == "lds" and not lds_fits:
+            raise ValueError(f"LDS-resident SA unsupported for n={n}, d={self.d}, p+c-1={T}")
         self.layout = layout if mode == "lightcone" else None
         self.cone = None
         self.adj_pad = None
-        if mode == "lightcone":
+        self._levels = None
+        if mode == "lightcone" and layout == "lds":
+            self.tape_cap = 0                    # the LDS kernel draws in the step, exactly
+        elif mode == "lightcone":
             # levels s_1..s_T = onestep^t(s); the rollout ping-pong buffers are reused
             self._levels = [self.tmp1, self.tmp2][:T] + [torch.empty_like(self.s) for _ in range(T - 2)]
             self._lvl = (_lib.ctypes.c_void_p * T)(*[t.data_ptr() for t in self._levels])
-            _lib.call("mjx_sa_lightcone_prepare", _device.ptr(self.graph.adj), n, self.graph.d, self.p, self.c, R,
+            _lib.call("mjx_sa_lightcone_prepare", _device.ptr(self.adj), n, self.d, self.p, self.c, R,
+                      _device.ptr(self.rep_graph) if self.rep_graph is not None else None,
                       _device.ptr(self.s), self._lvl, _device.stream_handle())
             if layout == "cone":
                 lv = _lib.load().mjx_sa_cone_words(self.p, self.c)
                 self.cone = torch.empty(n * W * lv, dtype=i64, device=dev)
                 _lib.call("mjx_sa_cone_pack", n, self.p, self.c, R, _device.ptr(self.s), self._lvl,
                           _device.ptr(self.cone), _device.stream_handle())
-                if self.graph.d == 3:
+                if self.d == 3:
                     # rows padded to 16 B: one load per row in the one-round-trip step
-                    self.adj_pad = torch.zeros((n, 4), dtype=torch.int32, device=dev)
-                    self.adj_pad[:, :3] = self.graph.adj.view(n, 3)
+                    # (graph g of a stack at rows g*n .. g*n + n - 1)
+                    rows = self.adj.numel() // 3
+                    self.adj_pad = torch.zeros((rows, 4), dtype=torch.int32, device=dev)
+                    self.adj_pad[:, :3] = self.adj.view(rows, 3)
             # proposal tape: (i, u) of `tape` steps per replica drawn ahead by
             # a wave per replica (0 = draw inside the step kernel)
             self.tape_cap = int(tape) if tape else 0
@@ -171,17 +245,21 @@ class SAReplicas:
         else:
             st.tr_i = st.tr_acc = st.tr_sum = st.tr_dE = None
         T = self.p + self.c - 1
-        if self.mode == "lightcone" and self.cone is not None:
-            _lib.call("mjx_sa_cone_steps", _device.ptr(self.graph.adj),
-                      _device.ptr(self.adj_pad) if self.adj_pad is not None else None, self.n, self.graph.d, self.p, self.c,
+        if self.layout == "lds":
+            _lib.call("mjx_sa_lds_steps", _device.ptr(self.adj), self.n, self.d, self.p, self.c, self.R,
+                      _device.ptr(self.s), _lib.ctypes.byref(st), k, self.par_a, self.par_b, self.a_cap, self.b_cap,
+                      int(self.t_cap), _device.stream_handle())
+        elif self.mode == "lightcone" and self.cone is not None:
+            _lib.call("mjx_sa_cone_steps", _device.ptr(self.adj),
+                      _device.ptr(self.adj_pad) if self.adj_pad is not None else None, self.n, self.d, self.p, self.c,
                       self.R, _device.ptr(self.s), _device.ptr(self.cone), _lib.ctypes.byref(st), k, self.par_a,
                       self.par_b, self.a_cap, self.b_cap, int(self.t_cap), _device.stream_handle())
         elif self.mode == "lightcone":
-            _lib.call("mjx_sa_lightcone_steps", _device.ptr(self.graph.adj), self.n, self.graph.d, self.p, self.c,
+            _lib.call("mjx_sa_lightcone_steps", _device.ptr(self.adj), self.n, self.d, self.p, self.c,
                       self.R, _device.ptr(self.s), self._lvl, _lib.ctypes.byref(st), k, self.par_a, self.par_b,
                       self.a_cap, self.b_cap, int(self.t_cap), _device.stream_handle())
         else:
-            _lib.call("mjx_sa_steps", _device.ptr(self.graph.adj), self.n, self.graph.d, self.p, self.c, self.R,
+            _lib.call("mjx_sa_steps", _device.ptr(self.adj), self.n, self.d, self.p, self.c, self.R,
                       _device.ptr(self.s), _device.ptr(self.tmp1), _device.ptr(self.tmp2) if T >= 2 else None,
                       _lib.ctypes.byref(st), k, self.par_a, self.par_b, self.a_cap, self.b_cap,
                       int(self.t_cap), _device.stream_handle())
@@ -194,6 +272,15 @@ class SAReplicas:
         (unpacked from the cone layout when that is in use)."""
         if self.mode != "lightcone":
             raise AttributeError("levels exist in the light-cone mode only")
+        if self.layout == "lds":
+            # kept in LDS during a call only: rebuilt here from s, as every call does
+            T = self.p + self.c - 1
+            self._levels = [torch.empty_like(self.s) for _ in range(T)]
+            lvl = (_lib.ctypes.c_void_p * T)(*[t.data_ptr() for t in self._levels])
+            _lib.call("mjx_sa_lightcone_prepare", _device.ptr(self.adj), self.n, self.d, self.p, self.c, self.R,
+                      _device.ptr(self.rep_graph) if self.rep_graph is not None else None,
+                      _device.ptr(self.s), lvl, _device.stream_handle())
+            return self._levels
         self._unpack_cone()
         return self._levels
 
@@ -225,9 +312,11 @@ class SAReplicas:
         mt = self.mt.cpu().numpy().view(np.uint32).reshape(self.R, 624).copy()
         return mt, self.mt_idx.cpu().numpy().copy()
 
-    def run(self, max_steps=None, chunk=256):
+    def run(self, max_steps=None, chunk=256, max_chunk=16384):
         """Step until every replica has reached consensus or the t cap
-        (``while(m_final<1)``, code/SA_RRG.py:72), or ``max_steps``."""
+        (``while(m_final<1)``, code/SA_RRG.py:72), or ``max_steps``.  The
+        done flags are read once per chunk; chunks grow from ``chunk`` to
+        ``max_chunk`` steps (a finished replica skips the rest of a chunk)."""
         taken = 0
         while not self.all_done():
             k = chunk if max_steps is None else min(chunk, max_steps - taken)
@@ -235,6 +324,7 @@ class SAReplicas:
                 break
             self.steps(k)
             taken += k
+            chunk = min(2 * chunk, max_chunk)
         return taken
 
     # -- results (code/SA_RRG.py:86-88) ---------------------------------------
@@ -317,7 +407,8 @@ def sa_run(d, n, p, c, par_a=PAR_A, par_b=PAR_B, N_stat=5, seed=0, seeds=None, N
         other (mjx_sa_init_mt hands the stream over); bit-identical to the
         script with the same graphs.
       * ``stream="independent"`` — replica k owns ``np.random.seed(seeds[k])``
-        (default seed + k); replicas sharing a graph run together, bit-packed.
+        (default seed + k); all N_stat replicas run together, bit-packed, each
+        on its own graph (graphs stacked in HBM, SAReplicas(graph_of=...)).
     """
     gl = _graph_list(d, n, N_stat, N, graphs, graph_seed)
     R = len(gl)
@@ -329,10 +420,12 @@ def sa_run(d, n, p, c, par_a=PAR_A, par_b=PAR_B, N_stat=5, seed=0, seeds=None, N
             res[key][k] = out[key][j]
 
     if stream == "global":
+        # replica k+1's draws start where replica k's last rand() left the one
+        # stream, so the replicas run one after another (tape=0: the stream is
+        # consumed exactly, never drawn ahead)
         state = None
-        m = "rollout" if mode == "rollout" else "lightcone"
         for k, g in enumerate(gl):
-            sa = SAReplicas(g, p, c, [int(seed) & 0xFFFFFFFF], par_a=par_a, par_b=par_b, mode=m, tape=0,
+            sa = SAReplicas(g, p, c, [int(seed) & 0xFFFFFFFF], par_a=par_a, par_b=par_b, mode=mode, tape=0,
                             mt_state=state)
             sa.run(max_steps=max_steps)
             store(k, sa.results(), 0)
@@ -344,17 +437,22 @@ def sa_run(d, n, p, c, par_a=PAR_A, par_b=PAR_B, N_stat=5, seed=0, seeds=None, N
         seeds = list(seeds)
         if len(seeds) != R:
             raise ValueError(f"seeds: one per replica ({R}), got {len(seeds)}")
-        # replicas that share a graph run together (bit-packed)
-        groups = {}
-        for k, g in enumerate(gl):
-            groups.setdefault(id(g), []).append(k)
-        for ks in groups.values():
-            sa = SAReplicas(gl[ks[0]], p, c, [seeds[k] for k in ks], par_a=par_a, par_b=par_b, mode=mode)
-            sa.run(max_steps=max_steps)
-            out = sa.results()
-            for j, k in enumerate(ks):
-                store(k, out, j)
-            del sa
+        # every replica at once, bit-packed, each on its own graph of a stack
+        # (graphs shared by several replicas are stored once)
+        uniq, graph_of = {}, []
+        for g in gl:
+            graph_of.append(uniq.setdefault(id(g), len(uniq)))
+        stack = [None] * len(uniq)
+        for g in gl:
+            stack[uniq[id(g)]] = g
+        src = stack[0] if len(stack) == 1 else stack
+        sa = SAReplicas(src, p, c, seeds, par_a=par_a, par_b=par_b, mode=mode,
+                        graph_of=None if len(stack) == 1 else graph_of)
+        sa.run(max_steps=max_steps)
+        out = sa.results()
+        for k in range(R):
+            store(k, out, k)
+        del sa
     else:
         raise ValueError(f"stream must be 'global' or 'independent', got {stream!r}")
     res["graphs"] = np.stack([g.astype(int) for g in gl])

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol(mjx_mod):
     for name in declared_functions():
         assert hasattr(raw, name), f"{name} declared in mjx.h but not exported"
         assert name in mjx_mod._lib.SIGNATURES, f"{name} has no ctypes signature"
-    assert lib.mjx_abi_version() == 1
+    assert lib.mjx_abi_version() == 2
 
 
 def test_sa_state_struct_matches_header(mjx_mod):

@@ -176,3 +176,44 @@ def test_bdcm_device_loop_stops_at_t_max(mjx_mod):
     assert res["counts"] == host["counts"] == 0.5 and list(res["iters"]) == list(host["iters"]) == [5, 5]
     for k in ("m_init", "ent1", "ent"):
         assert np.array_equal(res[k], host[k])
+
+
+def test_captured_loop_survives_buffer_reallocation(mjx_mod):
+    """A captured convergence loop bakes in the plan's update buffer and
+    scratch slab: converge at p=c=1, a sweep at p+c=3 (the update buffer
+    grows, a new scratch slab for the hub's class), converge at p=c=1 again
+    -- the second loop must not replay the first capture into freed memory
+    (ADVICE r02): it equals the host loop."""
+    rng = np.random.default_rng(3)
+    n = 120
+    u, v = mjx_mod.erdos_renyi_edges(n, 3.0 / (n - 1), seed=4)
+    hub_nb = rng.choice(np.arange(1, n), size=14, replace=False)        # degree >= 14: scratch slab at T=3
+    pairs = set(zip(u.tolist(), v.tolist())) | {(min(0, int(k)), max(0, int(k))) for k in hub_nb}
+    pairs = sorted((a, b) for a, b in pairs if a != b)
+    u, v = np.array([a for a, _ in pairs]), np.array([b for _, b in pairs])
+    n2, u2, v2, iso = mjx_mod.remove_isolated(n, u, v)
+    rp, col = mjx_mod.csr_from_edges(n2, u2, v2)
+    plan = mjx_mod.BDCMPlan(np.stack([u2, v2], axis=1), rp, col, n_total=n, n_iso=iso)
+    assert max(plan.classes) >= 13
+    assert mjx_mod.load_library().mjx_bdcm_scratch_bytes(max(plan.classes), 2, 1) > 0
+
+    def chi0(nc):
+        x = rng.random((2 * plan.E, nc))
+        return x / x.sum(axis=1, keepdims=True)
+
+    lm, damp, eps = 0.4, 0.1, 1e-9
+    x16, x64 = chi0(16), chi0(64)
+    a = dev(x16)
+    mjx_mod.bdcm_converge(a, plan, 1, 1, 1, lm, damp, eps, 40, batch=8, graph=True)
+    b64 = dev(x64)
+    mjx_mod.BDCM_ER(b64, plan, 2, 1, 1, lm, damp)
+    a2, b2 = dev(x16), dev(x16)
+    t_dev, _ = mjx_mod.bdcm_converge(a2, plan, 1, 1, 1, lm, damp, eps, 40, batch=8, graph=True)
+    t = 0
+    while t < t_dev:
+        mjx_mod.BDCM_ER(b2, plan, 1, 1, 1, lm, damp)
+        t += 1
+    assert torch.equal(a2, b2)
+    want = orc.BDCM_ER(x64, orc.Plan.from_csr(plan.edges_host, plan.row_ptr_host, plan.col_host, plan.n,
+                                               plan.n_iso), 2, 1, 1, lm, damp)
+    assert np.max(np.abs(b64.cpu().numpy() - want)) < 1e-12

@@ -121,13 +121,12 @@ def test_range_sweep_argument_checks(mjx_mod):
 @pytest.mark.parametrize("n,d,world", [(100_000, 6, 1), (100_037 + 1, 3, 3), (40_000_000, 3, 2), (5000, 4, 8),
                                         (3_000_000, 16, 1), (2_500_002, 5, 4)])
 @pytest.mark.parametrize("form", ["flat", "segments"])
-def test_binned_sweep_equals_gather_sweep(mjx_mod, n, d, world, form, monkeypatch):
+def test_binned_sweep_equals_gather_sweep(mjx_mod, n, d, world, form):
     """The source-binned plan (several 1M-node source blocks and 64K-node
     destination tiles from n = 2.5e6 on) gives the gather sweep's words and
     counts for every rank's rows; d = 16 fills the byte counters to the top.
-    Both phase-2 forms (flat tile stream, per-segment loop) are run."""
-    if form == "segments":
-        monkeypatch.setenv("MJX_BIN_APPLY", "segments")
+    Both phase-2 forms (flat tile stream, per-segment loop) are run, selected
+    by the ABI's apply_form argument."""
     seed = 9
     ranges = [mjx_mod.NodeRange(n, world, r) for r in range(world)]
     lib = mjx_mod.load_library()
@@ -147,7 +146,7 @@ def test_binned_sweep_equals_gather_sweep(mjx_mod, n, d, world, form, monkeypatc
                                           cw.data_ptr(), st) == 0
         # a plan per rank range, built through the same entry points ShardedRRG uses
         plan = mjx_mod.BinnedPlan(rows, n, d, r.lo, r.hi)
-        plan.sweep(s_in, got, cg)
+        plan.sweep(s_in, got, cg, apply_form=form)
         if sh is not None:
             out = torch.zeros_like(s_in)
             c3 = torch.zeros(1, dtype=torch.int64, device="cuda")

@@ -34,13 +34,15 @@ def test_sa_init_draws_reference_s0(mjx_mod):
 
 
 def _sa(mjx_mod, N, p, c, seeds, mode):
-    """mode: "lightcone" (default tape), "lightcone-notape" (draws inside the
-    step kernel), "lightcone-tape7" (tape chunks of 7 steps), "rollout"."""
+    """mode: "lightcone" (HBM cone layout, default tape), "lightcone-notape"
+    (draws inside the step kernel), "lightcone-tape7" (tape chunks of 7
+    steps), "lightcone-lds" (graph, levels and stream in LDS), "rollout"."""
     tape = {"lightcone-notape": 0, "lightcone-tape7": 7}.get(mode, 1024)
-    return mjx_mod.SAReplicas(N, p, c, seeds, mode=mode.split("-")[0], tape=tape)
+    layout = "lds" if mode == "lightcone-lds" else "cone"
+    return mjx_mod.SAReplicas(N, p, c, seeds, mode=mode.split("-")[0], tape=tape, layout=layout)
 
 
-MODES = ["lightcone", "lightcone-notape", "lightcone-tape7", "rollout"]
+MODES = ["lightcone", "lightcone-notape", "lightcone-tape7", "lightcone-lds", "rollout"]
 
 
 @pytest.mark.parametrize("mode", MODES)
@@ -110,26 +112,20 @@ def test_sa_lightcone_levels_stay_consistent(mjx_mod, d, p, c):
                                           (3, 2, 1, "lightcone"), (3, 1, 1, "spec8"), (3, 1, 1, "spec16"),
                                           (4, 1, 1, "spec8"), (4, 1, 1, "spec16"), (4, 1, 1, "lightcone"),
                                           (4, 2, 2, ""), (5, 1, 2, ""), (3, 3, 4, "")])
-def test_sa_cone_layout_equals_separate_levels(mjx_mod, d, p, c, kernel, monkeypatch):
+def test_sa_cone_layout_equals_separate_levels(mjx_mod, d, p, c, kernel):
     """The cone layout (levels of one (node, word) side by side) gives the
     same proposals, accepts, sums and delta_H as separate level arrays, and
     the same final configuration and levels (LV = 2, 4 and 8 words).  At
     d=3, p+c-1=2 three kernels run on the cone: the speculative 8-proposal
     batches of 8 or 16 proposals (default; also d=3 and d=4 at p+c-1=1), the one-round-trip step
-    (MJX_NO_SPEC) and the general light-cone step (MJX_NO_CONE2)."""
-    if kernel == "spec16":
-        monkeypatch.setenv("MJX_SPEC_K", "16")
-    elif kernel == "spec8":
-        monkeypatch.setenv("MJX_SPEC_K", "8")
-    elif kernel == "one_trip":
-        monkeypatch.setenv("MJX_NO_SPEC", "1")
-    elif kernel == "lightcone":
-        monkeypatch.setenv("MJX_NO_SPEC", "1")
-        monkeypatch.setenv("MJX_NO_CONE2", "1")
+    (no_spec) and the general light-cone step (no_spec + no_cone2), chosen
+    through the state's kernel options."""
+    opts = {"spec16": {"spec_k": 16}, "spec8": {"spec_k": 8}, "one_trip": {"no_spec": True},
+            "lightcone": {"no_spec": True, "no_cone2": True}}.get(kernel, {})
     n = 3000
     adj = mjx_mod.random_regular_graph(d, n, seed=4)
     R = 150
-    a = mjx_mod.SAReplicas(adj, p, c, list(range(R)), mode="lightcone", layout="cone")
+    a = mjx_mod.SAReplicas(adj, p, c, list(range(R)), mode="lightcone", layout="cone", kernel=opts)
     b = mjx_mod.SAReplicas(adj, p, c, list(range(R)), mode="lightcone", layout="levels")
     assert a.cone is not None and b.cone is None
     for k in (7, 600, 1500):
@@ -179,13 +175,13 @@ def test_E_delta_matches_oracle(mjx_mod):
 
 
 @pytest.mark.parametrize("split", ["1", "4", "64"])
-def test_sa_lightcone_wave_split_is_bit_exact(mjx_mod, split, monkeypatch):
+def test_sa_lightcone_wave_split_is_bit_exact(mjx_mod, split):
     """Waves per word column (1, 4, 64 replicas per wave ... 1) only change the
     schedule: the accept sequences equal the oracle's."""
-    monkeypatch.setenv("MJX_LC_SPLIT", split)
     n, d, p, c = 400, 3, 2, 1
     adj = mjx_mod.random_regular_graph(d, n, seed=5)
-    sa = mjx_mod.SAReplicas(adj, p, c, list(range(70)), mode="lightcone")
+    sa = mjx_mod.SAReplicas(adj, p, c, list(range(70)), mode="lightcone",
+                            kernel={"split": int(split), "no_spec": True, "no_cone2": True})
     tr = {k: v.cpu().numpy() for k, v in sa.steps(300, trace=True).items()}
     for r in (0, 5, 63, 64, 69):
         o = orc.sa_loop(adj, p, c, r, max_steps=300, trace=True)["trace"]

@@ -1,0 +1,113 @@
+"""SA replicas on distinct graphs, run together (code/SA_RRG.py:58-62 draws a
+fresh random regular graph for every replica), and the light-cone kernels'
+own-bit re-reads under stress.  Every replica is checked bit for bit against
+the C restatement of the reference's SA loop (oracle/orc_majority.c,
+code/SA_RRG.py:63-88) on ITS graph: proposals, accepts, sum(s_end), delta_H,
+final conf and step count."""
+import numpy as np
+import pytest
+
+from oracle import fast
+
+pytestmark = pytest.mark.gpu
+
+
+def _graphs(mjx_mod, d, n, G, base):
+    return [mjx_mod.random_regular_graph(d, n, seed=base + g) for g in range(G)]
+
+
+def _check(tr, conf, t, graphs, graph_of, seeds, p, c, K, replicas):
+    for r in replicas:
+        o = fast.sa_loop(graphs[graph_of[r]], p, c, seeds[r], max_steps=K, trace=True)
+        L = len(o["trace"]["i"])
+        assert L == t[r], r
+        for key in ("i", "accept", "sum_end", "dE"):
+            assert np.array_equal(tr[key][:L, r], o["trace"][key]), (r, key)
+        assert np.array_equal(conf[r], o["conf"]), r
+
+
+@pytest.mark.parametrize("d,n,p,c,R,K,kernel,mode,layout", [
+    (3, 500, 2, 1, 70, 400, {}, "lightcone", "cone"),                       # speculative batches
+    (3, 500, 2, 1, 70, 400, {"spec_k": 16}, "lightcone", "cone"),
+    (3, 500, 2, 1, 70, 300, {"no_spec": True}, "lightcone", "cone"),        # one round trip
+    (3, 500, 2, 1, 70, 300, {"no_spec": True, "no_cone2": True}, "lightcone", "cone"),
+    (4, 400, 1, 1, 130, 400, {}, "lightcone", "cone"),
+    (4, 300, 3, 1, 65, 300, {}, "lightcone", "cone"),                       # SA_RRG.py's p=3, c=1
+    (6, 200, 2, 1, 20, 200, {}, "lightcone", "cone"),
+    (3, 500, 2, 1, 70, 400, {}, "lightcone", "lds"),                        # LDS-resident replicas
+    (4, 400, 1, 1, 130, 400, {}, "lightcone", "lds"),
+    (4, 300, 3, 1, 65, 300, {}, "lightcone", "lds"),
+    (6, 200, 2, 1, 20, 200, {}, "lightcone", "lds"),
+    (5, 200, 2, 2, 20, 200, {}, "lightcone", "lds"),                        # runtime degree, T = 3
+    (4, 200, 1, 1, 5, 40, {}, "rollout", None),
+])
+def test_distinct_graphs_match_oracle(mjx_mod, d, n, p, c, R, K, kernel, mode, layout):
+    graphs = _graphs(mjx_mod, d, n, R, 100)
+    seeds = list(range(1000, 1000 + R))
+    sa = mjx_mod.SAReplicas(graphs, p, c, seeds, mode=mode, kernel=kernel, layout=layout or "auto")
+    assert sa.rep_graph is not None and sa.mode == mode and sa.layout == layout
+    tr = {k: v.cpu().numpy() for k, v in sa.steps(K, trace=True).items()}
+    conf, t = sa.conf().cpu().numpy(), sa.t.cpu().numpy()
+    _check(tr, conf, t, graphs, list(range(R)), seeds, p, c, K, sorted({0, 1, R // 2, R - 1, min(64, R - 1)}))
+
+
+def test_shared_graph_stack_with_graph_of(mjx_mod):
+    """Several replicas per graph (graph_of): each replica equals the oracle
+    on its graph, and replicas of one graph equal a single-graph run."""
+    d, n, p, c, K = 3, 400, 2, 1, 300
+    graphs = _graphs(mjx_mod, d, n, 3, 7)
+    R = 96
+    graph_of = [r % 3 for r in range(R)]
+    seeds = list(range(R))
+    sa = mjx_mod.SAReplicas(graphs, p, c, seeds, graph_of=graph_of, layout="cone")
+    tr = {k: v.cpu().numpy() for k, v in sa.steps(K, trace=True).items()}
+    conf, t = sa.conf().cpu().numpy(), sa.t.cpu().numpy()
+    _check(tr, conf, t, graphs, graph_of, seeds, p, c, K, (0, 1, 2, 50, 95))
+    one = mjx_mod.SAReplicas(graphs[1], p, c, [seeds[r] for r in range(1, R, 3)], layout="lds")
+    tr1 = one.steps(K, trace=True)
+    assert np.array_equal(tr1["accept"].cpu().numpy(), tr["accept"][:, 1::3])
+
+
+@pytest.mark.parametrize("multi,layout", [(False, "cone"), (True, "cone"), (True, "lds")])
+def test_own_bit_rereads_stress(mjx_mod, multi, layout):
+    """Built to expose stale own-bit reads: n = 64, d = 3,
+    R = 4096 replicas, 16-proposal speculative batches, p+c-1 = 2 -- every
+    batch re-reads words its lane has just flipped (the graph has 64 nodes),
+    most balls are not trees (the list path), and 64 replicas share each word.
+    Every replica's final configuration and step count equal the oracle's,
+    and sampled traces match."""
+    d, n, p, c, R, K = 3, 64, 2, 1, 4096, 400
+    graphs = _graphs(mjx_mod, d, n, 16 if multi else 1, 31)
+    graph_of = [r % 16 for r in range(R)] if multi else [0] * R
+    seeds = list(range(R))
+    src = graphs if multi else graphs[0]
+    sa = mjx_mod.SAReplicas(src, p, c, seeds, graph_of=graph_of if multi else None, kernel={"spec_k": 16},
+                            layout=layout)
+    assert sa.layout == layout
+    tr = {k: v.cpu().numpy() for k, v in sa.steps(K, trace=True).items()}
+    conf, t = sa.conf().cpu().numpy(), sa.t.cpu().numpy()
+    _check(tr, conf, t, graphs, graph_of, seeds, p, c, K, (0, 63, 64, 2047, 4095))
+    for r in range(R):
+        o = fast.sa_loop(graphs[graph_of[r]], p, c, seeds[r], max_steps=K)
+        assert o["num_steps"] == t[r] and np.array_equal(conf[r], o["conf"]), r
+
+
+@pytest.mark.parametrize("n,N_stat,seed,graph_seed", [(400, 6, 11, 60), (1000, 1, 5, 50)])
+def test_sa_run_distinct_graphs_to_consensus(mjx_mod, n, N_stat, seed, graph_seed):
+    """sa_run with the reference's shape -- a fresh graph per replica, run to
+    m_final = 1 (code/SA_RRG.py:58-88) at SA_RRG.py's p=3, c=1 -- all
+    replicas in one SAReplicas; conf / num_steps / mag_reached equal the
+    oracle's runs to consensus on the same graphs (1.1e4-3e4 proposals per
+    replica at n=400, 2.1e5 at n=1000; the steps-to-consensus distribution
+    has a heavy tail -- another seed at n=1000 runs past 2e7)."""
+    d, p, c = 4, 3, 1
+    res = mjx_mod.sa_run(d, n, p, c, N_stat=N_stat, seed=seed, graph_seed=graph_seed)
+    for k in range(N_stat):
+        g = mjx_mod.random_regular_graph(d, n, seed=graph_seed + k)
+        assert np.array_equal(res["graphs"][k], g)
+        o = fast.sa_loop(g, p, c, seed + k)
+        assert o["done"] == 1
+        assert res["num_steps"][k] == o["num_steps"]
+        assert np.array_equal(res["conf"][k], o["conf"])
+        assert res["mag_reached"][k] == o["mag_reached"]
+        assert res["done"][k] == 1
