@@ -257,6 +257,23 @@ int mjx_sa_cone_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int
                       double par_a, double par_b, double a_cap, double b_cap, int64_t t_cap,
                       void* stream);
 
+/* Record layout: the cone with each (node, word column) sector preceded by the
+ * node's adjacency row (int32 x4, zero padded): rec[(w*n + v)*LV + e], words
+ * 0..1 = the row, word 2 + t = level t, LV = mjx_sa_rec_words(d,p,c) (4 or 8;
+ * -1 if unsupported: d <= 4, p+c-1 <= 5).  The speculative step then fetches a
+ * ball node's row and levels in one line.  One graph shared by every replica
+ * (st->rep_graph must be NULL).  Same proposals, accepts and outputs as every
+ * other layout. */
+int mjx_sa_rec_words(int d, int p, int c);
+int mjx_sa_rec_pack(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R, const uint64_t* s,
+                    uint64_t* const* levels, uint64_t* rec, void* stream);
+int mjx_sa_rec_unpack(int64_t n, int d, int p, int c, int64_t R, const uint64_t* rec, uint64_t* s,
+                      uint64_t* const* levels, void* stream);
+int mjx_sa_rec_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d, int p, int c, int64_t R,
+                     uint64_t* s, uint64_t* rec, mjx_sa_state* st, int64_t nsteps,
+                     double par_a, double par_b, double a_cap, double b_cap, int64_t t_cap,
+                     void* stream);
+
 /* LDS-resident light-cone SA (small graphs, the reference's own sizes: n = 1e4,
  * d = 4, code/SA_RRG.py:44-52): a workgroup per replica keeps its graph (uint16
  * rows), the rollout levels onestep^t(s) (t = 0..p+c-1, bit arrays) and its
@@ -316,6 +333,22 @@ int mjx_hpr_new_biases_mask(int dtype, void* biases, const void* marg, const uin
  * stream of its own beside the iterations that consume the masks. */
 int mjx_hpr_refresh_masks(uint32_t* state, int32_t* left_next, int64_t n, int k, const double* thresh,
                           uint8_t* mask, void* stream);
+/* The same draws by G workgroups at once (MT19937 jump-ahead, csrc/mjx_mtjump.hip):
+ * the batch's 2nk words are split into chunks of L words (a multiple of 624), chunk
+ * j's workgroup jumps the batch-start state ahead by jL-1 words with the polynomial
+ * z^(jL-1) mod P (P = the characteristic polynomial of MT19937's state map).
+ * mjx_mt_jump_geometry: L and the number of chunks actually used for (n, k, G);
+ * mjx_mt_jump_table_words / mjx_mt_jump_table: the (chunks-1) x 312 uint64 table
+ * of those polynomials, computed on the HOST (setup, once per (n, k, G));
+ * mjx_hpr_refresh_masks_jump: reads state_in/ln_in (the engine at the batch start),
+ * writes state_out/ln_out (after the batch; must not alias the inputs), the masks
+ * as mjx_hpr_refresh_masks; `table` is the device copy. */
+int mjx_mt_jump_geometry(int64_t n, int k, int G, int64_t* L, int* G_used);
+int64_t mjx_mt_jump_table_words(int64_t n, int k, int G);
+int mjx_mt_jump_table(int64_t n, int k, int G, uint64_t* table);
+int mjx_hpr_refresh_masks_jump(const uint32_t* state_in, const int32_t* ln_in, uint32_t* state_out,
+                               int32_t* ln_out, int64_t n, int k, int G, const uint64_t* table,
+                               const double* thresh, uint8_t* mask, void* stream);
 /* The edge half of marginals_comp (code/HPR_pytorch_RRG.py:150-161) alone:
  * zwork[4E] = per-row normalised (Z+ [2E], Z- [2E]) of every directed row. */
 int mjx_hpr_edge_z(int dtype, const void* chi, int64_t E, int p, int c, double eps, void* zwork,

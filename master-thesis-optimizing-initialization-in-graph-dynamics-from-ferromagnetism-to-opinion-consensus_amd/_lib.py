@@ -56,12 +56,21 @@ SIGNATURES = {
     "mjx_sa_cone_unpack": [c_i64, c_int, c_int, c_i64, c_vp, c_vp, c_vp, c_vp],
     "mjx_sa_cone_steps": [c_vp, c_vp, c_i64, c_int, c_int, c_int, c_i64, c_vp, c_vp, c_vp,
                           c_i64, c_dbl, c_dbl, c_dbl, c_dbl, c_i64, c_vp],
+    "mjx_sa_rec_words": [c_int, c_int, c_int],
+    "mjx_sa_rec_pack": [c_vp, c_i64, c_int, c_int, c_int, c_i64, c_vp, c_vp, c_vp, c_vp],
+    "mjx_sa_rec_unpack": [c_i64, c_int, c_int, c_int, c_i64, c_vp, c_vp, c_vp, c_vp],
+    "mjx_sa_rec_steps": [c_vp, c_vp, c_i64, c_int, c_int, c_int, c_i64, c_vp, c_vp, c_vp,
+                         c_i64, c_dbl, c_dbl, c_dbl, c_dbl, c_i64, c_vp],
     "mjx_hpr_update": [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_int,
                        c_dbl, c_dbl, c_dbl, c_vp],
     "mjx_hpr_marginals": [c_int, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_dbl, c_vp, c_vp, c_vp],
     "mjx_hpr_new_biases": [c_int, c_vp, c_vp, c_vp, c_dbl, c_dbl, c_i64, c_vp, c_vp],
     "mjx_hpr_new_biases_mask": [c_int, c_vp, c_vp, c_vp, c_dbl, c_i64, c_vp, c_vp],
     "mjx_hpr_refresh_masks": [c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp],
+    "mjx_mt_jump_geometry": [c_i64, c_int, c_int, c_vp, c_vp],
+    "mjx_mt_jump_table_words": [c_i64, c_int, c_int],
+    "mjx_mt_jump_table": [c_i64, c_int, c_int, c_vp],
+    "mjx_hpr_refresh_masks_jump": [c_vp, c_vp, c_vp, c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp],
     "mjx_hpr_edge_z": [c_int, c_vp, c_i64, c_int, c_int, c_dbl, c_vp, c_vp],
     "mjx_hpr_node_biases": [c_int, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp],
     "mjx_hpr_q_supported": [c_int, c_int, c_int, c_int],
@@ -96,7 +105,8 @@ SIGNATURES = {
 }
 _RESTYPES = {"mjx_strerror": ctypes.c_char_p, "mjx_build_id": ctypes.c_char_p, "mjx_last_hip_error": ctypes.c_char_p,
              "mjx_sa_lightcone_lds": c_i64, "mjx_sa_lds_bytes": c_i64, "mjx_bdcm_lds_bytes": c_i64, "mjx_bdcm_scratch_bytes": c_i64,
-             "mjx_rrg_partner_host": c_i64, "mjx_er_work_bytes": c_i64, "mjx_hpr_er_scratch_bytes": c_i64}
+             "mjx_rrg_partner_host": c_i64, "mjx_er_work_bytes": c_i64, "mjx_hpr_er_scratch_bytes": c_i64,
+             "mjx_mt_jump_table_words": c_i64}
 
 MJX_OK, MJX_EINVAL, MJX_EHIP, MJX_ERANGE = 0, 1, 2, 3      # status codes (include/mjx.h)
 MJX_I8, MJX_I32, MJX_I64 = 1, 4, 8

@@ -324,6 +324,9 @@ struct LcLevels {
     int64_t ns;
     int64_t cs;
     u64* s0c;                // cone layout: the configuration's own array (level-0 flips mirrored), else null
+    int lo;                  // record layout (cone with rows): a (node, column) record of ns words holds the
+                             // node's adjacency row (int32 x4) in words 0..1 and level t at word lo + t
+                             // (s[t] = record base + lo + t); 0 = the plain cone / separate levels
     int off[LC_MAXT + 2];    // list slot offset of level t; off[T+1] = candidate list
     int tab;                 // slot offset of the ball table (node ids | adjacency rows | candidate entries)
     int ball;                // table capacity: nodes of the radius-T ball (d-regular bound)
@@ -1065,6 +1068,10 @@ struct ConeRd {
         a = (u64)x.x | ((u64)x.y << 32);
         b = (u64)x.z | ((u64)x.w << 32);
     }
+    __device__ __forceinline__ int4 row(uint32_t idx) const {                    // 16-B adjacency row of a record
+        const v4u32_t x = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(idx * 8u), 0, kSc1);
+        return make_int4((int)x.x, (int)x.y, (int)x.z, (int)x.w);
+    }
 };
 
 template <int D>
@@ -1395,16 +1402,19 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
     int done = live ? st.done[r] : 1;
     int64_t pos = 0;                                          // proposals of this launch consumed
     int ties = 0;
+    // sc1 loads: see ConeRd; over the record base (= the level-0 words unless
+    // the records carry the adjacency rows, L.lo = 2)
+    const uint32_t lo = (uint32_t)L.lo;
+    const ConeRd crd(cone - lo + colo, n * NS * 8);
     auto row = [&](int32_t v, int32_t (&o)[D]) {
-        const int4 q = adj_pad[(uint32_t)v < (uint32_t)n ? v : 0];             // never out of bounds
+        const uint32_t vv = (uint32_t)v < (uint32_t)n ? (uint32_t)v : 0u;     // never out of bounds
+        const int4 q = lo ? crd.row(vv * (uint32_t)NS) : adj_pad[vv];
         o[0] = q.x; o[1] = q.y; o[2] = q.z;
         if constexpr (D == 4) o[3] = q.w;
     };
-    // sc1 loads: see ConeRd
-    const ConeRd crd(cone + colo, n * NS * 8);
-    auto w = [&](int32_t v, int lv) { return crd.word((uint32_t)v * (uint32_t)NS + (uint32_t)lv); };
+    auto w = [&](int32_t v, int lv) { return crd.word((uint32_t)v * (uint32_t)NS + lo + (uint32_t)lv); };
     auto sector = [&](int32_t v, u64 (&o)[3]) {      // levels 0..T of v
-        const uint32_t q = (uint32_t)v * (uint32_t)NS;
+        const uint32_t q = (uint32_t)v * (uint32_t)NS + lo;
         crd.pair(q, o[0], o[1]);
         o[2] = (TT == 2) ? crd.word(q + 2) : 0ull;
     };
@@ -1933,7 +1943,8 @@ static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d
         return MJX_OK;
     };
     // ... and its speculative form: the 8 lanes of a group take 8 proposals of one replica
-    const int4* rows4 = (d == 4) ? (const int4*)adj : (const int4*)adj_pad;   // 16-B rows
+    // 16-B rows (the record layout reads them from the records)
+    const int4* rows4 = (d == 4 || L.lo) ? (const int4*)adj : (const int4*)adj_pad;
     // 8 proposals per batch; 16 when 8 would leave CUs without a wave (few word columns):
     // configs[1] at R = 1024 3.05 -> 1.78 us per step, at R = 4096 16 is slower (3.76 vs 4.10)
     const int spec_k = st.opt_spec_k ? st.opt_spec_k : ((W * 8 < kCUs) ? 16 : 8);
@@ -1998,6 +2009,7 @@ extern "C" int mjx_sa_lightcone_steps(const int32_t* adj, int64_t n, int d, int 
     L.ns = (R + 63) / 64;
     L.cs = 1;
     L.s0c = nullptr;
+    L.lo = 0;
     return lc_steps(adj, nullptr, n, d, T, R, L, stp, nsteps, par_a, par_b, a_cap, b_cap, t_cap, stream);
 }
 
@@ -2021,24 +2033,30 @@ struct ConeSrc {
 };
 
 template <bool PACK>
-__global__ void __launch_bounds__(kBlock) k_cone_xfer(int64_t words, int T, int LV, ConeSrc src, u64* cone,
-                                                      int64_t n, int64_t W) {
+__global__ void __launch_bounds__(kBlock) k_cone_xfer(int64_t words, int T, int LV, int lo, ConeSrc src, u64* cone,
+                                                      int64_t n, int64_t W, const int32_t* __restrict__ adj, int d) {
     for (int64_t w = (int64_t)blockIdx.x * kBlock + threadIdx.x; w < words; w += (int64_t)gridDim.x * kBlock) {
-        u64* dst = cone + ((w % W) * n + w / W) * LV;
+        const int64_t v = w / W;
+        u64* dst = cone + ((w % W) * n + v) * LV;
         if constexpr (PACK) {
-            for (int t = 0; t < LV; t += 2) {
+            if (lo) {                 // record layout: the node's row (int32 x4, zero padded) first
+                int32_t r[4] = {0, 0, 0, 0};
+                for (int e = 0; e < d; ++e) r[e] = adj[v * d + e];
+                *reinterpret_cast<int4*>(dst) = make_int4(r[0], r[1], r[2], r[3]);
+            }
+            for (int t = 0; t + lo < LV; t += 2) {
                 const u64 a = (t <= T) ? src.s[t][w] : 0ull;
                 const u64 b = (t + 1 <= T) ? src.s[t + 1][w] : 0ull;
-                *reinterpret_cast<ulonglong2*>(dst + t) = make_ulonglong2(a, b);
+                *reinterpret_cast<ulonglong2*>(dst + lo + t) = make_ulonglong2(a, b);
             }
         } else {
-            for (int t = 0; t <= T; ++t) const_cast<u64*>(src.s[t])[w] = dst[t];
+            for (int t = 0; t <= T; ++t) const_cast<u64*>(src.s[t])[w] = dst[lo + t];
         }
     }
 }
 
 static int cone_xfer(bool pack, int64_t n, int p, int c, int64_t R, const uint64_t* s, uint64_t* const* levels,
-                     uint64_t* cone, void* stream) {
+                     uint64_t* cone, void* stream, int LV, int lo = 0, const int32_t* adj = nullptr, int d = 0) {
     const int T = p + c - 1;
     if (!s || !levels || !cone || n < 1 || R < 1) return MJX_EINVAL;
     if (T < 1 || T > LC_MAXT) return MJX_ERANGE;
@@ -2051,20 +2069,54 @@ static int cone_xfer(bool pack, int64_t n, int p, int c, int64_t R, const uint64
     for (int t = T + 1; t <= LC_MAXT; ++t) src.s[t] = nullptr;
     const int64_t W = (R + 63) / 64, words = n * W;
     const int grid = grid_for(words);
-    if (pack) k_cone_xfer<true><<<grid, kBlock, 0, as_stream(stream)>>>(words, T, cone_lv(T), src, (u64*)cone, n, W);
-    else k_cone_xfer<false><<<grid, kBlock, 0, as_stream(stream)>>>(words, T, cone_lv(T), src, (u64*)cone, n, W);
+    if (pack)
+        k_cone_xfer<true><<<grid, kBlock, 0, as_stream(stream)>>>(words, T, LV, lo, src, (u64*)cone, n, W, adj, d);
+    else
+        k_cone_xfer<false><<<grid, kBlock, 0, as_stream(stream)>>>(words, T, LV, lo, src, (u64*)cone, n, W, adj, d);
     MJX_LAUNCH_CHECK("k_cone_xfer");
     return MJX_OK;
 }
 
 extern "C" int mjx_sa_cone_pack(int64_t n, int p, int c, int64_t R, const uint64_t* s, uint64_t* const* levels,
                                 uint64_t* cone, void* stream) {
-    return cone_xfer(true, n, p, c, R, s, levels, cone, stream);
+    if (p + c - 1 < 1 || p + c - 1 > LC_MAXT) return MJX_ERANGE;
+    return cone_xfer(true, n, p, c, R, s, levels, cone, stream, cone_lv(p + c - 1));
 }
 
 extern "C" int mjx_sa_cone_unpack(int64_t n, int p, int c, int64_t R, const uint64_t* cone, uint64_t* s,
                                   uint64_t* const* levels, void* stream) {
-    return cone_xfer(false, n, p, c, R, s, levels, const_cast<uint64_t*>(cone), stream);
+    if (p + c - 1 < 1 || p + c - 1 > LC_MAXT) return MJX_ERANGE;
+    return cone_xfer(false, n, p, c, R, s, levels, const_cast<uint64_t*>(cone), stream, cone_lv(p + c - 1));
+}
+
+// ---------------------------------------------------------------------------
+// Record layout: the cone sector of a (node, word column) preceded by the
+// node's adjacency row, one 32- or 64-B record (rows in words 0..1, level t at
+// word 2 + t), so the speculative step's row fetches of i, its neighbours and
+// their children bring their level words in the same line: one random line per
+// ball node instead of two (row + sector).  A graph shared by every replica only
+// (a column's replicas share its rows); d <= 4.
+// ---------------------------------------------------------------------------
+static int rec_lv(int d, int T) {
+    if (d < 1 || d > 4 || T < 1 || T > 5) return -1;
+    return (2 + T + 1 <= 4) ? 4 : 8;
+}
+
+extern "C" int mjx_sa_rec_words(int d, int p, int c) { return rec_lv(d, p + c - 1); }
+
+extern "C" int mjx_sa_rec_pack(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R, const uint64_t* s,
+                               uint64_t* const* levels, uint64_t* rec, void* stream) {
+    const int LV = rec_lv(d, p + c - 1);
+    if (!adj) return MJX_EINVAL;
+    if (LV < 0) return MJX_ERANGE;
+    return cone_xfer(true, n, p, c, R, s, levels, rec, stream, LV, 2, adj, d);
+}
+
+extern "C" int mjx_sa_rec_unpack(int64_t n, int d, int p, int c, int64_t R, const uint64_t* rec, uint64_t* s,
+                                 uint64_t* const* levels, void* stream) {
+    const int LV = rec_lv(d, p + c - 1);
+    if (LV < 0) return MJX_ERANGE;
+    return cone_xfer(false, n, p, c, R, s, levels, const_cast<uint64_t*>(rec), stream, LV, 2);
 }
 
 extern "C" int mjx_sa_cone_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d, int p, int c,
@@ -2081,5 +2133,24 @@ extern "C" int mjx_sa_cone_steps(const int32_t* adj, const int32_t* adj_pad, int
     L.ns = LV;
     L.cs = n * LV;
     L.s0c = (u64*)s;
+    L.lo = 0;
+    return lc_steps(adj, adj_pad, n, d, T, R, L, stp, nsteps, par_a, par_b, a_cap, b_cap, t_cap, stream);
+}
+
+extern "C" int mjx_sa_rec_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d, int p, int c,
+                                int64_t R, uint64_t* s, uint64_t* rec, mjx_sa_state* stp, int64_t nsteps,
+                                double par_a, double par_b, double a_cap, double b_cap, int64_t t_cap,
+                                void* stream) {
+    const int T = p + c - 1;
+    if (!stp || !adj || !s || !rec || n < 2 || R < 1 || d < 1 || nsteps < 0) return MJX_EINVAL;
+    if (stp->rep_graph) return MJX_EINVAL;          // rows are per column: one shared graph
+    const int LV = rec_lv(d, T);
+    if (LV < 0 || n > (int64_t)INT32_MAX) return MJX_ERANGE;
+    LcLevels L;
+    for (int t = 0; t <= T; ++t) L.s[t] = (u64*)rec + 2 + t;
+    L.ns = LV;
+    L.cs = n * LV;
+    L.s0c = (u64*)s;
+    L.lo = 2;
     return lc_steps(adj, adj_pad, n, d, T, R, L, stp, nsteps, par_a, par_b, a_cap, b_cap, t_cap, stream);
 }

@@ -383,6 +383,26 @@ class HPRState:
         b[16:24] = np.array([nxt], dtype=np.uint64).view(np.uint8)
         return torch.from_numpy(b)
 
+    JUMP_CHUNKS = 256      # workgroups of the jump-ahead generator (one per CU)
+
+    def _jump_table(self, k):
+        """Device copy of the jump polynomials z^(jL-1) mod P for a batch of k
+        iterations (mjx_mt_jump_table, host setup once per k), or None when
+        the batch fits one chunk."""
+        cache = self.__dict__.setdefault("_jump_tables", {})
+        if k not in cache:
+            lib = _lib.load()
+            words = lib.mjx_mt_jump_table_words(self.plan.n, k, self.JUMP_CHUNKS)
+            if words < 0:
+                raise _lib.MjxError(f"no jump-ahead geometry for n={self.plan.n}, k={k}")
+            if words == 0:
+                cache[k] = None
+            else:
+                host = np.empty(words, dtype=np.uint64)
+                _lib.call("mjx_mt_jump_table", self.plan.n, k, self.JUMP_CHUNKS, host.ctypes.data)
+                cache[k] = torch.from_numpy(host.view(np.int64)).to(self.s.device)
+        return cache[k]
+
     def draw_batch_device(self, k, t0=None):
         """draw_batch on the device (mjx_hpr_refresh_masks on the generator's
         own stream): the same masks, no host work but k thresholds."""
@@ -402,13 +422,17 @@ class HPRState:
         if self.layout == "q":
             scales.copy_(torch.tensor([self.decay(t0 + j) for j in range(k + 1)], dtype=self.dtype))
         gs = self._gen_stream
+        table = self._jump_table(k)
         with torch.cuda.stream(gs):
             gs.wait_event(self._mask_free[slot])           # the batch two back has copied its masks out
             self._snap[slot][0].copy_(self._mt)
             self._snap[slot][1].copy_(self._ln)
             self._gthr[slot].copy_(thr)
-            _lib.call("mjx_hpr_refresh_masks", _device.ptr(self._mt), _device.ptr(self._ln), self.plan.n, k,
-                      _device.ptr(self._gthr[slot]), _device.ptr(self._gmask[slot]), gs.cuda_stream)
+            # the batch-start state (the snapshot) in, the state after the batch out
+            _lib.call("mjx_hpr_refresh_masks_jump", _device.ptr(self._snap[slot][0]), _device.ptr(self._snap[slot][1]),
+                      _device.ptr(self._mt), _device.ptr(self._ln), self.plan.n, k, self.JUMP_CHUNKS,
+                      _device.ptr(table) if table is not None else None, _device.ptr(self._gthr[slot]),
+                      _device.ptr(self._gmask[slot]), gs.cuda_stream)
             self._gen_done[slot].record(gs)
         return {"k": k, "t0": t0, "slot": slot, "scales": scales, "device": True}
 

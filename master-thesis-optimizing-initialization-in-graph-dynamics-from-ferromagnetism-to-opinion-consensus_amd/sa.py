@@ -101,7 +101,9 @@ class SAReplicas:
         keeps each replica's graph, levels and stream in LDS for a whole call
         (mjx_sa_lds_steps; n <= 65535, the reference's own sizes), ``"cone"``
         keeps the cached levels of one (node, word) side by side in HBM
-        (mjx_sa_cone_steps), ``"levels"`` as separate arrays
+        (mjx_sa_cone_steps), ``"rec"`` the cone with each node's adjacency
+        row in front of its levels (mjx_sa_rec_steps; one shared graph, d <= 4),
+        ``"levels"`` as separate arrays
         (mjx_sa_lightcone_steps); ``"auto"``: lds where it fits, else cone;
         same results in every layout.  ``kernel``: light-cone kernel
         selection passed to the ABI (tests, tuning): ``split`` (waves per word
@@ -184,13 +186,16 @@ class SAReplicas:
         if mode not in ("lightcone", "rollout"):
             raise ValueError(f"unknown SA mode {mode!r}")
         self.mode = mode
-        if layout not in ("auto", "lds", "cone", "levels"):
+        if layout not in ("auto", "lds", "cone", "rec", "levels"):
             raise ValueError(f"unknown light-cone layout {layout!r}")
         lds_fits = 0 < _lib.load().mjx_sa_lds_bytes(n, self.d, self.p, self.c) <= 160 * 1024
         if layout == "auto":
             layout = "lds" if lds_fits else "cone"
         if mode == "lightcone" and layout == "lds" and not lds_fits:
             raise ValueError(f"LDS-resident SA unsupported for n={n}, d={self.d}, p+c-1={T}")
+        if mode == "lightcone" and layout == "rec" and (self.rep_graph is not None or
+                                                        _lib.load().mjx_sa_rec_words(self.d, self.p, self.c) < 0):
+            raise ValueError("the record layout needs one graph shared by every replica and d <= 4")
         self.layout = layout if mode == "lightcone" else None
         self.cone = None
         self.adj_pad = None
@@ -209,12 +214,18 @@ class SAReplicas:
                 self.cone = torch.empty(n * W * lv, dtype=i64, device=dev)
                 _lib.call("mjx_sa_cone_pack", n, self.p, self.c, R, _device.ptr(self.s), self._lvl,
                           _device.ptr(self.cone), _device.stream_handle())
-                if self.d == 3:
-                    # rows padded to 16 B: one load per row in the one-round-trip step
-                    # (graph g of a stack at rows g*n .. g*n + n - 1)
-                    rows = self.adj.numel() // 3
-                    self.adj_pad = torch.zeros((rows, 4), dtype=torch.int32, device=dev)
-                    self.adj_pad[:, :3] = self.adj.view(rows, 3)
+            elif layout == "rec":
+                # the cone with each node's adjacency row in front of its levels
+                lv = _lib.load().mjx_sa_rec_words(self.d, self.p, self.c)
+                self.cone = torch.empty(n * W * lv, dtype=i64, device=dev)
+                _lib.call("mjx_sa_rec_pack", _device.ptr(self.adj), n, self.d, self.p, self.c, R,
+                          _device.ptr(self.s), self._lvl, _device.ptr(self.cone), _device.stream_handle())
+            if layout == "cone" and self.d == 3:
+                # rows padded to 16 B: one load per row in the one-round-trip step
+                # (graph g of a stack at rows g*n .. g*n + n - 1)
+                rows = self.adj.numel() // 3
+                self.adj_pad = torch.zeros((rows, 4), dtype=torch.int32, device=dev)
+                self.adj_pad[:, :3] = self.adj.view(rows, 3)
             # proposal tape: (i, u) of `tape` steps per replica drawn ahead by
             # a wave per replica (0 = draw inside the step kernel)
             self.tape_cap = int(tape) if tape else 0
@@ -249,6 +260,10 @@ class SAReplicas:
             _lib.call("mjx_sa_lds_steps", _device.ptr(self.adj), self.n, self.d, self.p, self.c, self.R,
                       _device.ptr(self.s), _lib.ctypes.byref(st), k, self.par_a, self.par_b, self.a_cap, self.b_cap,
                       int(self.t_cap), _device.stream_handle())
+        elif self.layout == "rec":
+            _lib.call("mjx_sa_rec_steps", _device.ptr(self.adj), None, self.n, self.d, self.p, self.c,
+                      self.R, _device.ptr(self.s), _device.ptr(self.cone), _lib.ctypes.byref(st), k, self.par_a,
+                      self.par_b, self.a_cap, self.b_cap, int(self.t_cap), _device.stream_handle())
         elif self.mode == "lightcone" and self.cone is not None:
             _lib.call("mjx_sa_cone_steps", _device.ptr(self.adj),
                       _device.ptr(self.adj_pad) if self.adj_pad is not None else None, self.n, self.d, self.p, self.c,
@@ -296,8 +311,12 @@ class SAReplicas:
             return
         if getattr(self, "_s0buf", None) is None:
             self._s0buf = torch.empty_like(self.s)
-        _lib.call("mjx_sa_cone_unpack", self.n, self.p, self.c, self.R, _device.ptr(self.cone),
-                  _device.ptr(self._s0buf), self._lvl, _device.stream_handle())
+        if self.layout == "rec":
+            _lib.call("mjx_sa_rec_unpack", self.n, self.d, self.p, self.c, self.R, _device.ptr(self.cone),
+                      _device.ptr(self._s0buf), self._lvl, _device.stream_handle())
+        else:
+            _lib.call("mjx_sa_cone_unpack", self.n, self.p, self.c, self.R, _device.ptr(self.cone),
+                      _device.ptr(self._s0buf), self._lvl, _device.stream_handle())
 
     def all_done(self):
         return bool((self.done != 0).all().item())

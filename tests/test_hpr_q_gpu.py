@@ -192,6 +192,47 @@ def test_device_refresh_masks_equal_torch_cpu_stream(mjx_mod, pre, n, k):
     assert torch.equal(torch.rand(9, dtype=torch.float64, generator=g2), torch.rand(9, dtype=torch.float64, generator=h))
 
 
+@pytest.mark.parametrize("pre,n,k,G", [(0, 1000, 3, 256), (3, 4097, 2, 7), (1000, 313, 5, 2), (311, 624, 4, 256),
+                                       (0, 100, 1, 256), (623, 100_000, 16, 256)])
+def test_jump_refresh_masks_equal_torch_cpu_stream(mjx_mod, pre, n, k, G):
+    """mjx_hpr_refresh_masks_jump (G workgroups, each jumping the batch-start
+    state ahead by z^(jL-1) mod P): the same masks as torch.rand(n) < thresh
+    drawn on the CPU (code/HPR_pytorch_RRG.py:142) and the CPU generator's
+    state handed back, from fresh and mid-block stream positions, down to a
+    single chunk and up to the C3 batch (n = 1e5, 16 iterations)."""
+    import numpy as np
+    plan, mk = _pair(mjx_mod, 64, 4, 2, 2, seed=1)
+    st = mk("q")
+    g = torch.Generator().manual_seed(9)
+    if pre:
+        torch.rand(pre, dtype=torch.float64, generator=g)
+    h = torch.Generator()
+    h.set_state(g.get_state())
+    st.rng_attach(g)
+    thr = [0.05 + 0.9 * j / k for j in range(k)]
+    lib = mjx_mod.load_library()
+    words = lib.mjx_mt_jump_table_words(n, k, G)
+    assert words >= 0
+    table = None
+    if words:
+        host = np.zeros(words, dtype=np.uint64)
+        assert lib.mjx_mt_jump_table(n, k, G, host.ctypes.data) == 0
+        table = torch.from_numpy(host.view(np.int64)).cuda()
+    mask = torch.empty((k, n), dtype=torch.uint8, device="cuda")
+    th = torch.tensor(thr, dtype=torch.float64, device="cuda")
+    mt_out, ln_out = torch.empty_like(st._mt), torch.empty_like(st._ln)
+    assert lib.mjx_hpr_refresh_masks_jump(st._mt.data_ptr(), st._ln.data_ptr(), mt_out.data_ptr(), ln_out.data_ptr(),
+                                          n, k, G, table.data_ptr() if table is not None else None, th.data_ptr(),
+                                          mask.data_ptr(), torch.cuda.current_stream().cuda_stream) == 0
+    want = torch.stack([torch.rand(n, dtype=torch.float64, generator=h) < thr[j] for j in range(k)])
+    assert torch.equal(mask.cpu().bool(), want)
+    st._mt.copy_(mt_out)
+    st._ln.copy_(ln_out)
+    g2 = torch.Generator()
+    g2.set_state(st.rng_state_bytes())
+    assert torch.equal(torch.rand(9, dtype=torch.float64, generator=g2), torch.rand(9, dtype=torch.float64, generator=h))
+
+
 def test_hpr_run_device_rng_equals_host_rng(mjx_mod):
     """hpr_run with the stream continued on the device and with host draws:
     same stop iteration, configuration and generator position afterwards."""

@@ -36,13 +36,14 @@ def test_sa_init_draws_reference_s0(mjx_mod):
 def _sa(mjx_mod, N, p, c, seeds, mode):
     """mode: "lightcone" (HBM cone layout, default tape), "lightcone-notape"
     (draws inside the step kernel), "lightcone-tape7" (tape chunks of 7
-    steps), "lightcone-lds" (graph, levels and stream in LDS), "rollout"."""
+    steps), "lightcone-lds" (graph, levels and stream in LDS), "lightcone-rec"
+    (the cone with the adjacency rows in its records), "rollout"."""
     tape = {"lightcone-notape": 0, "lightcone-tape7": 7}.get(mode, 1024)
-    layout = "lds" if mode == "lightcone-lds" else "cone"
+    layout = {"lightcone-lds": "lds", "lightcone-rec": "rec"}.get(mode, "cone")
     return mjx_mod.SAReplicas(N, p, c, seeds, mode=mode.split("-")[0], tape=tape, layout=layout)
 
 
-MODES = ["lightcone", "lightcone-notape", "lightcone-tape7", "lightcone-lds", "rollout"]
+MODES = ["lightcone", "lightcone-notape", "lightcone-tape7", "lightcone-lds", "lightcone-rec", "rollout"]
 
 
 @pytest.mark.parametrize("mode", MODES)
@@ -112,20 +113,24 @@ def test_sa_lightcone_levels_stay_consistent(mjx_mod, d, p, c):
                                           (3, 2, 1, "lightcone"), (3, 1, 1, "spec8"), (3, 1, 1, "spec16"),
                                           (4, 1, 1, "spec8"), (4, 1, 1, "spec16"), (4, 1, 1, "lightcone"),
                                           (4, 2, 2, ""), (5, 1, 2, ""), (3, 3, 4, "")])
-def test_sa_cone_layout_equals_separate_levels(mjx_mod, d, p, c, kernel):
+@pytest.mark.parametrize("layout", ["cone", "rec"])
+def test_sa_cone_layout_equals_separate_levels(mjx_mod, d, p, c, kernel, layout):
     """The cone layout (levels of one (node, word) side by side) gives the
     same proposals, accepts, sums and delta_H as separate level arrays, and
     the same final configuration and levels (LV = 2, 4 and 8 words).  At
     d=3, p+c-1=2 three kernels run on the cone: the speculative 8-proposal
     batches of 8 or 16 proposals (default; also d=3 and d=4 at p+c-1=1), the one-round-trip step
     (no_spec) and the general light-cone step (no_spec + no_cone2), chosen
-    through the state's kernel options."""
+    through the state's kernel options.  ``rec``: the same with every node's
+    adjacency row in its records (d <= 4)."""
+    if layout == "rec" and (d > 4 or p + c - 1 > 5):
+        pytest.skip("record layout: d <= 4, p+c-1 <= 5")
     opts = {"spec16": {"spec_k": 16}, "spec8": {"spec_k": 8}, "one_trip": {"no_spec": True},
             "lightcone": {"no_spec": True, "no_cone2": True}}.get(kernel, {})
     n = 3000
     adj = mjx_mod.random_regular_graph(d, n, seed=4)
     R = 150
-    a = mjx_mod.SAReplicas(adj, p, c, list(range(R)), mode="lightcone", layout="cone", kernel=opts)
+    a = mjx_mod.SAReplicas(adj, p, c, list(range(R)), mode="lightcone", layout=layout, kernel=opts)
     b = mjx_mod.SAReplicas(adj, p, c, list(range(R)), mode="lightcone", layout="levels")
     assert a.cone is not None and b.cone is None
     for k in (7, 600, 1500):

@@ -68,7 +68,7 @@ def test_shared_graph_stack_with_graph_of(mjx_mod):
     assert np.array_equal(tr1["accept"].cpu().numpy(), tr["accept"][:, 1::3])
 
 
-@pytest.mark.parametrize("multi,layout", [(False, "cone"), (True, "cone"), (True, "lds")])
+@pytest.mark.parametrize("multi,layout", [(False, "cone"), (False, "rec"), (True, "cone"), (True, "lds")])
 def test_own_bit_rereads_stress(mjx_mod, multi, layout):
     """Built to expose stale own-bit reads: n = 64, d = 3,
     R = 4096 replicas, 16-proposal speculative batches, p+c-1 = 2 -- every

@@ -6,7 +6,8 @@ replica-packed, 2 sweeps per rollout, fused count on the last one) a few
 times, then (unless --no-hpr) the C3 HPR iteration (d=4 RRG, N=1e5,
 p=c=2, fp32: HPr_dp + marginals_comp, in the reference layout and in the
 loop state's decay-split layout), (unless --no-sa) 1000 light-cone SA steps
-at configs[1] (the speculative batches), and (unless --no-giant) a few sweeps
+at configs[1] (the speculative batches), (unless --no-er) the configs[3]
+ER degree-class sweeps (N=1e7, 4096 replicas), and (unless --no-giant) a few sweeps
 of the C5 partitioned N=1e9 d=6 graph on one rank, preceded by a calibration copy of a known byte count (torch's
 vectorised copy, 16 B per lane) that tools/pmc_parse.py uses to check the
 gfx950 FETCH_SIZE correction (MI355X_MICROARCH.md, HBM section).
@@ -32,6 +33,8 @@ def main():
     ap.add_argument("--giant-n", type=int, default=1_000_000_000)
     ap.add_argument("--no-sa", action="store_true")
     ap.add_argument("--sa-steps", type=int, default=1000)
+    ap.add_argument("--no-er", action="store_true")
+    ap.add_argument("--er-n", type=int, default=10_000_000)
     args = ap.parse_args()
     import torch
     import mjx
@@ -88,6 +91,19 @@ def main():
         torch.cuda.synchronize()
         del sa
         print("pmc_run sa done", flush=True)
+    if not args.no_er:
+        # configs[3]: ER mean degree 5, N=1e7, 4096 replicas: the degree-class
+        # sweeps of bench.py's er leg (2 sweeps + fused count per step)
+        ge = mjx.erdos_renyi_device(args.er_n, 5.0 / (args.er_n - 1), seed=31)
+        ge.class_ell()
+        es = torch.randint(-2 ** 62, 2 ** 62, (args.er_n * W,), dtype=torch.int64, device=dev, generator=gen)
+        eo, et = torch.empty_like(es), torch.empty_like(es)
+        for _ in range(args.reps):
+            counts.zero_()
+            mjx.rollout(ge, es, args.T, words=W, out=eo, tmp=et, counts=counts)
+        torch.cuda.synchronize()
+        del ge, es, eo, et
+        print("pmc_run er done", flush=True)
     if not args.no_giant:
         sh = mjx.ShardedRRG(6, args.giant_n, seed=12345, mode="binned")
         sh.drop_adjacency()
