@@ -18,14 +18,20 @@
 //     after the launch is numpy's (no draw-ahead);
 //   * the change sets C_t of the levels (C_0 = {i flipped}): candidates of
 //     level t are C_{t-1} and its neighbours, one lane each; a candidate's
-//     level-(t-1) inputs come from C_{t-1} (an LDS hash of node -> new value)
-//     or from the cached bit; it joins C_t when the always-stay majority
-//     (code/SA_RRG.py:19-20) differs from its cached level-t bit (inserted
-//     once: the hash dedups);
+//     level-(t-1) inputs are the cached bits XOR the change marks of C_{t-1}
+//     (one 8-byte read per node: level word and mark word side by side; a
+//     node in C_t holds the complement of its cached value); it joins C_t
+//     when the always-stay majority (code/SA_RRG.py:19-20) differs from its
+//     cached level-t bit (the mark's atomicOr dedups repeated candidates);
 //   * sum(s_end(flipped)) - sum(s_end) = sum over C_T of +-2; delta_H in float64
 //     in the reference's operation order (this unit is built with
 //     -ffp-contract=off), Metropolis test, schedule, stop tests;
-//   * an accepted proposal XORs its change sets into the level bit arrays.
+//   * an accepted proposal XORs its change sets into the level bit arrays;
+//     every proposal clears the marks it set (from the lists C_t).
+// Round 3: the round-2 form kept C_t as an LDS hash of node -> new value,
+// probed for every neighbour of every candidate (2-3 dependent LDS reads per
+// probe); marks make every value one read: 5.3 -> see DESIGN.md per step at
+// SA_RRG.py's p = 3, n = 1e4.
 // At the end of the launch the changed level-0 bits go back to the
 // replica-packed configuration s (atomicXor of the replica's bit: the other
 // 63 replicas of a word are other workgroups) and the MT state, a, b, t,
@@ -45,14 +51,11 @@ constexpr size_t kLdsMax = 160 * 1024;
 
 struct Geo {
     int rw;          // uint16 entries per adjacency row (4, 8 or 16)
-    int nw;          // uint32 words per level bit array (even)
+    int nw;          // uint32 bit words per level (even)
     int lc;          // change-list capacity per level (>= the radius-T ball)
-    int hs;          // hash slots per level (power of 2, >= 2 lc)
-    int hshift;      // 32 - log2(hs)
     int off_lev;     // byte offsets into the dynamic LDS
     int off_lev0;
     int off_mt;
-    int off_hash;
     int off_list;
     int off_cnt;
     int bytes;
@@ -77,16 +80,11 @@ static bool geometry(int64_t n, int d, int T, Geo* g) {
     lc = ((lc + 63) / 64) * 64;
     if (lc > 4096) return false;
     g->lc = (int)lc;
-    int hs = 64, lg = 6;
-    while (hs < 2 * lc) { hs *= 2; ++lg; }
-    g->hs = hs;
-    g->hshift = 32 - lg;
     int64_t off = ((int64_t)n * g->rw * 2 + 15) / 16 * 16;
-    g->off_lev = (int)off;   off += (int64_t)(T + 1) * g->nw * 4;
+    g->off_lev = (int)off;   off += (int64_t)(T + 1) * g->nw * 8;     // {level bits, change bits} per word
     g->off_lev0 = (int)off;  off += (int64_t)g->nw * 4;
     g->off_mt = (int)off;    off += MT_N * 4;
-    g->off_hash = (int)off;  off += (int64_t)(T + 1) * hs * 4;
-    g->off_list = (int)off;  off += (int64_t)(T + 1) * lc * 4;
+    g->off_list = (int)off;  off += (int64_t)(T + 1) * g->lc * 4;
     g->off_cnt = (int)off;   off += 16 * 4;
     g->bytes = (int)off;
     return (size_t)off <= kLdsMax;
@@ -103,6 +101,15 @@ __device__ __forceinline__ int64_t wave_sum(int64_t x) {
     return x;
 }
 
+// Level t of the replica is a bit array (bit v = the cached value onestep^t(s)
+// of node v) interleaved word by word with a change-bit array: lv[2(t nw + w)]
+// = level word w, lv[2(t nw + w) + 1] = change word w.  During a proposal the
+// change bits mark C_t, the nodes whose level-t value the flip changes; a
+// changed node's new value is the complement of its cached one (that is what
+// puts it in C_t), so "level t as the proposal sees it" is level XOR change:
+// ONE 8-byte LDS read per node, no hash table.  An accepted proposal XORs the
+// marked bits into the levels; every step clears the marks it set (the lists
+// hold them).
 template <int D>
 __global__ void __launch_bounds__(64) k_sa_lds(const int32_t* __restrict__ adj, int dd, int64_t n, int T, int64_t R,
                                                int64_t W, u64* __restrict__ s, mjx_sa_state st, int64_t nsteps,
@@ -114,15 +121,33 @@ __global__ void __launch_bounds__(64) k_sa_lds(const int32_t* __restrict__ adj, 
     const int64_t r = blockIdx.x;
     const int64_t col = r >> 6;
     const u64 rbit = 1ull << (r & 63);
-    const int nw = geo.nw, rw = geo.rw, hs = geo.hs, lc = geo.lc;
+    const int nw = geo.nw, rw = geo.rw, lc = geo.lc;
     uint16_t* rows = reinterpret_cast<uint16_t*>(smem);
-    uint32_t* lev = reinterpret_cast<uint32_t*>(smem + geo.off_lev);      // level t at lev + t*nw
+    uint32_t* lv = reinterpret_cast<uint32_t*>(smem + geo.off_lev);       // {level, change} word pairs
     uint32_t* lev0s = reinterpret_cast<uint32_t*>(smem + geo.off_lev0);   // level 0 at launch start
     uint32_t* mt = reinterpret_cast<uint32_t*>(smem + geo.off_mt);
-    uint32_t* hsh = reinterpret_cast<uint32_t*>(smem + geo.off_hash);     // level t at hsh + t*hs
-    uint32_t* lst = reinterpret_cast<uint32_t*>(smem + geo.off_list);     // level t at lst + t*lc
+    uint32_t* lst = reinterpret_cast<uint32_t*>(smem + geo.off_list);     // C_t at lst + t*lc
     int* cnts = reinterpret_cast<int*>(smem + geo.off_cnt);
     const int32_t* g = adj + (st.rep_graph ? (int64_t)st.rep_graph[r] : 0) * n * d;
+    auto lword = [&](int t, int w) -> uint32_t& { return lv[2 * (t * nw + w)]; };
+    auto cword = [&](int t, int w) -> uint32_t& { return lv[2 * (t * nw + w) + 1]; };
+    // the value of node v at level t as the current proposal sees it
+    auto seen = [&](int t, int v) -> uint32_t {
+        const uint2 x = *reinterpret_cast<const uint2*>(lv + 2 * (t * nw + (v >> 5)));
+        return ((x.x ^ x.y) >> (v & 31)) & 1u;
+    };
+    // neighbours of v: one 8-byte read for d <= 4
+    auto nbrs = [&](int v, int (&o)[D > 0 ? D : 16]) {
+        if constexpr (D > 0 && D <= 4) {
+            const uint2 x = *reinterpret_cast<const uint2*>(rows + v * 4);
+            o[0] = (int)(x.x & 0xffffu);
+            if constexpr (D > 1) o[1] = (int)(x.x >> 16);
+            if constexpr (D > 2) o[2] = (int)(x.y & 0xffffu);
+            if constexpr (D > 3) o[3] = (int)(x.y >> 16);
+        } else {
+            for (int q = 0; q < d; ++q) o[q] = rows[v * rw + q];
+        }
+    };
 
     // ---- launch setup: rows, level 0, MT state; then levels 1..T by sweeps in LDS
     for (int64_t q = lane; q < n * d; q += 64) {
@@ -135,30 +160,29 @@ __global__ void __launch_bounds__(64) k_sa_lds(const int32_t* __restrict__ adj, 
         const u64 m = __ballot(b);
         if (lane < 2) {
             const uint32_t x = (uint32_t)(m >> (32 * lane));
-            lev[(v0 >> 5) + lane] = x;
+            lword(0, (int)(v0 >> 5) + lane) = x;
             lev0s[(v0 >> 5) + lane] = x;
         }
     }
+    for (int k = lane; k < (T + 1) * nw; k += 64) lv[2 * k + 1] = 0u;
     for (int k = lane; k < MT_N; k += 64) mt[k] = st.mt[r * MT_N + k];
-    for (int k = lane; k < (T + 1) * hs; k += 64) hsh[k] = 0u;
     wave_sync();
-    auto bitof = [&](const uint32_t* L, int v) -> uint32_t { return (L[v >> 5] >> (v & 31)) & 1u; };
     auto maj = [&](int ones, uint32_t own) -> uint32_t {       // always-stay majority (code/SA_RRG.py:19-20)
         return (2 * ones > d) ? 1u : ((2 * ones < d) ? 0u : own);
     };
     for (int t = 1; t <= T; ++t) {
-        const uint32_t* lp = lev + (t - 1) * nw;
-        uint32_t* lt = lev + t * nw;
         for (int64_t v0 = 0; v0 < (int64_t)nw * 32; v0 += 64) {
             const int v = (int)(v0 + lane);
             uint32_t nb = 0;
             if (v < n) {
+                int nv[D > 0 ? D : 16];
+                nbrs(v, nv);
                 int ones = 0;
-                for (int q = 0; q < d; ++q) ones += (int)bitof(lp, rows[v * rw + q]);
-                nb = maj(ones, bitof(lp, v));
+                for (int q = 0; q < d; ++q) ones += (int)seen(t - 1, nv[q]);
+                nb = maj(ones, seen(t - 1, v));
             }
             const u64 m = __ballot(nb != 0);
-            if (lane < 2) lt[(v0 >> 5) + lane] = (uint32_t)(m >> (32 * lane));
+            if (lane < 2) lword(t, (int)(v0 >> 5) + lane) = (uint32_t)(m >> (32 * lane));
         }
         wave_sync();
     }
@@ -172,36 +196,6 @@ __global__ void __launch_bounds__(64) k_sa_lds(const int32_t* __restrict__ adj, 
     const uint32_t rng = (uint32_t)(n - 1);
     uint32_t mask = rng;
     mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
-    auto hslot = [&](int v) -> uint32_t { return ((uint32_t)(v + 1) * 0x9E3779B1u) >> geo.hshift; };
-    // value of node v at level l as the proposal sees it: C_l's new value, else the cached bit
-    auto val_at = [&](int l, int v) -> uint32_t {
-        const uint32_t* H = hsh + l * hs;
-        uint32_t h = hslot(v);
-        for (;;) {
-            const uint32_t e = H[h];
-            if (e == 0u) return bitof(lev + l * nw, v);
-            if ((e >> 1) == (uint32_t)(v + 1)) return e & 1u;
-            h = (h + 1) & (uint32_t)(hs - 1);
-        }
-    };
-    auto hins = [&](int l, int v, uint32_t val) -> bool {     // true: first insert of v at level l
-        uint32_t* H = hsh + l * hs;
-        const uint32_t key = ((uint32_t)(v + 1) << 1) | val;
-        uint32_t h = hslot(v);
-        for (;;) {
-            const uint32_t old = atomicCAS(&H[h], 0u, key);
-            if (old == 0u) return true;
-            if ((old >> 1) == (uint32_t)(v + 1)) return false;
-            h = (h + 1) & (uint32_t)(hs - 1);
-        }
-    };
-    auto next_word = [&]() -> uint32_t {                          // wave-uniform
-        if (idx >= MT_N) {
-            lds_twist(mt, lane);
-            idx = 0;
-        }
-        return mt_temper(mt[idx++]);
-    };
     int64_t k = 0;
     for (; k < nsteps && done == 0; ++k) {
         // randint(low=0, high=n) (code/SA_RRG.py:73): numpy's masked rejection, 64 words per ballot
@@ -227,15 +221,24 @@ __global__ void __launch_bounds__(64) k_sa_lds(const int32_t* __restrict__ adj, 
                 idx += (MT_N - idx < 64) ? MT_N - idx : 64;
             }
         }
-        // rand() (code/SA_RRG.py:76)
-        const uint32_t w1 = next_word();
-        const uint32_t w2 = next_word();
+        // rand() (code/SA_RRG.py:76): two consecutive words, one read when no twist falls between
+        uint32_t w1, w2;
+        if (idx + 1 < MT_N) {
+            w1 = mt_temper(mt[idx]);
+            w2 = mt_temper(mt[idx + 1]);
+            idx += 2;
+        } else {
+            if (idx >= MT_N) { lds_twist(mt, lane); idx = 0; }
+            w1 = mt_temper(mt[idx++]);
+            if (idx >= MT_N) { lds_twist(mt, lane); idx = 0; }
+            w2 = mt_temper(mt[idx++]);
+        }
         const double u = mt_double(w1, w2);
-        // level 0: i flipped
-        const uint32_t old_i = bitof(lev, iv);
+        // level 0: C_0 = {i}
+        const uint32_t old_i = (lword(0, iv >> 5) >> (iv & 31)) & 1u;
         if (lane == 0) {
-            hsh[hslot(iv)] = ((uint32_t)(iv + 1) << 1) | (old_i ^ 1u);     // empty table: the home slot
-            lst[0] = (uint32_t)iv | ((old_i ^ 1u) << 31);
+            cword(0, iv >> 5) |= 1u << (iv & 31);
+            lst[0] = (uint32_t)iv;
             cnts[0] = 1;
         }
         wave_sync();
@@ -250,18 +253,23 @@ __global__ void __launch_bounds__(64) k_sa_lds(const int32_t* __restrict__ adj, 
                 const int q = base + lane;
                 bool add = false;
                 int cand = 0;
-                uint32_t nb = 0;
                 if (q < m) {
                     const int slot = q / (d + 1), j = q - slot * (d + 1);
-                    const int v = (int)(prev[slot] & 0x7fffffffu);
+                    const int v = (int)prev[slot];
                     cand = (j == 0) ? v : (int)rows[v * rw + j - 1];
+                    int nv[D > 0 ? D : 16];
+                    nbrs(cand, nv);
                     int ones = 0;
-                    for (int e = 0; e < d; ++e) ones += (int)val_at(l - 1, rows[cand * rw + e]);
-                    nb = maj(ones, val_at(l - 1, cand));
-                    if (nb != bitof(lev + l * nw, cand)) add = hins(l, cand, nb);
+                    for (int e = 0; e < d; ++e) ones += (int)seen(l - 1, nv[e]);
+                    const uint32_t nb = maj(ones, seen(l - 1, cand));
+                    const uint32_t bit = 1u << (cand & 31);
+                    if (nb != ((lword(l, cand >> 5) >> (cand & 31)) & 1u)) {
+                        // first mark of cand at level l (candidates repeat)
+                        add = (atomicOr(&cword(l, cand >> 5), bit) & bit) == 0u;
+                    }
                 }
                 const u64 bal = __ballot(add);
-                if (add) cur[nc + __popcll(bal & ((1ull << lane) - 1ull))] = (uint32_t)cand | (nb << 31);
+                if (add) cur[nc + __popcll(bal & ((1ull << lane) - 1ull))] = (uint32_t)cand;
                 nc += __popcll(bal);
             }
             if (lane == 0) cnts[l] = nc;
@@ -269,10 +277,14 @@ __global__ void __launch_bounds__(64) k_sa_lds(const int32_t* __restrict__ adj, 
             if (nc == 0) break;
             last = l;
         }
+        // sum(s_end(flipped)) - sum(s_end): every node of C_T turned to its complement
         int64_t ds = 0;
         if (last == T) {
             const uint32_t* lt = lst + T * lc;
-            for (int q = lane; q < cnts[T]; q += 64) ds += (lt[q] >> 31) ? 2 : -2;
+            for (int q = lane; q < cnts[T]; q += 64) {
+                const int v = (int)lt[q];
+                ds += ((lword(T, v >> 5) >> (v & 31)) & 1u) ? -2 : 2;
+            }
             ds = wave_sum(ds);
         }
         const int64_t sum_new = sum_end + ds;
@@ -285,16 +297,17 @@ __global__ void __launch_bounds__(64) k_sa_lds(const int32_t* __restrict__ adj, 
         const double prob = (e < 1.0) ? e : 1.0;                    // (code/SA_RRG.py:75)
         const bool acc = u < prob;                                  // (code/SA_RRG.py:76)
         if (e < 1.0 && fabs(u - e) <= 4.0 * (nextafter(e, 2.0) - e)) ++ties;
-        if (acc) {                                                  // (code/SA_RRG.py:77)
-            for (int l = 0; l <= last; ++l) {
-                const uint32_t* cl = lst + l * lc;
-                for (int q = lane; q < cnts[l]; q += 64) {
-                    const uint32_t v = cl[q] & 0x7fffffffu;
-                    atomicXor(&lev[l * nw + (v >> 5)], 1u << (v & 31));
-                }
+        // accepted (code/SA_RRG.py:77): marked bits into the levels; always: clear the marks
+        for (int l = 0; l <= last; ++l) {
+            const uint32_t* cl = lst + l * lc;
+            for (int q = lane; q < cnts[l]; q += 64) {
+                const int v = (int)cl[q];
+                const uint32_t bit = 1u << (v & 31);
+                if (acc) atomicXor(&lword(l, v >> 5), bit);
+                atomicAnd(&cword(l, v >> 5), ~bit);
             }
-            sum_end = sum_new;
         }
+        if (acc) sum_end = sum_new;
         if (a < a_cap) a = par_a * a;                               // (code/SA_RRG.py:80-81)
         if (b < b_cap) b = par_b * b;
         t += 1;                                                     // (code/SA_RRG.py:82)
@@ -306,9 +319,6 @@ __global__ void __launch_bounds__(64) k_sa_lds(const int32_t* __restrict__ adj, 
             if (st.tr_sum) st.tr_sum[k * R + r] = sum_end;
             if (st.tr_dE) st.tr_dE[k * R + r] = dE;
         }
-        // empty the hash levels this step used (a level past `last` got no insert)
-        for (int l = 0; l <= last + 1 && l <= T; ++l)
-            for (int q = lane; q < hs; q += 64) hsh[l * hs + q] = 0u;
         wave_sync();
     }
     // steps of this launch after the replica finished
@@ -323,7 +333,7 @@ __global__ void __launch_bounds__(64) k_sa_lds(const int32_t* __restrict__ adj, 
     // ---- write back: changed configuration bits, the stream, the replica state
     for (int64_t v0 = 0; v0 < n; v0 += 64) {
         const int v = (int)(v0 + lane);
-        if (v < n && (bitof(lev, v) ^ bitof(lev0s, v)))
+        if (v < n && (((lword(0, v >> 5) ^ lev0s[v >> 5]) >> (v & 31)) & 1u))
             atomicXor((unsigned long long*)&s[(int64_t)v * W + col], (unsigned long long)rbit);
     }
     for (int q = lane; q < MT_N; q += 64) st.mt[r * MT_N + q] = mt[q];

@@ -189,8 +189,18 @@ class SAReplicas:
         if layout not in ("auto", "lds", "cone", "rec", "levels"):
             raise ValueError(f"unknown light-cone layout {layout!r}")
         lds_fits = 0 < _lib.load().mjx_sa_lds_bytes(n, self.d, self.p, self.c) <= 160 * 1024
+        # the speculative batches (k_sa_spec: d=3 at p+c-1 <= 2, d=4 at p+c-1 = 1) beat the
+        # LDS-resident kernel where they apply (configs[0] at d=4, p=c=1: 1.5 vs 2.7 us per
+        # step); the record layout is 2-3 % faster than the plain cone for one shared graph
+        # (configs[1]: 4.31 -> 4.20 us per step at R = 4096, same box)
+        spec = (self.d == 3 and T <= 2) or (self.d == 4 and T == 1)
         if layout == "auto":
-            layout = "lds" if lds_fits else "cone"
+            if spec and self.rep_graph is None:
+                layout = "rec"
+            elif lds_fits and not spec:
+                layout = "lds"
+            else:
+                layout = "cone"
         if mode == "lightcone" and layout == "lds" and not lds_fits:
             raise ValueError(f"LDS-resident SA unsupported for n={n}, d={self.d}, p+c-1={T}")
         if mode == "lightcone" and layout == "rec" and (self.rep_graph is not None or

@@ -95,7 +95,7 @@ def test_sa_lightcone_levels_stay_consistent(mjx_mod, d, p, c):
     (d = 3, 4, 6: batched-load evaluation; d = 5: the generic one)."""
     n = 2000
     adj = mjx_mod.random_regular_graph(d, n, seed=9)
-    sa = mjx_mod.SAReplicas(adj, p, c, list(range(130)), mode="lightcone")
+    sa = mjx_mod.SAReplicas(adj, p, c, list(range(130)), mode="lightcone", layout="cone")
     sa.steps(3000)
     W = sa.W
     g = mjx_mod.Graph.ell(adj)
@@ -185,7 +185,7 @@ def test_sa_lightcone_wave_split_is_bit_exact(mjx_mod, split):
     schedule: the accept sequences equal the oracle's."""
     n, d, p, c = 400, 3, 2, 1
     adj = mjx_mod.random_regular_graph(d, n, seed=5)
-    sa = mjx_mod.SAReplicas(adj, p, c, list(range(70)), mode="lightcone",
+    sa = mjx_mod.SAReplicas(adj, p, c, list(range(70)), mode="lightcone", layout="cone",
                             kernel={"split": int(split), "no_spec": True, "no_cone2": True})
     tr = {k: v.cpu().numpy() for k, v in sa.steps(300, trace=True).items()}
     for r in (0, 5, 63, 64, 69):

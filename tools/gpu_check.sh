@@ -34,10 +34,10 @@ for s in $STEPS; do
       stop_if_fatal $? prof ;;
     pmc)
       R="$GRAFT_REPO_ROOT"
-      ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE \
+      ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE \
           -d "$R/$OUT/pmc_fetch" -o run --output-format csv -- python3 "$R/tools/pmc_run.py" ) > $OUT/pmc_fetch.log 2>&1
       stop_if_fatal $? pmc_fetch
-      ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE \
+      ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE \
           -d "$R/$OUT/pmc_write" -o run --output-format csv -- python3 "$R/tools/pmc_run.py" ) > $OUT/pmc_write.log 2>&1
       stop_if_fatal $? pmc_write
       python3 tools/pmc_parse.py $OUT/pmc_fetch $OUT/pmc_write $((1024*1024*1024)) $OUT/pmc_traffic.json > $OUT/pmc_parse.log 2>&1
@@ -45,7 +45,7 @@ for s in $STEPS; do
     sq)
       # compute-side counters (one SQ pass: 8 SQ + 1 GRBM) over the HPR / SA / sweep workload
       R="$GRAFT_REPO_ROOT"
-      ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+      ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
           SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE \
           -d "$R/$OUT/pmc_sq" -o run --output-format csv -- python3 "$R/tools/pmc_run.py" --no-giant --no-er ) > $OUT/pmc_sq.log 2>&1
       stop_if_fatal $? pmc_sq ;;
