@@ -18,7 +18,7 @@ STEPS="${STEPS:-tests bench prof}"
 for s in $STEPS; do
   case $s in
     tests)
-      timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+      timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest ${PYTEST_PATHS:-tests} -m gpu -x -v --timeout 300 --timeout-method thread \
         ${PYTEST_ARGS:-} > $OUT/pytest_gpu.log 2>&1
       stop_if_fatal $? tests ;;
     smoke)
@@ -30,7 +30,7 @@ for s in $STEPS; do
     prof)
       ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats \
           -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run --output-format csv -- \
-          python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline ${BENCH_ARGS:-} ) > $OUT/prof.log 2>&1
+          python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline ${PROF_ARGS:-${BENCH_ARGS:-}} ) > $OUT/prof.log 2>&1
       stop_if_fatal $? prof ;;
     pmc)
       R="$GRAFT_REPO_ROOT"
