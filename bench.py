@@ -485,8 +485,11 @@ def bench_er(args, rank, world, dist, dev):
         "layout": "degree-class ELL, one launch per degree class (nb:113-117)",
         "ms_per_step": 1e3 * el / K,
         "node_updates_per_s": world * n * R * T * K / el,
+        "algorithmic_bytes_per_sweep": bytes_per_sweep,
         "algorithmic_GBps_per_gpu": bytes_per_sweep * T * K / el / 1e9,
         "frac_of_hbm_peak": bytes_per_sweep * T * K / el / 1e9 / HBM_PEAK_GBS,
+        # measured HBM bytes (rocprofv3 PMC FETCH/WRITE passes, same graph and replica count)
+        "traffic": er_sweep_traffic(),
     }
 
 
@@ -544,6 +547,73 @@ def bench_bdcm(args, rank, world, dist, dev):
         res["cpu_ms_per_iter"] = 1e3 * (time.perf_counter() - t0) / reps
         res["cpu_kind"] = "port (oracle/bdcm.py numpy restatement, 1 core)"
     return res
+
+
+FP32_VECTOR_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: the FP32 vector (= FP32 matrix) peak
+
+
+def hpr_dp_flops(d, p, c):
+    """Algorithmic FLOPs of one HPr_dp message update (all valid x_a of the
+    message, attr_value = +1), counted the way the kernel evaluates the DP
+    (csrc/mjx_hpr_impl.h xa_messages; code/HPR_pytorch_RRG.py:183-218):
+    bias x chi for the d-1 incoming rows, the count-table convolution of
+    incoming neighbours 1..d-3 into neighbour 0's table (one multiply, then
+    FMAs), the directional cumulative sums (one add per entry with a
+    successor in each of the T dimensions), and the fold of the last incoming
+    row (an FMA per non-empty corner, the weight and the row sum).  The
+    corner rule restates corner() of the kernel."""
+    T = p + c
+    X, K = 1 << T, d - 2
+    base = K + 1
+    NS = base ** T
+
+    def spin(x, t):
+        return -1 if (x >> (T - 1 - t)) & 1 else 1
+
+    def corner_ok(XA, x, XB):
+        for t in range(T):
+            s = spin(XA, t + 1) if t < T - 1 else spin(XA, p)
+            prev = spin(XA, t) if t < T - 1 else spin(XA, T - 1)
+            b, y = (1 if spin(x, t) > 0 else 0), spin(XB, t)
+            if s > 0:
+                lo = -((-(d - 1 - y + (0 if prev > 0 else 1))) // 2) - b
+                if lo > K:
+                    return False
+            else:
+                hi = (d - 1 - y + (0 if prev < 0 else -1)) // 2 - b
+                if hi < 0:
+                    return False
+        return True
+
+    def maxdigit(i):
+        return max((i // base ** (T - 1 - t)) % base for t in range(T))
+
+    total = 0
+    for XA in range(0, X, 2):                      # x_a[T-1] = +1
+        f = (d - 1) * X
+        for j in range(1, K):
+            f += sum(2 * X - 1 for i in range(NS) if maxdigit(i) <= j)
+        f += T * (NS // base) * K
+        f += sum(2 for x in range(X) for xb in range(X) if corner_ok(XA, x, xb)) + 2 * X
+        total += f
+    return total
+
+
+def sq_counters(kernel_prefix):
+    """wait / VALU-active fractions of a kernel from the committed SQ counter
+    pass (profiles/r03_sq_counters.json, tools/pmc_sq_parse.py), or None."""
+    path = os.path.join(ROOT, "profiles", "r03_sq_counters.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    for k, v in d.items():
+        if k.startswith("_") or kernel_prefix not in k:
+            continue
+        return {"kernel": k, "wait_frac": v.get("wait_frac"), "valu_active_frac": v.get("valu_active_frac"),
+                "source": "profiles/r03_sq_counters.json (a pass before the round-3 no-SLP build)"}
+    return None
 
 
 def bench_hpr(args, rank, world, dist, dev):
@@ -642,6 +712,11 @@ def bench_hpr(args, rank, world, dist, dev):
         "hpr_dp_frac_of_hbm_peak": qbytes / (upd_q / 1e3) / 1e9 / HBM_PEAK_GBS,
         "hpr_dp_traffic_bytes": rocprof_traffic("k_hpr_update_pipe_q"),
         "marginals_edge_z_traffic_bytes": rocprof_traffic("k_hpr_edge_z_q")}
+    # the compute side of the same launch (the DP is a mixed contraction)
+    fl = msgs * hpr_dp_flops(d, p, c)
+    res["loop_state_q"]["hpr_dp_compute"] = {
+        "flops_per_launch": fl, "achieved_tflops": fl / (upd_q / 1e3) / 1e12, "peak_tflops": FP32_VECTOR_PEAK_TFLOPS,
+        "frac": fl / (upd_q / 1e3) / 1e12 / FP32_VECTOR_PEAK_TFLOPS, "sq": sq_counters("k_hpr_update_pipe_q")}
     # the whole loop iteration of code/HPR_pytorch_RRG.py:344-356 (update,
     # marginals, bias refresh, trial configuration, majority check) in
     # hipGraph-replayed batches of 16 with one host read per batch
@@ -751,6 +826,22 @@ def rocprof_traffic(kernel_prefix="k_sweep_ell_rp"):
         return d.get(kernel_prefix, {}).get("bytes_per_launch")
     except (OSError, ValueError):
         return None
+
+
+def er_sweep_traffic():
+    """Measured HBM bytes of one ER step (one plain + one counting degree-class
+    sweep, every class launch summed) from profiles/pmc_traffic.json, whose
+    ER pass (tools/pmc_run.py) runs the bench's own graph (N=1e7, mean degree
+    5, seed 31) and replica count; None if absent."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    plain = sum(v["bytes_per_launch"] for k, v in d.items() if k.startswith("mjx::k_sweep_cls") and "false" in k)
+    count = sum(v["bytes_per_launch"] for k, v in d.items() if k.startswith("mjx::k_sweep_cls") and "true" in k)
+    return {"plain_sweep_bytes": plain, "counting_sweep_bytes": count} if plain and count else None
 
 
 def main():
