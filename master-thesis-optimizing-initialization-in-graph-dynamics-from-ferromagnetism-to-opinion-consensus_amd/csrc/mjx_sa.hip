@@ -23,6 +23,7 @@
 #include <math.h>
 #include <stdlib.h>
 #include <algorithm>
+#include <type_traits>
 
 #pragma clang fp contract(off)
 
@@ -1362,8 +1363,18 @@ __global__ void __launch_bounds__(64) k_sa_cone2(const int32_t* __restrict__ adj
 // (Two-hop adjacency records -- a node's row and its neighbours' rows in one
 // line -- measured no faster: the 16 MB adjacency is served on-die.)
 // ---------------------------------------------------------------------------
-constexpr int SPEC_LDS = 16384;  // bytes of hash sets per wave: 64 * K slots per replica (<= K * 18 keys)
+constexpr int SPEC_LDS = 16384 + 256;  // bytes of hash sets per wave: 64 * K slots per replica (<= K * 18
+                                       // keys), then a dummy insert word per lane
 
+// Diagnostic build only (-DMJX_SA_PROF, tools/sa_prof.py): per-phase s_memtime
+// cycles of k_sa_spec summed over waves; every stamp drains the wave's memory
+// counters first, so a phase's exposed latency is charged to that phase.
+#ifdef MJX_SA_PROF
+__device__ unsigned long long mjx_sa_prof[8];
+#define SA_STAMP(k) do { __builtin_amdgcn_sched_barrier(0); asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); const unsigned long long _c = __builtin_amdgcn_s_memtime(); _acc[k] += _c - _t0; _t0 = _c; __builtin_amdgcn_sched_barrier(0); } while (0)
+#else
+#define SA_STAMP(k) do {} while (0)
+#endif
 template <int D, int TT, int K>
 __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj, const int4* __restrict__ adj_pad,
                                                 int64_t n, int64_t R, int64_t W, LcLevels L, mjx_sa_state st,
@@ -1431,8 +1442,17 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
             h = (h + 1) & (SPEC_HS - 1);
         }
     };
-    auto hearlier = [&](int32_t v) -> bool {                 // an earlier proposal may write v
-        uint32_t h = hslot(v);
+    // the probe loops past a first slot held by another node (rare: ~40 keys in 512 slots)
+    auto hins_from = [&](int32_t v, uint32_t h) {
+        const uint32_t key = ((uint32_t)v << KB) | (uint32_t)k;
+        for (;;) {
+            const uint32_t old = atomicCAS(&htab[h], 0xffffffffu, key);
+            if (old == 0xffffffffu) return;
+            if ((old >> KB) == (uint32_t)v) { atomicMin(&htab[h], key); return; }
+            h = (h + 1) & (SPEC_HS - 1);
+        }
+    };
+    auto hearlier_from = [&](int32_t v, uint32_t h) -> bool {  // an earlier proposal may write v
         for (;;) {
             const uint32_t e = htab[h];
             if (e == 0xffffffffu) return false;
@@ -1440,6 +1460,58 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
             h = (h + 1) & (SPEC_HS - 1);
         }
     };
+    // N nodes at once, branch-free: every first-slot probe issued before any
+    // result is used (one LDS round trip for the group instead of one per
+    // node), results combined by selects; the probe loops run only where a
+    // first slot holds another node (rare: ~40 keys in 512 slots).  Masked-off
+    // entries probe slot 0 (reads) or the lane's own dummy word (inserts).
+    uint32_t* hdummy = lc_lists + hoff + (64 / K) * SPEC_HS + lane;
+    auto hins_n = [&](const int32_t* vv, const bool* mm, auto nn) {
+        constexpr int N = decltype(nn)::value;
+        uint32_t old[N];
+#pragma unroll
+        for (int q = 0; q < N; ++q) {
+            uint32_t* a = mm[q] ? &htab[hslot(vv[q])] : hdummy;
+            old[q] = atomicCAS(a, 0xffffffffu, ((uint32_t)vv[q] << KB) | (uint32_t)k);
+        }
+        bool more = false;
+#pragma unroll
+        for (int q = 0; q < N; ++q) more |= mm[q] && old[q] != 0xffffffffu;
+        if (more) {                       // the node is there already (min tag), or another node is
+#pragma unroll
+            for (int q = 0; q < N; ++q) {
+                if (!mm[q] || old[q] == 0xffffffffu) continue;
+                const uint32_t h = hslot(vv[q]);
+                if ((old[q] >> KB) == (uint32_t)vv[q]) atomicMin(&htab[h], ((uint32_t)vv[q] << KB) | (uint32_t)k);
+                else hins_from(vv[q], (h + 1) & (SPEC_HS - 1));
+            }
+        }
+    };
+    auto hearlier_n = [&](const int32_t* vv, const bool* mm, auto nn) -> bool {
+        constexpr int N = decltype(nn)::value;
+        uint32_t e[N];
+#pragma unroll
+        for (int q = 0; q < N; ++q) e[q] = htab[mm[q] ? hslot(vv[q]) : 0u];
+        bool hit = false, slow = false;
+#pragma unroll
+        for (int q = 0; q < N; ++q) {
+            const bool occ = mm[q] && e[q] != 0xffffffffu;
+            const bool same = (e[q] >> KB) == (uint32_t)vv[q];
+            hit |= occ && same && (e[q] & (uint32_t)(K - 1)) < (uint32_t)k;
+            slow |= occ && !same;
+        }
+        if (slow) {
+#pragma unroll
+            for (int q = 0; q < N; ++q) {
+                if (!mm[q] || e[q] == 0xffffffffu || (e[q] >> KB) == (uint32_t)vv[q]) continue;
+                hit |= hearlier_from(vv[q], (hslot(vv[q]) + 1) & (SPEC_HS - 1));
+            }
+        }
+        return hit;
+    };
+#ifdef MJX_SA_PROF
+    unsigned long long _acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, _t0 = __builtin_amdgcn_s_memtime();
+#endif
     for (;;) {
         const bool going = live && done == 0 && pos < nsteps;
         if (!__any(going)) break;
@@ -1449,6 +1521,7 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
             reinterpret_cast<uint4*>(lc_lists + hoff)[q] = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
+        SA_STAMP(5);
         const int64_t kk = pos + k;
         const bool mine = going && kk < nsteps;
         int32_t i = 0;
@@ -1486,6 +1559,7 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
                     for (int x2 = 0; x2 < D; ++x2)
                         if (m2 > m || x2 > x) ok &= (A1[m2][x2] == i) || (A1[m2][x2] != cc);
             }
+        SA_STAMP(0);
         int old_i = 0;
         int64_t ds = 0;
         uint32_t ch1 = 0, nv1 = 0, ch2 = 0;      // positions: 0 = i, 1+m = a_m, 1+D+m*D+x = child
@@ -1529,6 +1603,7 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
                 const uint32_t nb = maj(ones, bv(wa[m][0]));
                 if (nb != bv(wa[m][1])) { ch1 |= 2u << m; nv1 |= nb << (1 + m); }
             }
+            SA_STAMP(1);
             if constexpr (TT == 1) {
                 // T = 1: the sum over the level-1 changes (lc_tree2)
                 int64_t acc = 0;
@@ -1588,45 +1663,75 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
             if (simple) ds = lc_delta_mlp<D, true>(adj, NS, colo, bit, T, L, lists, i, cnt, &old_i, A0, A1);
             else ds = lc_delta_mlp<D, false>(adj, NS, colo, bit, T, L, lists, i, cnt, &old_i, A0, A1);
         }
+        SA_STAMP(2);
         // potential writes of every proposal into the replica's hash set
-        if (mine && (ok || listpath)) {
+        constexpr int NTW = 1 + D + D * D;                  // tree positions: i, the a_m, their children
+        if (mine && listpath) {
             hins(i);
-            if (listpath) {
 #pragma unroll
-                for (int lv = 1; lv <= T; ++lv)
-                    for (int q = 0; q < cnt[lv]; ++q) hins((int32_t)(lists[(L.off[lv] + q) * 64] & 0x7fffffffu));
-            } else {
-                const uint32_t chg = ch1 | ch2;
-#pragma unroll
-                for (int m = 0; m < D; ++m) {
-                    if ((chg >> (1 + m)) & 1u) hins(A0[m]);
-#pragma unroll
-                    for (int x = 0; x < D; ++x)
-                        if ((ch2 >> (1 + D + m * D + x)) & 1u) hins(A1[m][x]);
-                }
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        // does an earlier proposal of the batch write a node this one read?
-        bool stands = mine && (ok || listpath);
-        if (stands && k > 0) {
-            bool hit = hearlier(i);
+            for (int lv = 1; lv <= T; ++lv)
+                for (int q = 0; q < cnt[lv]; ++q) hins((int32_t)(lists[(L.off[lv] + q) * 64] & 0x7fffffffu));
+        } else if (mine && ok) {
+            const uint32_t chg = ch1 | ch2;
+            int32_t wv[NTW];
+            bool wm[NTW];
+            wv[0] = i;
+            wm[0] = true;
 #pragma unroll
             for (int m = 0; m < D; ++m) {
-                hit |= hearlier(A0[m]);
+                wv[1 + m] = A0[m];
+                wm[1 + m] = (chg >> (1 + m)) & 1u;
 #pragma unroll
                 for (int x = 0; x < D; ++x) {
-                    if (A1[m][x] == i) continue;
-                    hit |= hearlier(A1[m][x]);
-                    if (TT == 1 || listpath || !((ch1 >> (1 + m)) & 1u)) continue;   // grandchildren read only here
+                    wv[1 + D + m * D + x] = A1[m][x];
+                    wm[1 + D + m * D + x] = (ch2 >> (1 + D + m * D + x)) & 1u;
+                }
+            }
+            hins_n(wv, wm, std::integral_constant<int, NTW>{});
+        }
+        SA_STAMP(6);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        SA_STAMP(7);
+        // does an earlier proposal of the batch write a node this one read?
+        // (k > 0 lanes are tree balls: a list-path ball stands only as k = 0)
+        bool stands = mine && (ok || listpath);
+        if (stands && k > 0) {
+            int32_t rv[NTW];
+            bool rm[NTW];
+            rv[0] = i;
+            rm[0] = true;
 #pragma unroll
-                    for (int y = 0; y < D; ++y)
-                        if (C[m][x][y] != A0[m]) hit |= hearlier(C[m][x][y]);
+            for (int m = 0; m < D; ++m) {
+                rv[1 + m] = A0[m];
+                rm[1 + m] = true;
+#pragma unroll
+                for (int x = 0; x < D; ++x) {
+                    rv[1 + D + m * D + x] = A1[m][x];
+                    rm[1 + D + m * D + x] = A1[m][x] != i;
+                }
+            }
+            bool hit = hearlier_n(rv, rm, std::integral_constant<int, NTW>{});
+            if constexpr (TT == 2) {
+                // the grandchildren, read only under the neighbours that changed at level 1
+#pragma unroll
+                for (int m = 0; m < D; ++m) {
+                    if (!((ch1 >> (1 + m)) & 1u)) continue;
+                    int32_t gv[D * D];
+                    bool gm[D * D];
+#pragma unroll
+                    for (int x = 0; x < D; ++x)
+#pragma unroll
+                        for (int y = 0; y < D; ++y) {
+                            gv[x * D + y] = C[m][x][y];
+                            gm[x * D + y] = A1[m][x] != i && C[m][x][y] != A0[m];
+                        }
+                    hit |= hearlier_n(gv, gm, std::integral_constant<int, D * D>{});
                 }
             }
             stands = !hit;
         }
+        SA_STAMP(3);
         // resolution: J0 = first proposal that does not stand
         const int gs = g * K;
         const uint32_t nst = (uint32_t)((__ballot(!stands) >> gs) & GM);
@@ -1705,7 +1810,12 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
+        SA_STAMP(4);
     }
+#ifdef MJX_SA_PROF
+    if (threadIdx.x == 0)
+        for (int q = 0; q < 8; ++q) atomicAdd(&mjx_sa_prof[q], _acc[q]);
+#endif
     // steps of this launch after the replica finished
     if (live && (st.tr_i || st.tr_acc || st.tr_sum || st.tr_dE)) {
         for (int64_t q = pos + k; q < nsteps; q += K) {
@@ -2154,3 +2264,14 @@ extern "C" int mjx_sa_rec_steps(const int32_t* adj, const int32_t* adj_pad, int6
     L.lo = 2;
     return lc_steps(adj, adj_pad, n, d, T, R, L, stp, nsteps, par_a, par_b, a_cap, b_cap, t_cap, stream);
 }
+
+#ifdef MJX_SA_PROF
+extern "C" int mjx_sa_prof_read(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mjx_sa_prof), 8 * sizeof(unsigned long long)) != hipSuccess) return MJX_EHIP;
+    if (reset) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(mjx_sa_prof), z, sizeof(z)) != hipSuccess) return MJX_EHIP;
+    }
+    return MJX_OK;
+}
+#endif
