@@ -484,7 +484,7 @@ class HPRState:
 
 def hpr_run(d, n, p, c, damppar=0.4, attr_value=1, lmbd_in=None, pie=0.3, gamma=0.1, TT=10000, edges=None,
             nbrs=None, seed=0, dtype=torch.float32, chi0=None, biases0=None, generator=None, batch=16, graph=True,
-            layout=None, rng="device"):
+            layout=None, rng="device", init_generator=None):
     """The HPR experiment of code/HPR_pytorch_RRG.py:224-377 for one graph.
 
     Randomness follows the reference: with ``generator`` a torch CPU generator
@@ -498,6 +498,12 @@ def hpr_run(d, n, p, c, damppar=0.4, attr_value=1, lmbd_in=None, pie=0.3, gamma=
     continues the generator's stream on the device beside the iterations
     (mjx_hpr_refresh_masks, bit-identical uniforms), "host" draws torch.rand
     on the CPU while the previous batch runs.
+    ``init_generator``: the generator chi0 and biases0 are drawn from
+    (default ``generator``).  The reference draws them with
+    ``device=device`` (:102, :334), i.e. on a GPU box from torch's CUDA
+    generator, and only the per-iteration rand(n) (:142) from the CPU one:
+    pass a ``torch.Generator("cuda")`` to make those same draws, in the same
+    order (chi0 first, :331), on the device.
     Returns the np.savez keys of :377 (mag_reached, conf, num_steps, graphs).
     """
     from .graph import random_regular_edges
@@ -507,11 +513,12 @@ def hpr_run(d, n, p, c, damppar=0.4, attr_value=1, lmbd_in=None, pie=0.3, gamma=
     if generator is None:
         generator = torch.Generator().manual_seed(int(seed))
     nc = 4 ** (p + c)
-    if chi0 is None:
-        chi0 = torch.rand((2 * plan.E, nc), dtype=torch.float64, generator=generator)
+    ig = generator if init_generator is None else init_generator
+    if chi0 is None:                                       # mes_init_mat, code/HPR_pytorch_RRG.py:101-103
+        chi0 = torch.rand((2 * plan.E, nc), dtype=torch.float64, device=ig.device, generator=ig)
         chi0 = chi0 / torch.sum(chi0, axis=1, keepdims=True)
-    if biases0 is None:
-        biases0 = torch.rand((n, 2), dtype=torch.float64, generator=generator)
+    if biases0 is None:                                    # code/HPR_pytorch_RRG.py:334-335
+        biases0 = torch.rand((n, 2), dtype=torch.float64, device=ig.device, generator=ig)
         biases0 = biases0 / torch.sum(biases0, axis=1, keepdims=True)
     st = HPRState(plan, p, c, chi0, biases0, dtype=dtype, damppar=damppar, attr_value=attr_value,
                   lmbd_in=lmbd_in, pie=pie, gamma=gamma, layout=layout)

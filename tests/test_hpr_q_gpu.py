@@ -246,3 +246,27 @@ def test_hpr_run_device_rng_equals_host_rng(mjx_mod):
     assert out[0][0]["num_steps"][0] == out[1][0]["num_steps"][0]
     assert np.array_equal(out[0][0]["conf"], out[1][0]["conf"])
     assert torch.equal(out[0][1], out[1][1])
+
+
+def test_hpr_run_initial_state_from_the_cuda_generator(mjx_mod):
+    """The reference draws chi0 and the biases with device=device
+    (code/HPR_pytorch_RRG.py:102,334): on a GPU box torch's CUDA generator,
+    chi0 first.  hpr_run(init_generator=cuda generator) makes those draws in
+    that order: same run as the explicitly drawn initial state, and the CUDA
+    generator left at the same offset."""
+    n, d, p, c = 200, 4, 1, 1
+    edges = mjx_mod.random_regular_edges(d, n, seed=3)
+    E = n * d // 2
+    gi = torch.Generator("cuda").manual_seed(21)
+    res = mjx_mod.hpr_run(d, n, p, c, TT=60, edges=edges, dtype=torch.float64,
+                          generator=torch.Generator().manual_seed(4), init_generator=gi)
+    gj = torch.Generator("cuda").manual_seed(21)
+    chi = torch.rand((2 * E, 4 ** (p + c)), dtype=torch.float64, device="cuda", generator=gj)
+    chi = chi / torch.sum(chi, axis=1, keepdims=True)
+    b = torch.rand((n, 2), dtype=torch.float64, device="cuda", generator=gj)
+    b = b / torch.sum(b, axis=1, keepdims=True)
+    ref = mjx_mod.hpr_run(d, n, p, c, TT=60, edges=edges, dtype=torch.float64,
+                          generator=torch.Generator().manual_seed(4), chi0=chi, biases0=b)
+    assert res["num_steps"][0] == ref["num_steps"][0]
+    assert np.array_equal(res["conf"], ref["conf"])
+    assert torch.equal(torch.rand(7, device="cuda", generator=gi), torch.rand(7, device="cuda", generator=gj))
