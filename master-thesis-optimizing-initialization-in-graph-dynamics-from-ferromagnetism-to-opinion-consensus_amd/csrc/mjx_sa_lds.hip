@@ -348,6 +348,385 @@ __global__ void __launch_bounds__(64) k_sa_lds(const int32_t* __restrict__ adj, 
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// Latency form for d <= 4 (k_sa_lds_fast<D, T>): the same LDS image and the
+// same change sets, but a proposal's step is a chain of few LDS round trips.
+// One wave serves one replica, so a step IS its chain of dependent LDS
+// accesses (k_sa_lds: ~20 at p = 3 -- list and count reads after every
+// level, a mark for C_0, the stream words read per draw).  Here:
+//   * proposals are parsed 64 stream words at a time: every lane tempers one
+//     word, one ballot marks the randint-acceptable ones, and a scalar scan
+//     (first set bit, two readlanes for rand()'s words) cuts the window into
+//     up to 21 (i, u) pairs kept one per lane -- ~1/17 of a round trip per
+//     proposal; a pair that would cross a twist is drawn serially; the stream
+//     index handed back is the end of the last proposal consumed, numpy's;
+//   * C_0 = {i} needs no mark: level-0 values are read as cached bit XOR
+//     (v == i);
+//   * C_t lives in lanes (candidate + a ballot mask): the candidates of level
+//     t+1 are gathered from the member lanes by ds_bpermute (no LDS list, no
+//     count read), the members' neighbour rows come along (read at level t);
+//     marks dedup repeated candidates by the atomicOr's return, as before;
+//   * sum(s_end) changes by a wave reduction over the lanes of C_T, and the
+//     clears / accepted XORs are issued from the same lanes.
+// A level whose candidates exceed one wave (|C_{t-1}| (d+1) > 64) falls back
+// to the LDS lists of k_sa_lds for the rest of the step (the lists are written
+// on every level for that purpose).  Same draws, accepts and state as k_sa_lds.
+template <int D, int T>
+__global__ void __launch_bounds__(64) k_sa_lds_fast(const int32_t* __restrict__ adj, int64_t n, int64_t R,
+                                                    int64_t W, u64* __restrict__ s, mjx_sa_state st, int64_t nsteps,
+                                                    double par_a, double par_b, double a_cap, double b_cap,
+                                                    int64_t t_cap, Geo geo) {
+    static_assert(D >= 1 && D <= 4 && T >= 1 && T <= kMaxT, "fast LDS SA: d <= 4");
+    constexpr int DP1 = D + 1;
+    constexpr int MAXM = 64 / DP1;                 // members of C_{t-1} one wave can expand
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int lane = threadIdx.x;
+    const int64_t r = blockIdx.x;
+    const int64_t col = r >> 6;
+    const u64 rbit = 1ull << (r & 63);
+    const int nw = geo.nw, lc = geo.lc;
+    uint16_t* rows = reinterpret_cast<uint16_t*>(smem);
+    uint32_t* lv = reinterpret_cast<uint32_t*>(smem + geo.off_lev);
+    uint32_t* lev0s = reinterpret_cast<uint32_t*>(smem + geo.off_lev0);
+    uint32_t* mt = reinterpret_cast<uint32_t*>(smem + geo.off_mt);
+    uint32_t* lst = reinterpret_cast<uint32_t*>(smem + geo.off_list);
+    const int32_t* g = adj + (st.rep_graph ? (int64_t)st.rep_graph[r] : 0) * n * D;
+    auto lword = [&](int t, int w) -> uint32_t& { return lv[2 * (t * nw + w)]; };
+    auto cword = [&](int t, int w) -> uint32_t& { return lv[2 * (t * nw + w) + 1]; };
+    auto seen = [&](int t, int v) -> uint32_t {
+        const uint2 x = *reinterpret_cast<const uint2*>(lv + 2 * (t * nw + (v >> 5)));
+        return ((x.x ^ x.y) >> (v & 31)) & 1u;
+    };
+    auto nbrs = [&](int v, int (&o)[D]) {
+        const uint2 x = *reinterpret_cast<const uint2*>(rows + v * 4);
+        o[0] = (int)(x.x & 0xffffu);
+        if constexpr (D > 1) o[1] = (int)(x.x >> 16);
+        if constexpr (D > 2) o[2] = (int)(x.y & 0xffffu);
+        if constexpr (D > 3) o[3] = (int)(x.y >> 16);
+    };
+    auto maj = [&](int ones, uint32_t own) -> uint32_t {       // always-stay majority (code/SA_RRG.py:19-20)
+        return (2 * ones > D) ? 1u : ((2 * ones < D) ? 0u : own);
+    };
+
+    // ---- launch setup (as k_sa_lds)
+    for (int64_t q = lane; q < n * D; q += 64) {
+        const int64_t v = q / D;
+        rows[v * 4 + (q - v * D)] = (uint16_t)g[q];
+    }
+    for (int64_t v0 = 0; v0 < (int64_t)nw * 32; v0 += 64) {
+        const int64_t v = v0 + lane;
+        const bool b = v < n && (s[v * W + col] & rbit);
+        const u64 m = __ballot(b);
+        if (lane < 2) {
+            const uint32_t x = (uint32_t)(m >> (32 * lane));
+            lword(0, (int)(v0 >> 5) + lane) = x;
+            lev0s[(v0 >> 5) + lane] = x;
+        }
+    }
+    for (int k = lane; k < (T + 1) * nw; k += 64) lv[2 * k + 1] = 0u;
+    for (int k = lane; k < MT_N; k += 64) mt[k] = st.mt[r * MT_N + k];
+    wave_sync();
+    for (int t = 1; t <= T; ++t) {
+        for (int64_t v0 = 0; v0 < (int64_t)nw * 32; v0 += 64) {
+            const int v = (int)(v0 + lane);
+            uint32_t nb = 0;
+            if (v < n) {
+                int nv[D];
+                nbrs(v, nv);
+                int ones = 0;
+#pragma unroll
+                for (int q = 0; q < D; ++q) ones += (int)seen(t - 1, nv[q]);
+                nb = maj(ones, seen(t - 1, v));
+            }
+            const u64 m = __ballot(nb != 0);
+            if (lane < 2) lword(t, (int)(v0 >> 5) + lane) = (uint32_t)(m >> (32 * lane));
+        }
+        wave_sync();
+    }
+
+    double a = st.a[r], b = st.b[r];
+    int64_t t = st.t[r], sum_end = st.sum_end[r];
+    int done = st.done[r];
+    int idx = st.mt_idx[r];
+    int ties = 0;
+    const uint32_t rng = (uint32_t)(n - 1);
+    uint32_t mask = rng;
+    mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+
+    // ---- proposal windows: lane j holds proposal j of the current window
+    int pb_i = 0, pb_end = 0;
+    uint32_t pb_w1 = 0, pb_w2 = 0;
+    int npend = 0, pk = 0;
+    auto refill = [&]() {
+        npend = 0;
+        pk = 0;
+        while (npend == 0) {
+            if (idx >= MT_N) {
+                lds_twist(mt, lane);
+                idx = 0;
+            }
+            const int lim = (MT_N - idx < 64) ? MT_N - idx : 64;
+            uint32_t tw = 0, y = 0;
+            bool ok = false;
+            if (lane < lim) {
+                tw = mt_temper(mt[idx + lane]);
+                y = tw & mask;
+                ok = y <= rng;
+            }
+            const u64 okm = __ballot(ok);
+            int pos = 0;
+            while (pos < 64) {
+                const u64 m = okm >> pos;
+                if (!m) break;
+                const int f = pos + __ffsll((unsigned long long)m) - 1;
+                if (f + 2 >= lim) break;
+                const int iv = __builtin_amdgcn_readlane((int)y, f);
+                const uint32_t w1 = (uint32_t)__builtin_amdgcn_readlane((int)tw, f + 1);
+                const uint32_t w2 = (uint32_t)__builtin_amdgcn_readlane((int)tw, f + 2);
+                if (lane == npend) { pb_i = iv; pb_w1 = w1; pb_w2 = w2; pb_end = idx + f + 3; }
+                ++npend;
+                pos = f + 3;
+            }
+            if (npend > 0) { idx += pos; break; }
+            if (!okm) { idx += lim; continue; }                  // every word rejected by randint
+            const int f = __ffsll((unsigned long long)okm) - 1;
+            if (f > 0) { idx += f; continue; }                   // rejected words before the next i
+            // i is the window's first word and rand()'s two words cross the end of the
+            // state: the serial draw twists between them, as numpy does
+            const int iv = __builtin_amdgcn_readlane((int)y, 0);
+            idx += 1;
+            if (idx >= MT_N) { lds_twist(mt, lane); idx = 0; }
+            const uint32_t w1 = mt_temper(mt[idx]);
+            idx += 1;
+            if (idx >= MT_N) { lds_twist(mt, lane); idx = 0; }
+            const uint32_t w2 = mt_temper(mt[idx]);
+            idx += 1;
+            if (lane == 0) { pb_i = iv; pb_w1 = w1; pb_w2 = w2; pb_end = idx; }
+            npend = 1;
+        }
+    };
+
+    // per level: the candidate a lane holds, the mask of lanes in C_l (fast
+    // levels), or the list count (levels taken by the LDS-list path)
+    int lc_c[T + 1];
+    u64 lc_m[T + 1];
+    int lc_n[T + 1];
+    bool lc_fast[T + 1];
+    bool drew = false;
+    int64_t k = 0;
+    for (; k < nsteps && done == 0; ++k) {
+        if (pk == npend) refill();
+        drew = true;
+        const int iv = __builtin_amdgcn_readlane(pb_i, pk);
+        const uint32_t w1 = (uint32_t)__builtin_amdgcn_readlane((int)pb_w1, pk);
+        const uint32_t w2 = (uint32_t)__builtin_amdgcn_readlane((int)pb_w2, pk);
+        ++pk;
+        const double u = mt_double(w1, w2);
+        const uint32_t lw0 = lword(0, iv >> 5);
+        const uint32_t old_i = (lw0 >> (iv & 31)) & 1u;
+        // ---- level 1: i and its neighbours, values of level 0 with i flipped; a
+        // repeated row entry (not in a simple graph) is dropped by lane compares
+        int cand, nv[D];
+        {
+            int ri[D];
+            nbrs(iv, ri);
+            cand = iv;
+#pragma unroll
+            for (int q = 0; q < D; ++q)
+                if (lane == q + 1) cand = ri[q];
+            bool dup = lane > 0 && cand == iv;
+#pragma unroll
+            for (int q = 0; q < D; ++q)
+                if (q + 1 < lane) dup |= ri[q] == cand;
+            nbrs(cand, nv);
+            int ones = 0;
+#pragma unroll
+            for (int e = 0; e < D; ++e) ones += (int)(((lword(0, nv[e] >> 5) >> (nv[e] & 31)) & 1u) ^ (nv[e] == iv));
+            const uint32_t own = ((lword(0, cand >> 5) >> (cand & 31)) & 1u) ^ (cand == iv);
+            const uint32_t nb = maj(ones, own);
+            const uint32_t cur = (lword(1, cand >> 5) >> (cand & 31)) & 1u;
+            const bool chg = lane <= D && !dup && nb != cur;
+            const u64 m = __ballot(chg);
+            if (chg) {
+                atomicOr(&cword(1, cand >> 5), 1u << (cand & 31));
+                lst[lc + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)cand;
+            }
+            lc_c[1] = cand;
+            lc_m[1] = m;
+            lc_n[1] = __popcll(m);
+            lc_fast[1] = true;
+        }
+        int last = lc_n[1] ? 1 : 0;
+        int64_t ds = 0;
+        bool fast = true;
+        if (T == 1 && last == 1) {
+            const uint32_t cur = (lword(1, cand >> 5) >> (cand & 31)) & 1u;
+            ds = ((lc_m[1] >> lane) & 1ull) ? (cur ? -2 : 2) : 0;
+        }
+#pragma unroll
+        for (int l = 2; l <= T; ++l) {
+            if (last != l - 1) break;
+            wave_sync();                                     // marks of C_{l-1} before they are read
+            const u64 pm = lc_m[l - 1];
+            const int np = lc_n[l - 1];
+            int nc = 0;
+            if (fast && np <= MAXM) {
+                // candidates: member s = lane / (d+1) of C_{l-1} (its lane found by a
+                // scan of the mask), j = 0 the member itself, j > 0 its j-th neighbour
+                const int sl = lane / DP1, j = lane - sl * DP1;
+                int src = 0;
+                u64 x = pm;
+                for (int q = 0; q < np; ++q) {
+                    const int pbit = __ffsll((unsigned long long)x) - 1;
+                    if (q == sl) src = pbit;
+                    x &= x - 1;
+                }
+                const int mc = __shfl(cand, src, 64);
+                int pn[D];
+#pragma unroll
+                for (int e = 0; e < D; ++e) pn[e] = __shfl(nv[e], src, 64);
+                const bool act = sl < np;
+                int c2 = mc;
+#pragma unroll
+                for (int e = 0; e < D; ++e)
+                    if (j == e + 1) c2 = pn[e];
+                if (!act) c2 = iv;
+                int nv2[D];
+                nbrs(c2, nv2);
+                int ones = 0;
+#pragma unroll
+                for (int e = 0; e < D; ++e) ones += (int)seen(l - 1, nv2[e]);
+                const uint32_t nb = maj(ones, seen(l - 1, c2));
+                const uint32_t cur = (lword(l, c2 >> 5) >> (c2 & 31)) & 1u;
+                bool add = false;
+                if (act && nb != cur) {
+                    const uint32_t bit = 1u << (c2 & 31);
+                    add = (atomicOr(&cword(l, c2 >> 5), bit) & bit) == 0u;   // first mark (candidates repeat)
+                }
+                const u64 m = __ballot(add);
+                if (add) lst[l * lc + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)c2;
+                nc = __popcll(m);
+                cand = c2;
+#pragma unroll
+                for (int e = 0; e < D; ++e) nv[e] = nv2[e];
+                lc_c[l] = c2;
+                lc_m[l] = m;
+                lc_fast[l] = true;
+                if (l == T) ds = add ? (cur ? -2 : 2) : 0;
+            } else {
+                // the LDS-list path of k_sa_lds (lists of every level are in lst)
+                fast = false;
+                const uint32_t* prev = lst + (l - 1) * lc;
+                uint32_t* curl = lst + l * lc;
+                const int m = np * DP1;
+                for (int base = 0; base < m; base += 64) {
+                    const int q = base + lane;
+                    bool add = false;
+                    int cd = 0;
+                    uint32_t cur = 0;
+                    if (q < m) {
+                        const int slot = q / DP1, j = q - slot * DP1;
+                        const int v = (int)prev[slot];
+                        cd = (j == 0) ? v : (int)rows[v * 4 + j - 1];
+                        int nv2[D];
+                        nbrs(cd, nv2);
+                        int ones = 0;
+#pragma unroll
+                        for (int e = 0; e < D; ++e) ones += (int)seen(l - 1, nv2[e]);
+                        const uint32_t nb = maj(ones, seen(l - 1, cd));
+                        const uint32_t bit = 1u << (cd & 31);
+                        cur = (lword(l, cd >> 5) >> (cd & 31)) & 1u;
+                        if (nb != cur) add = (atomicOr(&cword(l, cd >> 5), bit) & bit) == 0u;
+                    }
+                    const u64 bal = __ballot(add);
+                    if (add) curl[nc + __popcll(bal & ((1ull << lane) - 1ull))] = (uint32_t)cd;
+                    nc += __popcll(bal);
+                    if (l == T && add) ds += cur ? -2 : 2;
+                }
+                lc_fast[l] = false;
+                wave_sync();
+            }
+            lc_n[l] = nc;
+            if (nc == 0) break;
+            last = l;
+        }
+        if (last == T) ds = wave_sum(ds);
+        else ds = 0;
+        // sum(s_end(flipped)) - sum(s_end): every node of C_T turned to its complement
+        const int64_t sum_new = sum_end + ds;
+        // delta_H (code/SA_RRG.py:37), same operation order, no contraction
+        const double si = old_i ? 1.0 : -1.0;
+        const double t1 = (-2.0 * a) * si;
+        const double t2 = b * (double)(sum_end - sum_new);
+        const double dE = (t1 + t2) / (double)n;
+        const double e = exp(-dE);
+        const double prob = (e < 1.0) ? e : 1.0;                    // (code/SA_RRG.py:75)
+        const bool acc = u < prob;                                  // (code/SA_RRG.py:76)
+        if (e < 1.0 && fabs(u - e) <= 4.0 * (nextafter(e, 2.0) - e)) ++ties;
+        // accepted (code/SA_RRG.py:77): C_0..C_last into the levels; always: clear the marks
+        if (acc && lane == 0) atomicXor(&lword(0, iv >> 5), 1u << (iv & 31));
+#pragma unroll
+        for (int l = 1; l <= T; ++l) {
+            if (l > last) break;
+            if (lc_fast[l]) {
+                if ((lc_m[l] >> lane) & 1ull) {
+                    const int v = lc_c[l];
+                    const uint32_t bit = 1u << (v & 31);
+                    if (acc) atomicXor(&lword(l, v >> 5), bit);
+                    atomicAnd(&cword(l, v >> 5), ~bit);
+                }
+            } else {
+                const uint32_t* cl = lst + l * lc;
+                for (int q = lane; q < lc_n[l]; q += 64) {
+                    const int v = (int)cl[q];
+                    const uint32_t bit = 1u << (v & 31);
+                    if (acc) atomicXor(&lword(l, v >> 5), bit);
+                    atomicAnd(&cword(l, v >> 5), ~bit);
+                }
+            }
+        }
+        if (acc) sum_end = sum_new;
+        if (a < a_cap) a = par_a * a;                               // (code/SA_RRG.py:80-81)
+        if (b < b_cap) b = par_b * b;
+        t += 1;                                                     // (code/SA_RRG.py:82)
+        if (t > t_cap) done = 2;                                    // (code/SA_RRG.py:84)
+        else if (sum_end == n) done = 1;                            // m(s_endstate(s)) == 1
+        if (lane == 0) {
+            if (st.tr_i) st.tr_i[k * R + r] = iv;
+            if (st.tr_acc) st.tr_acc[k * R + r] = acc ? 1 : 0;
+            if (st.tr_sum) st.tr_sum[k * R + r] = sum_end;
+            if (st.tr_dE) st.tr_dE[k * R + r] = dE;
+        }
+        wave_sync();
+    }
+    // the stream index numpy would hold: the end of the last proposal consumed
+    if (drew) idx = __builtin_amdgcn_readlane(pb_end, pk - 1);
+    if (lane == 0) {
+        for (; k < nsteps; ++k) {
+            if (st.tr_i) st.tr_i[k * R + r] = -1;
+            if (st.tr_acc) st.tr_acc[k * R + r] = -1;
+            if (st.tr_sum) st.tr_sum[k * R + r] = sum_end;
+            if (st.tr_dE) st.tr_dE[k * R + r] = 0.0;
+        }
+    }
+    for (int64_t v0 = 0; v0 < n; v0 += 64) {
+        const int v = (int)(v0 + lane);
+        if (v < n && (((lword(0, v >> 5) ^ lev0s[v >> 5]) >> (v & 31)) & 1u))
+            atomicXor((unsigned long long*)&s[(int64_t)v * W + col], (unsigned long long)rbit);
+    }
+    for (int q = lane; q < MT_N; q += 64) st.mt[r * MT_N + q] = mt[q];
+    if (lane == 0) {
+        st.mt_idx[r] = idx;
+        st.a[r] = a;
+        st.b[r] = b;
+        st.t[r] = t;
+        st.sum_end[r] = sum_end;
+        st.done[r] = done;
+        if (st.tr_tie) st.tr_tie[r] += ties;
+    }
+}
+
 }  // namespace salds
 }  // namespace mjx
 
@@ -368,6 +747,7 @@ extern "C" int mjx_sa_lds_steps(const int32_t* adj, int64_t n, int d, int p, int
     if (!salds::geometry(n, d, T, &g)) return MJX_ERANGE;
     const mjx_sa_state st = *stp;
     if (!st.mt || !st.mt_idx || !st.a || !st.b || !st.t || !st.sum_end || !st.done) return MJX_EINVAL;
+    if (st.opt_flags & ~(MJX_SA_NO_SPEC | MJX_SA_NO_CONE2 | MJX_SA_LDS_SERIAL)) return MJX_EINVAL;
     if (nsteps == 0) return MJX_OK;
     if (R > INT32_MAX) return MJX_ERANGE;
     const int64_t W = (R + 63) / 64;
@@ -380,6 +760,26 @@ extern "C" int mjx_sa_lds_steps(const int32_t* adj, int64_t n, int d, int p, int
         MJX_LAUNCH_CHECK("k_sa_lds");
         return MJX_OK;
     };
+    if (!(st.opt_flags & MJX_SA_LDS_SERIAL) && (d == 3 || d == 4) && T <= 4) {
+        auto gof = [&](auto kern) -> int {
+            MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, g.bytes),
+                    "sa_lds lds");
+            kern<<<(unsigned)R, 64, (size_t)g.bytes, hs>>>(adj, n, R, W, (u64*)s, st, nsteps, par_a, par_b, a_cap,
+                                                           b_cap, t_cap, g);
+            MJX_LAUNCH_CHECK("k_sa_lds_fast");
+            return MJX_OK;
+        };
+#define MJX_LDS_FAST(DD)                                            \
+        switch (T) {                                                \
+            case 1: return gof(salds::k_sa_lds_fast<DD, 1>);        \
+            case 2: return gof(salds::k_sa_lds_fast<DD, 2>);        \
+            case 3: return gof(salds::k_sa_lds_fast<DD, 3>);        \
+            default: return gof(salds::k_sa_lds_fast<DD, 4>);       \
+        }
+        if (d == 3) { MJX_LDS_FAST(3) }
+        MJX_LDS_FAST(4)
+#undef MJX_LDS_FAST
+    }
     switch (d) {
         case 3: return go(salds::k_sa_lds<3>);
         case 4: return go(salds::k_sa_lds<4>);

@@ -10,6 +10,7 @@ import pytest
 import torch
 
 from conftest import load_golden
+from oracle import fast
 from oracle import majority as orc
 
 pytestmark = pytest.mark.gpu
@@ -36,14 +37,17 @@ def test_sa_init_draws_reference_s0(mjx_mod):
 def _sa(mjx_mod, N, p, c, seeds, mode):
     """mode: "lightcone" (HBM cone layout, default tape), "lightcone-notape"
     (draws inside the step kernel), "lightcone-tape7" (tape chunks of 7
-    steps), "lightcone-lds" (graph, levels and stream in LDS), "lightcone-rec"
+    steps), "lightcone-lds" (graph, levels and stream in LDS; "-ldsserial" the
+    list-based step), "lightcone-rec"
     (the cone with the adjacency rows in its records), "rollout"."""
     tape = {"lightcone-notape": 0, "lightcone-tape7": 7}.get(mode, 1024)
-    layout = {"lightcone-lds": "lds", "lightcone-rec": "rec"}.get(mode, "cone")
-    return mjx_mod.SAReplicas(N, p, c, seeds, mode=mode.split("-")[0], tape=tape, layout=layout)
+    layout = {"lightcone-lds": "lds", "lightcone-ldsserial": "lds", "lightcone-rec": "rec"}.get(mode, "cone")
+    kernel = {"lds_serial": True} if mode == "lightcone-ldsserial" else None
+    return mjx_mod.SAReplicas(N, p, c, seeds, mode=mode.split("-")[0], tape=tape, layout=layout, kernel=kernel)
 
 
-MODES = ["lightcone", "lightcone-notape", "lightcone-tape7", "lightcone-lds", "lightcone-rec", "rollout"]
+MODES = ["lightcone", "lightcone-notape", "lightcone-tape7", "lightcone-lds", "lightcone-ldsserial", "lightcone-rec",
+         "rollout"]
 
 
 @pytest.mark.parametrize("mode", MODES)
@@ -239,3 +243,39 @@ def test_sa_run_independent_per_replica_graphs(mjx_mod):
         o = orc.sa_loop(g[k], 2, 1, 40 + k, max_steps=400)
         assert np.array_equal(res["conf"][k], o["conf"]), k
         assert res["num_steps"][k] == o["num_steps"], k
+
+
+@pytest.mark.parametrize("d,p,c,serial", [(4, 3, 1, False), (4, 3, 1, True), (3, 2, 1, False), (4, 1, 1, False)])
+def test_sa_lds_stream_position_in_ragged_calls(mjx_mod, d, p, c, serial):
+    """The LDS-resident step parses the numpy stream 64 words at a time and
+    hands back the index after the last proposal it consumed: calls of
+    ragged lengths (1, 2, 3, 5, 7, ... steps) give the oracle's trace, and the
+    MT19937 state after them equals numpy's RandomState after the same draws
+    (binomial s0, then randint(0, n) and rand() per proposal,
+    code/SA_RRG.py:65,73,76) -- twists included."""
+    n, R = 300, 3
+    graphs = [mjx_mod.random_regular_graph(d, n, seed=70 + g) for g in range(R)]
+    seeds = [17, 18, 19]
+    kernel = {"lds_serial": True} if serial else None
+    sa = mjx_mod.SAReplicas(graphs, p, c, seeds, layout="lds", kernel=kernel)
+    got = {k: [] for k in ("i", "accept", "sum_end", "dE")}
+    total = 0
+    for k in [1, 2, 3, 5, 7, 11, 1, 64, 65, 129, 3, 200]:
+        tr = sa.steps(k, trace=True)
+        for key in got:
+            got[key].append(tr[key].cpu().numpy())
+        total += k
+    got = {key: np.concatenate(v) for key, v in got.items()}
+    mt, idx = sa.mt_state()
+    for r in range(R):
+        o = fast.sa_loop(graphs[r], p, c, seeds[r], max_steps=total, trace=True)
+        L = len(o["trace"]["i"])
+        for key in got:
+            assert np.array_equal(got[key][:L, r], o["trace"][key]), (r, key)
+        rs = np.random.RandomState(seeds[r])
+        rs.binomial(n=1, p=0.5, size=[n])
+        for _ in range(L):
+            rs.randint(low=0, high=n)
+            rs.rand()
+        st = rs.get_state()
+        assert np.array_equal(mt[r], st[1].astype(np.uint32)) and int(idx[r]) == st[2], r
