@@ -364,7 +364,8 @@ def bench_sa_c1(args, rank, world, dist, dev, c1_cpu=None):
         sa.steps(args.sa_warmin)
         el = _timed(lambda: sa.steps(K), dist, dev)
         props = world * R * K / el
-        res[tag] = {"mode": sa.mode, "proposals_per_s": props, "sweeps_per_s": props / n, "ms_per_step": 1e3 * el / K}
+        res[tag] = {"mode": sa.mode, "layout": sa.layout, "proposals_per_s": props, "sweeps_per_s": props / n,
+                    "ms_per_step": 1e3 * el / K}
         del sa
     res["proposals_per_s"] = res["distinct_graphs"]["proposals_per_s"]
     if c1_cpu is not None:
@@ -417,9 +418,10 @@ def bench_sa_consensus(args, rank, world, dist, dev):
       * to_consensus: n = --consensus-n (1000), where the runs end (1e5-1e7
         proposals per replica): wall time to consensus, the num_steps /
         mag_reached distributions (the script's np.savez keys);
-      * script_size: the script's n = 1e4 for a fixed wall budget: there no
-        replica reaches consensus within 1.7e7 proposals (round-3 measurement),
-        so this reports the rate and how far the runs got."""
+      * script_size: the script's n = 1e4 for a fixed wall budget: there the
+        runs need 4.4e7 to >3.2e8 proposals per replica (round 3, 900 s on 64
+        replicas: 38 done, profiles/r03_sa_consensus_n1e4.log), so this
+        reports the rate and how far the runs got."""
     import mjx
     d, p, c, R = 4, 3, 1, args.consensus_replicas
     out = {"config": f"SA_RRG.py's problem: d={d} RRG, p={p} c={c}, {R} replicas per GPU each on its own graph, "

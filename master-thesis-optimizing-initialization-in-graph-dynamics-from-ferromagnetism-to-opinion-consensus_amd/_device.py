@@ -18,6 +18,11 @@ def require_gpu():
     return torch.device("cuda", torch.cuda.current_device())
 
 
+def cu_count():
+    """Compute units of the current device (256 on an MI355X)."""
+    return torch.cuda.get_device_properties(require_gpu()).multi_processor_count
+
+
 def stream_handle():
     return torch.cuda.current_stream().cuda_stream
 

@@ -101,6 +101,16 @@ __device__ __forceinline__ int64_t wave_sum(int64_t x) {
     return x;
 }
 
+// Diagnostic build only (-DMJX_SA_PROF, tools/sa_lds_prof.py): per-phase
+// s_memtime cycles of k_sa_lds_fast summed over waves; every stamp drains the
+// wave's counters first, so a phase's exposed latency is charged to it.
+#ifdef MJX_SA_PROF
+__device__ unsigned long long mjx_sa_lds_prof[8];
+#define LDS_STAMP(k) do { __builtin_amdgcn_sched_barrier(0); asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); const unsigned long long _c = __builtin_amdgcn_s_memtime(); _acc[k] += _c - _t0; _t0 = _c; __builtin_amdgcn_sched_barrier(0); } while (0)
+#else
+#define LDS_STAMP(k) do {} while (0)
+#endif
+
 // Level t of the replica is a bit array (bit v = the cached value onestep^t(s)
 // of node v) interleaved word by word with a change-bit array: lv[2(t nw + w)]
 // = level word w, lv[2(t nw + w) + 1] = change word w.  During a proposal the
@@ -372,7 +382,7 @@ __global__ void __launch_bounds__(64) k_sa_lds(const int32_t* __restrict__ adj, 
 // A level whose candidates exceed one wave (|C_{t-1}| (d+1) > 64) falls back
 // to the LDS lists of k_sa_lds for the rest of the step (the lists are written
 // on every level for that purpose).  Same draws, accepts and state as k_sa_lds.
-template <int D, int T>
+template <int D, int T, bool TRACE>
 __global__ void __launch_bounds__(64) k_sa_lds_fast(const int32_t* __restrict__ adj, int64_t n, int64_t R,
                                                     int64_t W, u64* __restrict__ s, mjx_sa_state st, int64_t nsteps,
                                                     double par_a, double par_b, double a_cap, double b_cap,
@@ -453,10 +463,15 @@ __global__ void __launch_bounds__(64) k_sa_lds_fast(const int32_t* __restrict__ 
     const uint32_t rng = (uint32_t)(n - 1);
     uint32_t mask = rng;
     mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+    double inv_n = 1.0 / (double)n;                       // screening only (dE itself divides)
+    // the float64 schedule lives in VGPRs (its arithmetic is vector anyway):
+    // the scalar file is what the step's control flow needs
+    asm volatile("" : "+v"(a), "+v"(b), "+v"(par_a), "+v"(par_b), "+v"(a_cap), "+v"(b_cap), "+v"(inv_n));
 
     // ---- proposal windows: lane j holds proposal j of the current window
     int pb_i = 0, pb_end = 0;
     uint32_t pb_w1 = 0, pb_w2 = 0;
+    double pb_u = 0.0;
     int npend = 0, pk = 0;
     auto refill = [&]() {
         npend = 0;
@@ -505,24 +520,33 @@ __global__ void __launch_bounds__(64) k_sa_lds_fast(const int32_t* __restrict__ 
             if (lane == 0) { pb_i = iv; pb_w1 = w1; pb_w2 = w2; pb_end = idx; }
             npend = 1;
         }
+        pb_u = mt_double(pb_w1, pb_w2);                       // rand() of every proposal at once
     };
 
-    // per level: the candidate a lane holds, the mask of lanes in C_l (fast
-    // levels), or the list count (levels taken by the LDS-list path)
+    // per level: the candidate a lane holds, its cached bit, whether it is in
+    // C_l (fast levels), or the list count (levels taken by the LDS-list path)
     int lc_c[T + 1];
-    u64 lc_m[T + 1];
+    uint32_t lc_v[T + 1];
+    bool lc_in[T + 1];
     int lc_n[T + 1];
     bool lc_fast[T + 1];
+    // the next proposal's adjacency rows (static), read during this step
+    int ri_n[D], nv_n[D];
+    bool pf = false;
     bool drew = false;
     int64_t k = 0;
+#ifdef MJX_SA_PROF
+    unsigned long long _acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, _t0 = __builtin_amdgcn_s_memtime();
+#endif
     for (; k < nsteps && done == 0; ++k) {
         if (pk == npend) refill();
         drew = true;
         const int iv = __builtin_amdgcn_readlane(pb_i, pk);
-        const uint32_t w1 = (uint32_t)__builtin_amdgcn_readlane((int)pb_w1, pk);
-        const uint32_t w2 = (uint32_t)__builtin_amdgcn_readlane((int)pb_w2, pk);
+        const double u = __builtin_bit_cast(
+            double, ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(__builtin_bit_cast(uint64_t, pb_u) >> 32), pk) << 32) |
+                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)__builtin_bit_cast(uint64_t, pb_u), pk));
         ++pk;
-        const double u = mt_double(w1, w2);
+        LDS_STAMP(0);
         const uint32_t lw0 = lword(0, iv >> 5);
         const uint32_t old_i = (lw0 >> (iv & 31)) & 1u;
         // ---- level 1: i and its neighbours, values of level 0 with i flipped; a
@@ -530,7 +554,12 @@ __global__ void __launch_bounds__(64) k_sa_lds_fast(const int32_t* __restrict__ 
         int cand, nv[D];
         {
             int ri[D];
-            nbrs(iv, ri);
+            if (pf) {
+#pragma unroll
+                for (int e = 0; e < D; ++e) { ri[e] = ri_n[e]; nv[e] = nv_n[e]; }
+            } else {
+                nbrs(iv, ri);
+            }
             cand = iv;
 #pragma unroll
             for (int q = 0; q < D; ++q)
@@ -539,7 +568,10 @@ __global__ void __launch_bounds__(64) k_sa_lds_fast(const int32_t* __restrict__ 
 #pragma unroll
             for (int q = 0; q < D; ++q)
                 if (q + 1 < lane) dup |= ri[q] == cand;
-            nbrs(cand, nv);
+            if (!pf) nbrs(cand, nv);
+            // the next proposal's row (its neighbours' rows follow after the levels)
+            pf = pk < npend;
+            if (pf) nbrs(__builtin_amdgcn_readlane(pb_i, pk), ri_n);
             int ones = 0;
 #pragma unroll
             for (int e = 0; e < D; ++e) ones += (int)(((lword(0, nv[e] >> 5) >> (nv[e] & 31)) & 1u) ^ (nv[e] == iv));
@@ -553,22 +585,26 @@ __global__ void __launch_bounds__(64) k_sa_lds_fast(const int32_t* __restrict__ 
                 lst[lc + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)cand;
             }
             lc_c[1] = cand;
-            lc_m[1] = m;
+            lc_v[1] = cur;
+            lc_in[1] = chg;
             lc_n[1] = __popcll(m);
             lc_fast[1] = true;
         }
         int last = lc_n[1] ? 1 : 0;
+        LDS_STAMP(1);
+        // sum(s_end(flipped)) - sum(s_end): every node of C_T turned to its complement,
+        // +2 for a -1 -> +1 change, -2 for +1 -> -1 (counted by ballots)
         int64_t ds = 0;
-        bool fast = true;
         if (T == 1 && last == 1) {
-            const uint32_t cur = (lword(1, cand >> 5) >> (cand & 31)) & 1u;
-            ds = ((lc_m[1] >> lane) & 1ull) ? (cur ? -2 : 2) : 0;
+            const bool in = lc_in[1];
+            ds = 2 * ((int64_t)__popcll(__ballot(in && lc_v[1] == 0u)) - (int64_t)__popcll(__ballot(in && lc_v[1] != 0u)));
         }
+        bool fast = true;
 #pragma unroll
         for (int l = 2; l <= T; ++l) {
             if (last != l - 1) break;
             wave_sync();                                     // marks of C_{l-1} before they are read
-            const u64 pm = lc_m[l - 1];
+            const u64 pm = __ballot(lc_in[l - 1]);
             const int np = lc_n[l - 1];
             int nc = 0;
             if (fast && np <= MAXM) {
@@ -599,10 +635,16 @@ __global__ void __launch_bounds__(64) k_sa_lds_fast(const int32_t* __restrict__ 
                 for (int e = 0; e < D; ++e) ones += (int)seen(l - 1, nv2[e]);
                 const uint32_t nb = maj(ones, seen(l - 1, c2));
                 const uint32_t cur = (lword(l, c2 >> 5) >> (c2 & 31)) & 1u;
-                bool add = false;
-                if (act && nb != cur) {
-                    const uint32_t bit = 1u << (c2 & 31);
-                    add = (atomicOr(&cword(l, c2 >> 5), bit) & bit) == 0u;   // first mark (candidates repeat)
+                const bool chg = act && nb != cur;
+                const uint32_t bit = 1u << (c2 & 31);
+                bool add = chg;
+                if (l == T) {
+                    // the last level counts distinct nodes: the first mark wins
+                    if (chg) add = (atomicOr(&cword(l, c2 >> 5), bit) & bit) == 0u;
+                } else if (chg) {
+                    // inner levels keep repeats (marks, clears and the accepted
+                    // values are idempotent; the next level's dedup absorbs them)
+                    atomicOr(&cword(l, c2 >> 5), bit);
                 }
                 const u64 m = __ballot(add);
                 if (add) lst[l * lc + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)c2;
@@ -611,15 +653,19 @@ __global__ void __launch_bounds__(64) k_sa_lds_fast(const int32_t* __restrict__ 
 #pragma unroll
                 for (int e = 0; e < D; ++e) nv[e] = nv2[e];
                 lc_c[l] = c2;
-                lc_m[l] = m;
+                lc_v[l] = cur;
+                lc_in[l] = add;
                 lc_fast[l] = true;
-                if (l == T) ds = add ? (cur ? -2 : 2) : 0;
+                if (l == T)
+                    ds = 2 * ((int64_t)__popcll(__ballot(add && cur == 0u)) - (int64_t)__popcll(__ballot(add && cur != 0u)));
             } else {
-                // the LDS-list path of k_sa_lds (lists of every level are in lst)
+                // the LDS-list path of k_sa_lds (lists of every level are in lst;
+                // this path dedups every level it builds)
                 fast = false;
                 const uint32_t* prev = lst + (l - 1) * lc;
                 uint32_t* curl = lst + l * lc;
                 const int m = np * DP1;
+                int64_t dsl = 0;
                 for (int base = 0; base < m; base += 64) {
                     const int q = base + lane;
                     bool add = false;
@@ -642,38 +688,69 @@ __global__ void __launch_bounds__(64) k_sa_lds_fast(const int32_t* __restrict__ 
                     const u64 bal = __ballot(add);
                     if (add) curl[nc + __popcll(bal & ((1ull << lane) - 1ull))] = (uint32_t)cd;
                     nc += __popcll(bal);
-                    if (l == T && add) ds += cur ? -2 : 2;
+                    dsl += 2 * ((int64_t)__popcll(__ballot(add && cur == 0u)) - (int64_t)__popcll(__ballot(add && cur != 0u)));
                 }
+                if (l == T) ds = dsl;
                 lc_fast[l] = false;
                 wave_sync();
             }
             lc_n[l] = nc;
+            LDS_STAMP(l < 4 ? l : 4);
             if (nc == 0) break;
             last = l;
         }
-        if (last == T) ds = wave_sum(ds);
-        else ds = 0;
-        // sum(s_end(flipped)) - sum(s_end): every node of C_T turned to its complement
+        if (last != T) ds = 0;
+        // the next proposal's neighbour rows
+        if (pf) {
+            int cn = __builtin_amdgcn_readlane(pb_i, pk);
+#pragma unroll
+            for (int q = 0; q < D; ++q)
+                if (lane == q + 1) cn = ri_n[q];
+            nbrs(cn, nv_n);
+        }
         const int64_t sum_new = sum_end + ds;
         // delta_H (code/SA_RRG.py:37), same operation order, no contraction
         const double si = old_i ? 1.0 : -1.0;
         const double t1 = (-2.0 * a) * si;
         const double t2 = b * (double)(sum_end - sum_new);
-        const double dE = (t1 + t2) / (double)n;
-        const double e = exp(-dE);
-        const double prob = (e < 1.0) ? e : 1.0;                    // (code/SA_RRG.py:75)
-        const bool acc = u < prob;                                  // (code/SA_RRG.py:76)
-        if (e < 1.0 && fabs(u - e) <= 4.0 * (nextafter(e, 2.0) - e)) ++ties;
-        // accepted (code/SA_RRG.py:77): C_0..C_last into the levels; always: clear the marks
+        const double num = t1 + t2;
+        // u < min(1, exp(-dE)) (code/SA_RRG.py:75-76) decided by an fp32 exp
+        // wherever u is farther from it than that exp's error (|x| * 2^-24 from
+        // rounding x, a few ulp from the exp itself: 1e-6 (1 + |x|) relative
+        // covers both); otherwise, and for the trace, the float64 dE and exp of
+        // the reference, unchanged.  Same decision bit for bit.
+        const float xf = (float)(-num * inv_n);
+        const float ef = __expf(xf);
+        const float mg = ef * (1e-6f * (1.0f + fabsf(xf))) + 1e-37f;
+        bool acc;
+        double dE = 0.0;
+        if (fabs(u - (double)ef) > (double)mg) {
+            acc = u < (double)ef;
+            if (TRACE && st.tr_dE) dE = num / (double)n;
+        } else {
+            dE = num / (double)n;
+            const double e = exp(-dE);
+            const double prob = (e < 1.0) ? e : 1.0;                // (code/SA_RRG.py:75)
+            acc = u < prob;                                         // (code/SA_RRG.py:76)
+            if (e < 1.0 && fabs(u - e) <= 4.0 * (nextafter(e, 2.0) - e)) ++ties;
+        }
+        LDS_STAMP(5);
+        // accepted (code/SA_RRG.py:77): every node of C_0..C_last takes its new value
+        // (the complement of its cached one: set or clear, idempotent for the repeats
+        // of inner fast levels; list levels are duplicate-free and flip); always:
+        // clear the marks
         if (acc && lane == 0) atomicXor(&lword(0, iv >> 5), 1u << (iv & 31));
 #pragma unroll
         for (int l = 1; l <= T; ++l) {
             if (l > last) break;
             if (lc_fast[l]) {
-                if ((lc_m[l] >> lane) & 1ull) {
+                if (lc_in[l]) {
                     const int v = lc_c[l];
                     const uint32_t bit = 1u << (v & 31);
-                    if (acc) atomicXor(&lword(l, v >> 5), bit);
+                    if (acc) {
+                        if (lc_v[l]) atomicAnd(&lword(l, v >> 5), ~bit);
+                        else atomicOr(&lword(l, v >> 5), bit);
+                    }
                     atomicAnd(&cword(l, v >> 5), ~bit);
                 }
             } else {
@@ -692,17 +769,22 @@ __global__ void __launch_bounds__(64) k_sa_lds_fast(const int32_t* __restrict__ 
         t += 1;                                                     // (code/SA_RRG.py:82)
         if (t > t_cap) done = 2;                                    // (code/SA_RRG.py:84)
         else if (sum_end == n) done = 1;                            // m(s_endstate(s)) == 1
-        if (lane == 0) {
+        if (TRACE && lane == 0) {
             if (st.tr_i) st.tr_i[k * R + r] = iv;
             if (st.tr_acc) st.tr_acc[k * R + r] = acc ? 1 : 0;
             if (st.tr_sum) st.tr_sum[k * R + r] = sum_end;
             if (st.tr_dE) st.tr_dE[k * R + r] = dE;
         }
         wave_sync();
+        LDS_STAMP(6);
     }
+#ifdef MJX_SA_PROF
+    if (lane == 0)
+        for (int q = 0; q < 8; ++q) atomicAdd(&mjx_sa_lds_prof[q], _acc[q]);
+#endif
     // the stream index numpy would hold: the end of the last proposal consumed
     if (drew) idx = __builtin_amdgcn_readlane(pb_end, pk - 1);
-    if (lane == 0) {
+    if (TRACE && lane == 0) {
         for (; k < nsteps; ++k) {
             if (st.tr_i) st.tr_i[k * R + r] = -1;
             if (st.tr_acc) st.tr_acc[k * R + r] = -1;
@@ -731,6 +813,18 @@ __global__ void __launch_bounds__(64) k_sa_lds_fast(const int32_t* __restrict__ 
 }  // namespace mjx
 
 using namespace mjx;
+
+#ifdef MJX_SA_PROF
+extern "C" int mjx_sa_lds_prof_read(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(salds::mjx_sa_lds_prof), 8 * sizeof(unsigned long long)) != hipSuccess)
+        return MJX_EHIP;
+    if (reset) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(salds::mjx_sa_lds_prof), z, sizeof(z)) != hipSuccess) return MJX_EHIP;
+    }
+    return MJX_OK;
+}
+#endif
 
 extern "C" int64_t mjx_sa_lds_bytes(int64_t n, int d, int p, int c) {
     salds::Geo g;
@@ -769,12 +863,13 @@ extern "C" int mjx_sa_lds_steps(const int32_t* adj, int64_t n, int d, int p, int
             MJX_LAUNCH_CHECK("k_sa_lds_fast");
             return MJX_OK;
         };
-#define MJX_LDS_FAST(DD)                                            \
-        switch (T) {                                                \
-            case 1: return gof(salds::k_sa_lds_fast<DD, 1>);        \
-            case 2: return gof(salds::k_sa_lds_fast<DD, 2>);        \
-            case 3: return gof(salds::k_sa_lds_fast<DD, 3>);        \
-            default: return gof(salds::k_sa_lds_fast<DD, 4>);       \
+        const bool tr = st.tr_i || st.tr_acc || st.tr_sum || st.tr_dE;
+#define MJX_LDS_FAST(DD)                                                                                   \
+        switch (T) {                                                                                       \
+            case 1: return tr ? gof(salds::k_sa_lds_fast<DD, 1, true>) : gof(salds::k_sa_lds_fast<DD, 1, false>); \
+            case 2: return tr ? gof(salds::k_sa_lds_fast<DD, 2, true>) : gof(salds::k_sa_lds_fast<DD, 2, false>); \
+            case 3: return tr ? gof(salds::k_sa_lds_fast<DD, 3, true>) : gof(salds::k_sa_lds_fast<DD, 3, false>); \
+            default: return tr ? gof(salds::k_sa_lds_fast<DD, 4, true>) : gof(salds::k_sa_lds_fast<DD, 4, false>); \
         }
         if (d == 3) { MJX_LDS_FAST(3) }
         MJX_LDS_FAST(4)

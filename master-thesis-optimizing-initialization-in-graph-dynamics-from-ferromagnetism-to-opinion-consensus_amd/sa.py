@@ -188,17 +188,22 @@ class SAReplicas:
         self.mode = mode
         if layout not in ("auto", "lds", "cone", "rec", "levels"):
             raise ValueError(f"unknown light-cone layout {layout!r}")
-        lds_fits = 0 < _lib.load().mjx_sa_lds_bytes(n, self.d, self.p, self.c) <= 160 * 1024
-        # the speculative batches (k_sa_spec: d=3 at p+c-1 <= 2, d=4 at p+c-1 = 1) beat the
-        # LDS-resident kernel where they apply (configs[0] at d=4, p=c=1: 1.5 vs 2.7 us per
-        # step); the record layout is 2-3 % faster than the plain cone for one shared graph
-        # (configs[1]: 4.31 -> 4.20 us per step at R = 4096, same box)
+        lds_bytes = _lib.load().mjx_sa_lds_bytes(n, self.d, self.p, self.c)
+        lds_fits = 0 < lds_bytes <= 160 * 1024
+        # A replica in LDS is one workgroup for a whole call: the lane-held step (d <= 4,
+        # k_sa_lds_fast) runs SA_RRG.py's shapes fastest (d=4, n=1e4, 64 replicas: p=c=1
+        # 0.83 us per step vs 1.42 in the speculative batches, p=3 1.78 vs 69 in the cone)
+        # while the replicas fit the CUs in one round; more replicas than that go to the
+        # speculative batches (k_sa_spec: d=3 at p+c-1 <= 2, d=4 at p+c-1 = 1), in the
+        # record layout for one shared graph (configs[1]: 4.31 -> 4.20 us per step at
+        # R = 4096 vs the plain cone, same box), else to the cone.
         spec = (self.d == 3 and T <= 2) or (self.d == 4 and T == 1)
+        one_round = lds_fits and R <= _device.cu_count() * max(1, (160 * 1024) // lds_bytes)
         if layout == "auto":
-            if spec and self.rep_graph is None:
-                layout = "rec"
-            elif lds_fits and not spec:
+            if lds_fits and (one_round or not spec):
                 layout = "lds"
+            elif spec and self.rep_graph is None:
+                layout = "rec"
             else:
                 layout = "cone"
         if mode == "lightcone" and layout == "lds" and not lds_fits:

@@ -1,0 +1,33 @@
+"""Phase timers of k_sa_lds_fast (diagnostic build with -DMJX_SA_PROF): per-wave
+s_memtime cycles per phase, per step, at SA_RRG.py's shapes (d=4, n=1e4, 64
+replicas on distinct graphs, p=c=1 and p=3, c=1)."""
+import ctypes
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+import mjx  # noqa: E402
+
+mjx.load_library()
+raw = ctypes.CDLL(mjx.lib_path())
+names = ["refill+proposal", "level 1", "level 2", "level 3", "level 4", "dE+exp+accept", "apply+trace"]
+n, d, R = 10_000, 4, 64
+graphs = [mjx.random_regular_graph(d, n, seed=7000 + k) for k in range(R)]
+for (p, c) in ((1, 1), (3, 1)):
+    sa = mjx.SAReplicas(graphs, p, c, list(range(R)), layout="lds")
+    K = 20000
+    sa.steps(K)
+    torch.cuda.synchronize()
+    buf = (ctypes.c_ulonglong * 8)()
+    raw.mjx_sa_lds_prof_read(buf, 1)
+    t0 = time.perf_counter()
+    sa.steps(K)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    raw.mjx_sa_lds_prof_read(buf, 1)
+    print(f"p={p} c={c}: {1e6 * el / K:.3f} us/step; cycles per step per wave: "
+          + ", ".join(f"{nm} {buf[q] / R / K:.0f}" for q, nm in enumerate(names))
+          + f"; total {sum(buf[:8]) / R / K:.0f}", flush=True)
+    del sa
