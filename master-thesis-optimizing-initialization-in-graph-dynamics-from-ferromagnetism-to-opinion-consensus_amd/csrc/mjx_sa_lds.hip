@@ -53,6 +53,7 @@ struct Geo {
     int rw;          // uint16 entries per adjacency row (4, 8 or 16)
     int nw;          // uint32 bit words per level (even)
     int lc;          // change-list capacity per level (>= the radius-T ball)
+    int lvs;         // uint32 per level word entry: {level, marks} (2) or {level, marks A, marks B, -} (4)
     int off_lev;     // byte offsets into the dynamic LDS
     int off_lev0;
     int off_mt;
@@ -71,8 +72,9 @@ static int64_t ball(int d, int T) {
     return b;
 }
 
-static bool geometry(int64_t n, int d, int T, Geo* g) {
+static bool geometry(int64_t n, int d, int T, Geo* g, int planes = 1) {
     if (n < 2 || n > 65535 || d < 1 || d > 16 || T < 1 || T > kMaxT) return false;
+    g->lvs = (planes == 1) ? 2 : 4;
     g->rw = (d <= 4) ? 4 : (d <= 8) ? 8 : 16;
     g->nw = (int)(((n + 63) / 64) * 2);
     int64_t lc = ball(d, T);
@@ -81,10 +83,10 @@ static bool geometry(int64_t n, int d, int T, Geo* g) {
     if (lc > 4096) return false;
     g->lc = (int)lc;
     int64_t off = ((int64_t)n * g->rw * 2 + 15) / 16 * 16;
-    g->off_lev = (int)off;   off += (int64_t)(T + 1) * g->nw * 8;     // {level bits, change bits} per word
+    g->off_lev = (int)off;   off += (int64_t)(T + 1) * g->nw * 4 * g->lvs;   // {level bits, change bits} per word
     g->off_lev0 = (int)off;  off += (int64_t)g->nw * 4;
     g->off_mt = (int)off;    off += MT_N * 4;
-    g->off_list = (int)off;  off += (int64_t)(T + 1) * g->lc * 4;
+    g->off_list = (int)off;  off += (int64_t)planes * (T + 1) * g->lc * 4;
     g->off_cnt = (int)off;   off += 16 * 4;
     g->bytes = (int)off;
     return (size_t)off <= kLdsMax;
@@ -809,6 +811,557 @@ __global__ void __launch_bounds__(64) k_sa_lds_fast(const int32_t* __restrict__ 
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// Two proposals per step (k_sa_lds_pair<D, T>, d <= 4): the lane-held step
+// of k_sa_lds_fast is ALU-issue bound on its one wave (a few hundred VALU /
+// SALU instructions per level, 5-20 lanes busy), so the wave's two halves
+// evaluate the next two proposals A = k and B = k+1 of the replica at once,
+// both against the current levels, each with its own mark plane (a level
+// word entry is {level, marks A, marks B, -}, one 16-B read).  B stands
+// unless A is accepted and A may have changed something B read: B's lanes
+// read, beside every level-(l-1) value they use, A's level-(l-1) marks, and a
+// node B reads at level l-1 or whose cached level-l value B reads (one of
+// B's candidates) can change under A only if it or one of its neighbours is
+// in A's C_{l-1} -- exactly the nodes B reads; level 0 (no marks) by
+// comparing with i_A.  The acceptance of each is its own (dE depends on the
+// step's schedule value and its own ds only), so both are decided at once;
+// A's consequences (stop, t cap) are resolved first, then B is taken or
+// drawn again next step.  Proposal windows carry a leftover proposal into
+// the next window when no twist can fall between them.  Same draws, accepts
+// and state as k_sa_lds.
+template <int D, int T, bool TRACE>
+__global__ void __launch_bounds__(64) k_sa_lds_pair(const int32_t* __restrict__ adj, int64_t n, int64_t R,
+                                                    int64_t W, u64* __restrict__ s, mjx_sa_state st, int64_t nsteps,
+                                                    double par_a, double par_b, double a_cap, double b_cap,
+                                                    int64_t t_cap, Geo geo) {
+    static_assert(D >= 1 && D <= 4 && T >= 1 && T <= kMaxT, "paired LDS SA: d <= 4");
+    constexpr int DP1 = D + 1;
+    constexpr int MAXM = 32 / DP1;                 // members of C_{t-1} one half-wave can expand
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int lane = threadIdx.x;
+    const int h = lane >> 5, hl = lane & 31;
+    const u64 hmask = h ? 0xffffffff00000000ull : 0x00000000ffffffffull;
+    const u64 ltmask = (1ull << lane) - 1ull;
+    const int64_t r = blockIdx.x;
+    const int64_t col = r >> 6;
+    const u64 rbit = 1ull << (r & 63);
+    const int nw = geo.nw, lc = geo.lc;
+    uint16_t* rows = reinterpret_cast<uint16_t*>(smem);
+    uint32_t* lv = reinterpret_cast<uint32_t*>(smem + geo.off_lev);       // {level, marks A, marks B, -}
+    uint32_t* lev0s = reinterpret_cast<uint32_t*>(smem + geo.off_lev0);
+    uint32_t* mt = reinterpret_cast<uint32_t*>(smem + geo.off_mt);
+    uint32_t* lsth = reinterpret_cast<uint32_t*>(smem + geo.off_list) + h * (T + 1) * lc;   // this half's lists
+    const int32_t* g = adj + (st.rep_graph ? (int64_t)st.rep_graph[r] : 0) * n * D;
+    auto lword = [&](int t, int w) -> uint32_t& { return lv[4 * (t * nw + w)]; };
+    auto mword = [&](int t, int w, int pl) -> uint32_t& { return lv[4 * (t * nw + w) + 1 + pl]; };
+    // node v at level t as this half's proposal sees it, and A's mark on it
+    auto look = [&](int t, int v, uint32_t& val, uint32_t& amark) {
+        const uint4 x = *reinterpret_cast<const uint4*>(lv + 4 * (t * nw + (v >> 5)));
+        const int sh = v & 31;
+        val = ((x.x ^ (h ? x.z : x.y)) >> sh) & 1u;
+        amark = (x.y >> sh) & 1u;
+    };
+    auto nbrs = [&](int v, int (&o)[D]) {
+        const uint2 x = *reinterpret_cast<const uint2*>(rows + v * 4);
+        o[0] = (int)(x.x & 0xffffu);
+        if constexpr (D > 1) o[1] = (int)(x.x >> 16);
+        if constexpr (D > 2) o[2] = (int)(x.y & 0xffffu);
+        if constexpr (D > 3) o[3] = (int)(x.y >> 16);
+    };
+    auto maj = [&](int ones, uint32_t own) -> uint32_t {       // always-stay majority (code/SA_RRG.py:19-20)
+        return (2 * ones > D) ? 1u : ((2 * ones < D) ? 0u : own);
+    };
+    auto half_count = [&](bool x) -> int { return __popcll(__ballot(x) & hmask); };
+
+    // ---- launch setup
+    for (int64_t q = lane; q < n * D; q += 64) {
+        const int64_t v = q / D;
+        rows[v * 4 + (q - v * D)] = (uint16_t)g[q];
+    }
+    for (int k = lane; k < (T + 1) * nw * 4; k += 64) lv[k] = 0u;
+    wave_sync();
+    for (int64_t v0 = 0; v0 < (int64_t)nw * 32; v0 += 64) {
+        const int64_t v = v0 + lane;
+        const bool b = v < n && (s[v * W + col] & rbit);
+        const u64 m = __ballot(b);
+        if (lane < 2) {
+            const uint32_t x = (uint32_t)(m >> (32 * lane));
+            lword(0, (int)(v0 >> 5) + lane) = x;
+            lev0s[(v0 >> 5) + lane] = x;
+        }
+    }
+    for (int k = lane; k < MT_N; k += 64) mt[k] = st.mt[r * MT_N + k];
+    wave_sync();
+    for (int t = 1; t <= T; ++t) {
+        for (int64_t v0 = 0; v0 < (int64_t)nw * 32; v0 += 64) {
+            const int v = (int)(v0 + lane);
+            uint32_t nb = 0;
+            if (v < n) {
+                int nv[D];
+                nbrs(v, nv);
+                int ones = 0;
+#pragma unroll
+                for (int q = 0; q < D; ++q) ones += (int)((lword(t - 1, nv[q] >> 5) >> (nv[q] & 31)) & 1u);
+                nb = maj(ones, (lword(t - 1, v >> 5) >> (v & 31)) & 1u);
+            }
+            const u64 m = __ballot(nb != 0);
+            if (lane < 2) lword(t, (int)(v0 >> 5) + lane) = (uint32_t)(m >> (32 * lane));
+        }
+        wave_sync();
+    }
+
+    double a = st.a[r], b = st.b[r];
+    int64_t t = st.t[r], sum_end = st.sum_end[r];
+    int done = st.done[r];
+    int idx = st.mt_idx[r];
+    int ties = 0;
+    const uint32_t rng = (uint32_t)(n - 1);
+    uint32_t mask = rng;
+    mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+    double inv_n = 1.0 / (double)n;
+    asm volatile("" : "+v"(a), "+v"(b), "+v"(par_a), "+v"(par_b), "+v"(a_cap), "+v"(b_cap), "+v"(inv_n));
+
+    // ---- proposal windows: lane j holds proposal j
+    int pb_i = 0, pb_end = 0;
+    uint32_t pb_w1 = 0, pb_w2 = 0;
+    double pb_u = 0.0;
+    int npend = 0, pk = 0;
+    // append the proposals of stream windows at lanes npend..; with `one`, at
+    // most one window and no twist (a carried proposal's stream must not be
+    // twisted away under it)
+    auto parse = [&](bool one) {
+        for (;;) {
+            if (idx >= MT_N) {
+                if (one) break;
+                lds_twist(mt, lane);
+                idx = 0;
+            }
+            const int lim = (MT_N - idx < 64) ? MT_N - idx : 64;
+            uint32_t tw = 0, y = 0;
+            bool ok = false;
+            if (lane < lim) {
+                tw = mt_temper(mt[idx + lane]);
+                y = tw & mask;
+                ok = y <= rng;
+            }
+            const u64 okm = __ballot(ok);
+            int pos = 0, got = 0;
+            while (pos < 64 && npend < 64) {
+                const u64 m = okm >> pos;
+                if (!m) break;
+                const int f = pos + __ffsll((unsigned long long)m) - 1;
+                if (f + 2 >= lim) break;
+                const int iv = __builtin_amdgcn_readlane((int)y, f);
+                const uint32_t w1 = (uint32_t)__builtin_amdgcn_readlane((int)tw, f + 1);
+                const uint32_t w2 = (uint32_t)__builtin_amdgcn_readlane((int)tw, f + 2);
+                if (lane == npend) { pb_i = iv; pb_w1 = w1; pb_w2 = w2; pb_end = idx + f + 3; }
+                ++npend;
+                ++got;
+                pos = f + 3;
+            }
+            if (got > 0) { idx += pos; break; }
+            if (one) break;
+            if (!okm) { idx += lim; continue; }
+            const int f = __ffsll((unsigned long long)okm) - 1;
+            if (f > 0) { idx += f; continue; }
+            const int iv = __builtin_amdgcn_readlane((int)y, 0);
+            idx += 1;
+            if (idx >= MT_N) { lds_twist(mt, lane); idx = 0; }
+            const uint32_t w1 = mt_temper(mt[idx]);
+            idx += 1;
+            if (idx >= MT_N) { lds_twist(mt, lane); idx = 0; }
+            const uint32_t w2 = mt_temper(mt[idx]);
+            idx += 1;
+            if (lane == npend) { pb_i = iv; pb_w1 = w1; pb_w2 = w2; pb_end = idx; }
+            ++npend;
+            break;
+        }
+        pb_u = mt_double(pb_w1, pb_w2);
+    };
+    auto rl_double = [&](double x, int l) -> double {
+        const uint64_t bits = __builtin_bit_cast(uint64_t, x);
+        return __builtin_bit_cast(double, ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(bits >> 32), l) << 32) |
+                                              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bits, l));
+    };
+
+    // per level and candidate slot (a lane holds up to two candidates of its
+    // half: 2 x 32 lanes expand up to 2 (32 / (d+1)) members of C_{l-1})
+    int lc_c[T + 1][2];
+    uint32_t lc_v[T + 1][2];
+    bool lc_in[T + 1][2];
+    int lc_n[T + 1];
+    bool lc_fast[T + 1];
+    bool drew = false;
+    int64_t k = 0;
+#ifdef MJX_SA_PROF
+    unsigned long long _acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, _t0 = __builtin_amdgcn_s_memtime();
+#endif
+    while (k < nsteps && done == 0) {
+        const int avail = npend - pk;
+        if (avail == 1 && idx + 64 <= MT_N) {
+            // carry the leftover proposal to lane 0, append one window
+            const int ci = __builtin_amdgcn_readlane(pb_i, pk), ce = __builtin_amdgcn_readlane(pb_end, pk);
+            const uint32_t c1 = (uint32_t)__builtin_amdgcn_readlane((int)pb_w1, pk);
+            const uint32_t c2 = (uint32_t)__builtin_amdgcn_readlane((int)pb_w2, pk);
+            if (lane == 0) { pb_i = ci; pb_end = ce; pb_w1 = c1; pb_w2 = c2; }
+            npend = 1;
+            pk = 0;
+            parse(true);
+        } else if (avail == 0) {
+            npend = 0;
+            pk = 0;
+            parse(false);
+            if (npend == 1 && idx + 64 <= MT_N) parse(true);
+        }
+        drew = true;
+        const bool both = npend - pk >= 2 && k + 1 < nsteps;
+        const int iA = __builtin_amdgcn_readlane(pb_i, pk);
+        const int iB = both ? __builtin_amdgcn_readlane(pb_i, pk + 1) : iA;
+        const double uA = rl_double(pb_u, pk);
+        const double uB = both ? rl_double(pb_u, pk + 1) : uA;
+        const int iv = h ? iB : iA;
+        const double u = h ? uB : uA;
+        const bool act = h == 0 || both;
+        LDS_STAMP(0);
+        const uint32_t old_i = (lword(0, iv >> 5) >> (iv & 31)) & 1u;
+        bool conf = false;
+        // ---- level 1 (per half): i and its neighbours, level 0 with i flipped
+        int cand[2], nv[2][D];
+        int last;
+        {
+            int ri[D];
+            nbrs(iv, ri);
+            int c = iv;
+#pragma unroll
+            for (int q = 0; q < D; ++q)
+                if (hl == q + 1) c = ri[q];
+            bool dup = hl > 0 && c == iv;
+#pragma unroll
+            for (int q = 0; q < D; ++q)
+                if (q + 1 < hl) dup |= ri[q] == c;
+            nbrs(c, nv[0]);
+            const bool live = act && hl <= D && !dup;
+            int ones = 0;
+            bool hitA = c == iA;
+#pragma unroll
+            for (int e = 0; e < D; ++e) {
+                ones += (int)(((lword(0, nv[0][e] >> 5) >> (nv[0][e] & 31)) & 1u) ^ (nv[0][e] == iv));
+                hitA |= nv[0][e] == iA;
+            }
+            if (h == 1 && live && hitA) conf = true;
+            const uint32_t own = ((lword(0, c >> 5) >> (c & 31)) & 1u) ^ (c == iv);
+            const uint32_t nb = maj(ones, own);
+            const uint32_t cur = (lword(1, c >> 5) >> (c & 31)) & 1u;
+            const bool chg = live && nb != cur;
+            const u64 m = __ballot(chg);
+            if (chg) {
+                atomicOr(&mword(1, c >> 5, h), 1u << (c & 31));
+                lsth[lc + __popcll(m & hmask & ltmask)] = (uint32_t)c;
+            }
+            cand[0] = c;
+            cand[1] = iv;
+#pragma unroll
+            for (int e = 0; e < D; ++e) nv[1][e] = nv[0][e];
+            lc_c[1][0] = c;
+            lc_v[1][0] = cur;
+            lc_in[1][0] = chg;
+            lc_c[1][1] = iv;
+            lc_v[1][1] = 0u;
+            lc_in[1][1] = false;
+            lc_fast[1] = true;
+            lc_n[1] = __popcll(m & hmask);
+            last = lc_n[1] ? 1 : 0;
+        }
+        LDS_STAMP(1);
+        int64_t ds = 0;
+        if (T == 1 && last == 1) {
+            const bool in = lc_in[1][0];
+            ds = 2 * ((int64_t)half_count(in && lc_v[1][0] == 0u) - (int64_t)half_count(in && lc_v[1][0] != 0u));
+        }
+#pragma unroll
+        for (int l = 2; l <= T; ++l) {
+            lc_in[l][0] = lc_in[l][1] = false;
+            lc_c[l][0] = lc_c[l][1] = iv;
+            lc_v[l][0] = lc_v[l][1] = 0u;
+            lc_fast[l] = true;
+            lc_n[l] = 0;
+            const bool go = last == l - 1;
+            if (!__any(go)) break;
+            wave_sync();                                     // marks of C_{l-1} before they are read
+            const u64 pm0 = __ballot(lc_in[l - 1][0]) & hmask;
+            const u64 pm1 = __ballot(lc_in[l - 1][1]) & hmask;
+            const int np0 = __popcll(pm0);
+            const int np = lc_n[l - 1];
+            const bool prev2 = __any(pm1 != 0ull);           // members held in slot 1 too
+            int nc = 0;
+            if (go && np <= 2 * MAXM && lc_fast[l - 1]) {
+                const bool two = __any(go && np > MAXM);     // candidates in slot 1 too
+                int c2[2], nv2[2][D] = {};
+                uint32_t cur[2];
+                bool add[2];
+                int64_t dsl = 0;
+#pragma unroll
+                for (int sl = 0; sl < 2; ++sl) {
+                    add[sl] = false;
+                    cur[sl] = 0u;
+                    c2[sl] = iv;
+                    if (sl == 1 && !two) continue;
+                    // candidate q of this half: member q / (d+1) of C_{l-1} (slot-0
+                    // members first), j = q mod (d+1): 0 the member, else its j-th neighbour
+                    const int q = sl * 32 + hl;
+                    const int mi = q / DP1, j = q - mi * DP1;
+                    const bool act2 = mi < np;
+                    const bool in1 = mi >= np0;
+                    u64 x = in1 ? pm1 : pm0;
+                    const int rank = in1 ? mi - np0 : mi;
+                    for (int z = 0; z < rank && z < 32; ++z) x &= x - 1;
+                    const int src = act2 ? __ffsll((unsigned long long)x) - 1 : lane;
+                    int mc = __shfl(cand[0], src, 64);
+                    int pn[D];
+#pragma unroll
+                    for (int e = 0; e < D; ++e) pn[e] = __shfl(nv[0][e], src, 64);
+                    if (prev2) {
+                        const int mc1 = __shfl(cand[1], src, 64);
+                        int pn1[D];
+#pragma unroll
+                        for (int e = 0; e < D; ++e) pn1[e] = __shfl(nv[1][e], src, 64);
+                        if (in1) {
+                            mc = mc1;
+#pragma unroll
+                            for (int e = 0; e < D; ++e) pn[e] = pn1[e];
+                        }
+                    }
+                    int cc = mc;
+#pragma unroll
+                    for (int e = 0; e < D; ++e)
+                        if (j == e + 1) cc = pn[e];
+                    if (!act2) cc = iv;
+                    nbrs(cc, nv2[sl]);
+                    int ones = 0;
+                    uint32_t am = 0, val, mk;
+#pragma unroll
+                    for (int e = 0; e < D; ++e) {
+                        look(l - 1, nv2[sl][e], val, mk);
+                        ones += (int)val;
+                        am |= mk;
+                    }
+                    uint32_t own;
+                    look(l - 1, cc, own, mk);
+                    am |= mk;
+                    if (h == 1 && act2 && am) conf = true;
+                    const uint32_t nb = maj(ones, own);
+                    cur[sl] = (lword(l, cc >> 5) >> (cc & 31)) & 1u;
+                    const bool chg = act2 && nb != cur[sl];
+                    const uint32_t bit = 1u << (cc & 31);
+                    add[sl] = chg;
+                    if (l == T) {
+                        if (chg) add[sl] = (atomicOr(&mword(l, cc >> 5, h), bit) & bit) == 0u;
+                    } else if (chg) {
+                        atomicOr(&mword(l, cc >> 5, h), bit);
+                    }
+                    c2[sl] = cc;
+                }
+#pragma unroll
+                for (int sl = 0; sl < 2; ++sl) {
+                    const u64 m = __ballot(add[sl]) & hmask;
+                    if (add[sl]) lsth[l * lc + nc + __popcll(m & ltmask)] = (uint32_t)c2[sl];
+                    nc += __popcll(m);
+                    dsl += 2 * ((int64_t)__popcll(__ballot(add[sl] && cur[sl] == 0u) & hmask) -
+                                (int64_t)__popcll(__ballot(add[sl] && cur[sl] != 0u) & hmask));
+                    cand[sl] = c2[sl];
+#pragma unroll
+                    for (int e = 0; e < D; ++e) nv[sl][e] = nv2[sl][e];
+                    lc_c[l][sl] = c2[sl];
+                    lc_v[l][sl] = cur[sl];
+                    lc_in[l][sl] = add[sl];
+                }
+                if (l == T) ds = dsl;
+            } else if (go) {
+                // this half's LDS-list path (its lists hold every level; deduped here)
+                const uint32_t* prev = lsth + (l - 1) * lc;
+                uint32_t* curl = lsth + l * lc;
+                const int m = np * DP1;
+                int64_t dsl = 0;
+                for (int base = 0; base < m; base += 32) {
+                    const int q = base + hl;
+                    bool add = false;
+                    int cd = 0;
+                    uint32_t cur = 0;
+                    if (q < m) {
+                        const int slot = q / DP1, j = q - slot * DP1;
+                        const int v = (int)prev[slot];
+                        cd = (j == 0) ? v : (int)rows[v * 4 + j - 1];
+                        int nv2[D];
+                        nbrs(cd, nv2);
+                        int ones = 0;
+                        uint32_t am = 0, val, mk;
+#pragma unroll
+                        for (int e = 0; e < D; ++e) {
+                            look(l - 1, nv2[e], val, mk);
+                            ones += (int)val;
+                            am |= mk;
+                        }
+                        uint32_t own;
+                        look(l - 1, cd, own, mk);
+                        am |= mk;
+                        if (h == 1 && am) conf = true;
+                        const uint32_t nb = maj(ones, own);
+                        const uint32_t bit = 1u << (cd & 31);
+                        cur = (lword(l, cd >> 5) >> (cd & 31)) & 1u;
+                        if (nb != cur) add = (atomicOr(&mword(l, cd >> 5, h), bit) & bit) == 0u;
+                    }
+                    const u64 bal = __ballot(add) & hmask;
+                    if (add) curl[nc + __popcll(bal & ltmask)] = (uint32_t)cd;
+                    nc += __popcll(bal);
+                    dsl += 2 * ((int64_t)__popcll(__ballot(add && cur == 0u) & hmask) -
+                                (int64_t)__popcll(__ballot(add && cur != 0u) & hmask));
+                }
+                if (l == T) ds = dsl;
+                lc_fast[l] = false;
+            }
+            wave_sync();
+            if (go) {
+                lc_n[l] = nc;
+                if (nc > 0) last = l;
+            }
+            LDS_STAMP(l < 4 ? l : 4);
+        }
+        if (last != T) ds = 0;
+        // ---- delta_H and the Metropolis test of each half's proposal (code/SA_RRG.py:37,74-76)
+        const double aA = a, bA = b;
+        const double aB = (a < a_cap) ? par_a * a : a;               // the schedule after step A (:80-81)
+        const double bB = (b < b_cap) ? par_b * b : b;
+        const double ah = h ? aB : aA, bh = h ? bB : bA;
+        const double si = old_i ? 1.0 : -1.0;
+        const double t1 = (-2.0 * ah) * si;
+        const double t2 = bh * (double)(-ds);
+        const double num = t1 + t2;
+        const float xf = (float)(-num * inv_n);
+        const float ef = __expf(xf);
+        const float mg = ef * (1e-6f * (1.0f + fabsf(xf))) + 1e-37f;
+        bool acc, tie = false;
+        double dE = 0.0;
+        if (fabs(u - (double)ef) > (double)mg) {
+            acc = u < (double)ef;
+            if (TRACE && st.tr_dE) dE = num / (double)n;
+        } else {
+            dE = num / (double)n;
+            const double e = exp(-dE);
+            const double prob = (e < 1.0) ? e : 1.0;
+            acc = u < prob;
+            tie = e < 1.0 && fabs(u - e) <= 4.0 * (nextafter(e, 2.0) - e);
+        }
+        LDS_STAMP(5);
+        // ---- resolve: A first; B stands unless A is accepted and touched B's reads
+        const bool accA = __builtin_amdgcn_readlane((int)acc, 0) != 0;
+        const bool accB = __builtin_amdgcn_readlane((int)acc, 32) != 0;
+        const int64_t dsA = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)((uint64_t)ds >> 32), 0) << 32) |
+                                      (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ds, 0));
+        const int64_t dsB = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)((uint64_t)ds >> 32), 32) << 32) |
+                                      (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ds, 32));
+        const bool confB = (__ballot(conf) & 0xffffffff00000000ull) != 0ull;
+        const int64_t sumA = accA ? sum_end + dsA : sum_end;
+        const int64_t tA = t + 1;
+        const int doneA = (tA > t_cap) ? 2 : ((sumA == n) ? 1 : 0);             // (:84), m(s_endstate) == 1
+        const bool takeB = both && doneA == 0 && !(accA && confB);
+#ifdef MJX_SA_PROF
+        _acc[7] += (both ? 1000 : 0) + (takeB ? 1000000 : 0);   // pairs tried (x1e3), B taken (x1e6)
+#endif
+        ties += (__builtin_amdgcn_readlane((int)tie, 0) ? 1 : 0) + ((takeB && __builtin_amdgcn_readlane((int)tie, 32)) ? 1 : 0);
+        const bool mine = h ? (takeB && accB) : accA;
+        if (lane == 0 && accA) atomicXor(&lword(0, iA >> 5), 1u << (iA & 31));
+        if (lane == 32 && takeB && accB) atomicXor(&lword(0, iB >> 5), 1u << (iB & 31));
+#pragma unroll
+        for (int l = 1; l <= T; ++l) {
+            if (l <= last) {
+                if (lc_fast[l]) {
+#pragma unroll
+                    for (int sl = 0; sl < 2; ++sl) {
+                        if (lc_in[l][sl]) {
+                            const int v = lc_c[l][sl];
+                            const uint32_t bit = 1u << (v & 31);
+                            if (mine) {
+                                if (lc_v[l][sl]) atomicAnd(&lword(l, v >> 5), ~bit);
+                                else atomicOr(&lword(l, v >> 5), bit);
+                            }
+                            atomicAnd(&mword(l, v >> 5, h), ~bit);
+                        }
+                    }
+                } else {
+                    const uint32_t* cl = lsth + l * lc;
+                    for (int q = hl; q < lc_n[l]; q += 32) {
+                        const int v = (int)cl[q];
+                        const uint32_t bit = 1u << (v & 31);
+                        if (mine) atomicXor(&lword(l, v >> 5), bit);
+                        atomicAnd(&mword(l, v >> 5, h), ~bit);
+                    }
+                }
+            }
+        }
+        // step A (code/SA_RRG.py:77-84)
+        sum_end = sumA;
+        a = aB;
+        b = bB;
+        t = tA;
+        done = doneA;
+        if (TRACE && lane == 0) {
+            if (st.tr_i) st.tr_i[k * R + r] = iA;
+            if (st.tr_acc) st.tr_acc[k * R + r] = accA ? 1 : 0;
+            if (st.tr_sum) st.tr_sum[k * R + r] = sum_end;
+            if (st.tr_dE) st.tr_dE[k * R + r] = dE;
+        }
+        ++k;
+        ++pk;
+        if (takeB) {
+            if (accB) sum_end += dsB;
+            if (a < a_cap) a = par_a * a;
+            if (b < b_cap) b = par_b * b;
+            t += 1;
+            if (t > t_cap) done = 2;
+            else if (sum_end == n) done = 1;
+            if (TRACE && lane == 32) {
+                if (st.tr_i) st.tr_i[k * R + r] = iB;
+                if (st.tr_acc) st.tr_acc[k * R + r] = accB ? 1 : 0;
+                if (st.tr_sum) st.tr_sum[k * R + r] = sum_end;
+                if (st.tr_dE) st.tr_dE[k * R + r] = dE;
+            }
+            ++k;
+            ++pk;
+        }
+        wave_sync();
+        LDS_STAMP(6);
+    }
+#ifdef MJX_SA_PROF
+    if (lane == 0)
+        for (int q = 0; q < 8; ++q) atomicAdd(&mjx_sa_lds_prof[q], _acc[q]);
+#endif
+    if (drew) idx = __builtin_amdgcn_readlane(pb_end, pk - 1);
+    if (TRACE && lane == 0) {
+        for (; k < nsteps; ++k) {
+            if (st.tr_i) st.tr_i[k * R + r] = -1;
+            if (st.tr_acc) st.tr_acc[k * R + r] = -1;
+            if (st.tr_sum) st.tr_sum[k * R + r] = sum_end;
+            if (st.tr_dE) st.tr_dE[k * R + r] = 0.0;
+        }
+    }
+    for (int64_t v0 = 0; v0 < n; v0 += 64) {
+        const int v = (int)(v0 + lane);
+        if (v < n && (((lword(0, v >> 5) ^ lev0s[v >> 5]) >> (v & 31)) & 1u))
+            atomicXor((unsigned long long*)&s[(int64_t)v * W + col], (unsigned long long)rbit);
+    }
+    for (int q = lane; q < MT_N; q += 64) st.mt[r * MT_N + q] = mt[q];
+    if (lane == 0) {
+        st.mt_idx[r] = idx;
+        st.a[r] = a;
+        st.b[r] = b;
+        st.t[r] = t;
+        st.sum_end[r] = sum_end;
+        st.done[r] = done;
+        if (st.tr_tie) st.tr_tie[r] += ties;
+    }
+}
+
 }  // namespace salds
 }  // namespace mjx
 
@@ -841,7 +1394,7 @@ extern "C" int mjx_sa_lds_steps(const int32_t* adj, int64_t n, int d, int p, int
     if (!salds::geometry(n, d, T, &g)) return MJX_ERANGE;
     const mjx_sa_state st = *stp;
     if (!st.mt || !st.mt_idx || !st.a || !st.b || !st.t || !st.sum_end || !st.done) return MJX_EINVAL;
-    if (st.opt_flags & ~(MJX_SA_NO_SPEC | MJX_SA_NO_CONE2 | MJX_SA_LDS_SERIAL)) return MJX_EINVAL;
+    if (st.opt_flags & ~(MJX_SA_NO_SPEC | MJX_SA_NO_CONE2 | MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE)) return MJX_EINVAL;
     if (nsteps == 0) return MJX_OK;
     if (R > INT32_MAX) return MJX_ERANGE;
     const int64_t W = (R + 63) / 64;
@@ -854,6 +1407,29 @@ extern "C" int mjx_sa_lds_steps(const int32_t* adj, int64_t n, int d, int p, int
         MJX_LAUNCH_CHECK("k_sa_lds");
         return MJX_OK;
     };
+    salds::Geo g2;
+    if (!(st.opt_flags & (MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE)) && (d == 3 || d == 4) && T <= 4 &&
+        salds::geometry(n, d, T, &g2, 2)) {
+        auto gop = [&](auto kern) -> int {
+            MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, g2.bytes),
+                    "sa_lds lds");
+            kern<<<(unsigned)R, 64, (size_t)g2.bytes, hs>>>(adj, n, R, W, (u64*)s, st, nsteps, par_a, par_b, a_cap,
+                                                            b_cap, t_cap, g2);
+            MJX_LAUNCH_CHECK("k_sa_lds_pair");
+            return MJX_OK;
+        };
+        const bool trp = st.tr_i || st.tr_acc || st.tr_sum || st.tr_dE;
+#define MJX_LDS_PAIR(DD)                                                                                   \
+        switch (T) {                                                                                       \
+            case 1: return trp ? gop(salds::k_sa_lds_pair<DD, 1, true>) : gop(salds::k_sa_lds_pair<DD, 1, false>); \
+            case 2: return trp ? gop(salds::k_sa_lds_pair<DD, 2, true>) : gop(salds::k_sa_lds_pair<DD, 2, false>); \
+            case 3: return trp ? gop(salds::k_sa_lds_pair<DD, 3, true>) : gop(salds::k_sa_lds_pair<DD, 3, false>); \
+            default: return trp ? gop(salds::k_sa_lds_pair<DD, 4, true>) : gop(salds::k_sa_lds_pair<DD, 4, false>); \
+        }
+        if (d == 3) { MJX_LDS_PAIR(3) }
+        MJX_LDS_PAIR(4)
+#undef MJX_LDS_PAIR
+    }
     if (!(st.opt_flags & MJX_SA_LDS_SERIAL) && (d == 3 || d == 4) && T <= 4) {
         auto gof = [&](auto kern) -> int {
             MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, g.bytes),

@@ -37,17 +37,18 @@ def test_sa_init_draws_reference_s0(mjx_mod):
 def _sa(mjx_mod, N, p, c, seeds, mode):
     """mode: "lightcone" (HBM cone layout, default tape), "lightcone-notape"
     (draws inside the step kernel), "lightcone-tape7" (tape chunks of 7
-    steps), "lightcone-lds" (graph, levels and stream in LDS; "-ldsserial" the
-    list-based step), "lightcone-rec"
+    steps), "lightcone-lds" (graph, levels and stream in LDS, two proposals per
+    step; "-ldssingle" one, "-ldsserial" the list-based step), "lightcone-rec"
     (the cone with the adjacency rows in its records), "rollout"."""
     tape = {"lightcone-notape": 0, "lightcone-tape7": 7}.get(mode, 1024)
-    layout = {"lightcone-lds": "lds", "lightcone-ldsserial": "lds", "lightcone-rec": "rec"}.get(mode, "cone")
-    kernel = {"lds_serial": True} if mode == "lightcone-ldsserial" else None
+    layout = {"lightcone-lds": "lds", "lightcone-ldsserial": "lds", "lightcone-ldssingle": "lds",
+              "lightcone-rec": "rec"}.get(mode, "cone")
+    kernel = {"lightcone-ldsserial": {"lds_serial": True}, "lightcone-ldssingle": {"lds_single": True}}.get(mode)
     return mjx_mod.SAReplicas(N, p, c, seeds, mode=mode.split("-")[0], tape=tape, layout=layout, kernel=kernel)
 
 
-MODES = ["lightcone", "lightcone-notape", "lightcone-tape7", "lightcone-lds", "lightcone-ldsserial", "lightcone-rec",
-         "rollout"]
+MODES = ["lightcone", "lightcone-notape", "lightcone-tape7", "lightcone-lds", "lightcone-ldsserial",
+         "lightcone-ldssingle", "lightcone-rec", "rollout"]
 
 
 @pytest.mark.parametrize("mode", MODES)
@@ -245,10 +246,12 @@ def test_sa_run_independent_per_replica_graphs(mjx_mod):
         assert res["num_steps"][k] == o["num_steps"], k
 
 
-@pytest.mark.parametrize("d,p,c,serial", [(4, 3, 1, False), (4, 3, 1, True), (3, 2, 1, False), (4, 1, 1, False)])
-def test_sa_lds_stream_position_in_ragged_calls(mjx_mod, d, p, c, serial):
-    """The LDS-resident step parses the numpy stream 64 words at a time and
-    hands back the index after the last proposal it consumed: calls of
+@pytest.mark.parametrize("d,p,c,kern", [(4, 3, 1, None), (4, 3, 1, "lds_serial"), (4, 3, 1, "lds_single"),
+                                        (3, 2, 1, None), (4, 1, 1, None), (4, 1, 1, "lds_single")])
+def test_sa_lds_stream_position_in_ragged_calls(mjx_mod, d, p, c, kern):
+    """The LDS-resident steps parse the numpy stream 64 words at a time
+    (the paired step carries a leftover proposal into the next window) and
+    hand back the index after the last proposal consumed: calls of
     ragged lengths (1, 2, 3, 5, 7, ... steps) give the oracle's trace, and the
     MT19937 state after them equals numpy's RandomState after the same draws
     (binomial s0, then randint(0, n) and rand() per proposal,
@@ -256,7 +259,7 @@ def test_sa_lds_stream_position_in_ragged_calls(mjx_mod, d, p, c, serial):
     n, R = 300, 3
     graphs = [mjx_mod.random_regular_graph(d, n, seed=70 + g) for g in range(R)]
     seeds = [17, 18, 19]
-    kernel = {"lds_serial": True} if serial else None
+    kernel = {kern: True} if kern else None
     sa = mjx_mod.SAReplicas(graphs, p, c, seeds, layout="lds", kernel=kernel)
     got = {k: [] for k in ("i", "accept", "sum_end", "dE")}
     total = 0

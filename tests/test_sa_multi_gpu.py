@@ -40,6 +40,8 @@ def _check(tr, conf, t, graphs, graph_of, seeds, p, c, K, replicas):
     (6, 200, 2, 1, 20, 200, {}, "lightcone", "lds"),
     (5, 200, 2, 2, 20, 200, {}, "lightcone", "lds"),                        # runtime degree, T = 3
     (4, 300, 3, 1, 65, 300, {"lds_serial": True}, "lightcone", "lds"),     # the list-based LDS step
+    (4, 300, 3, 1, 65, 300, {"lds_single": True}, "lightcone", "lds"),     # one proposal per LDS step
+    (4, 64, 2, 2, 40, 400, {"lds_single": True}, "lightcone", "lds"),
     (3, 64, 2, 1, 40, 400, {}, "lightcone", "lds"),                         # small graph: many non-tree balls
     (4, 64, 2, 2, 40, 400, {}, "lightcone", "lds"),                         # T = 3, levels beyond one wave
     (4, 200, 1, 1, 5, 40, {}, "rollout", None),

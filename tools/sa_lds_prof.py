@@ -12,11 +12,12 @@ import mjx  # noqa: E402
 
 mjx.load_library()
 raw = ctypes.CDLL(mjx.lib_path())
-names = ["refill+proposal", "level 1", "level 2", "level 3", "level 4", "dE+exp+accept", "apply+trace"]
+names = ["refill+proposal", "level 1", "level 2", "level 3", "level 4", "dE+exp+accept", "apply+trace",
+         "pair code"]
 n, d, R = 10_000, 4, 64
 graphs = [mjx.random_regular_graph(d, n, seed=7000 + k) for k in range(R)]
-for (p, c) in ((1, 1), (3, 1)):
-    sa = mjx.SAReplicas(graphs, p, c, list(range(R)), layout="lds")
+for (p, c, kern) in ((1, 1, None), (3, 1, None), (3, 1, {"lds_single": True})):
+    sa = mjx.SAReplicas(graphs, p, c, list(range(R)), layout="lds", kernel=kern)
     K = 20000
     sa.steps(K)
     torch.cuda.synchronize()
@@ -27,7 +28,8 @@ for (p, c) in ((1, 1), (3, 1)):
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     raw.mjx_sa_lds_prof_read(buf, 1)
-    print(f"p={p} c={c}: {1e6 * el / K:.3f} us/step; cycles per step per wave: "
+    print(f"p={p} c={c} {kern or 'pair'}: {1e6 * el / K:.3f} us/step; cycles per step per wave: "
           + ", ".join(f"{nm} {buf[q] / R / K:.0f}" for q, nm in enumerate(names))
-          + f"; total {sum(buf[:8]) / R / K:.0f}", flush=True)
+          + f"; total {sum(buf[:7]) / R / K:.0f}; pairs tried {(buf[7] % 1000000) / 1000 / R / K:.3f}, "
+          f"second taken {(buf[7] // 1000000) / R / K:.3f} per step", flush=True)
     del sa
