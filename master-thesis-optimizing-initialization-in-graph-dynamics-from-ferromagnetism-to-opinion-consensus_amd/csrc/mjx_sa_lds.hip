@@ -828,8 +828,10 @@ __global__ void __launch_bounds__(64) k_sa_lds_fast(const int32_t* __restrict__ 
 // step's schedule value and its own ds only), so both are decided at once;
 // A's consequences (stop, t cap) are resolved first, then B is taken or
 // drawn again next step.  Proposal windows carry a leftover proposal into
-// the next window when no twist can fall between them.  Same draws, accepts
-// and state as k_sa_lds.
+// the next window when no twist can fall between them.  A half whose C_{l-1}
+// exceeds 32 / (d+1) members takes its LDS lists for the rest of the step
+// (3 % of the steps at p = 3; two candidate slots per lane instead measured
+// slower).  Same draws, accepts and state as k_sa_lds.
 template <int D, int T, bool TRACE>
 __global__ void __launch_bounds__(64) k_sa_lds_pair(const int32_t* __restrict__ adj, int64_t n, int64_t R,
                                                     int64_t W, u64* __restrict__ s, mjx_sa_state st, int64_t nsteps,
@@ -985,11 +987,9 @@ __global__ void __launch_bounds__(64) k_sa_lds_pair(const int32_t* __restrict__ 
                                               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bits, l));
     };
 
-    // per level and candidate slot (a lane holds up to two candidates of its
-    // half: 2 x 32 lanes expand up to 2 (32 / (d+1)) members of C_{l-1})
-    int lc_c[T + 1][2];
-    uint32_t lc_v[T + 1][2];
-    bool lc_in[T + 1][2];
+    int lc_c[T + 1];
+    uint32_t lc_v[T + 1];
+    bool lc_in[T + 1];
     int lc_n[T + 1];
     bool lc_fast[T + 1];
     bool drew = false;
@@ -1027,48 +1027,41 @@ __global__ void __launch_bounds__(64) k_sa_lds_pair(const int32_t* __restrict__ 
         const uint32_t old_i = (lword(0, iv >> 5) >> (iv & 31)) & 1u;
         bool conf = false;
         // ---- level 1 (per half): i and its neighbours, level 0 with i flipped
-        int cand[2], nv[2][D];
+        int cand, nv[D];
         int last;
         {
             int ri[D];
             nbrs(iv, ri);
-            int c = iv;
+            cand = iv;
 #pragma unroll
             for (int q = 0; q < D; ++q)
-                if (hl == q + 1) c = ri[q];
-            bool dup = hl > 0 && c == iv;
+                if (hl == q + 1) cand = ri[q];
+            bool dup = hl > 0 && cand == iv;
 #pragma unroll
             for (int q = 0; q < D; ++q)
-                if (q + 1 < hl) dup |= ri[q] == c;
-            nbrs(c, nv[0]);
+                if (q + 1 < hl) dup |= ri[q] == cand;
+            nbrs(cand, nv);
             const bool live = act && hl <= D && !dup;
             int ones = 0;
-            bool hitA = c == iA;
+            bool hitA = cand == iA;
 #pragma unroll
             for (int e = 0; e < D; ++e) {
-                ones += (int)(((lword(0, nv[0][e] >> 5) >> (nv[0][e] & 31)) & 1u) ^ (nv[0][e] == iv));
-                hitA |= nv[0][e] == iA;
+                ones += (int)(((lword(0, nv[e] >> 5) >> (nv[e] & 31)) & 1u) ^ (nv[e] == iv));
+                hitA |= nv[e] == iA;
             }
             if (h == 1 && live && hitA) conf = true;
-            const uint32_t own = ((lword(0, c >> 5) >> (c & 31)) & 1u) ^ (c == iv);
+            const uint32_t own = ((lword(0, cand >> 5) >> (cand & 31)) & 1u) ^ (cand == iv);
             const uint32_t nb = maj(ones, own);
-            const uint32_t cur = (lword(1, c >> 5) >> (c & 31)) & 1u;
+            const uint32_t cur = (lword(1, cand >> 5) >> (cand & 31)) & 1u;
             const bool chg = live && nb != cur;
             const u64 m = __ballot(chg);
             if (chg) {
-                atomicOr(&mword(1, c >> 5, h), 1u << (c & 31));
-                lsth[lc + __popcll(m & hmask & ltmask)] = (uint32_t)c;
+                atomicOr(&mword(1, cand >> 5, h), 1u << (cand & 31));
+                lsth[lc + __popcll(m & hmask & ltmask)] = (uint32_t)cand;
             }
-            cand[0] = c;
-            cand[1] = iv;
-#pragma unroll
-            for (int e = 0; e < D; ++e) nv[1][e] = nv[0][e];
-            lc_c[1][0] = c;
-            lc_v[1][0] = cur;
-            lc_in[1][0] = chg;
-            lc_c[1][1] = iv;
-            lc_v[1][1] = 0u;
-            lc_in[1][1] = false;
+            lc_c[1] = cand;
+            lc_v[1] = cur;
+            lc_in[1] = chg;
             lc_fast[1] = true;
             lc_n[1] = __popcll(m & hmask);
             last = lc_n[1] ? 1 : 0;
@@ -1076,107 +1069,77 @@ __global__ void __launch_bounds__(64) k_sa_lds_pair(const int32_t* __restrict__ 
         LDS_STAMP(1);
         int64_t ds = 0;
         if (T == 1 && last == 1) {
-            const bool in = lc_in[1][0];
-            ds = 2 * ((int64_t)half_count(in && lc_v[1][0] == 0u) - (int64_t)half_count(in && lc_v[1][0] != 0u));
+            const bool in = lc_in[1];
+            ds = 2 * ((int64_t)half_count(in && lc_v[1] == 0u) - (int64_t)half_count(in && lc_v[1] != 0u));
         }
 #pragma unroll
         for (int l = 2; l <= T; ++l) {
-            lc_in[l][0] = lc_in[l][1] = false;
-            lc_c[l][0] = lc_c[l][1] = iv;
-            lc_v[l][0] = lc_v[l][1] = 0u;
+            lc_in[l] = false;
             lc_fast[l] = true;
             lc_n[l] = 0;
             const bool go = last == l - 1;
             if (!__any(go)) break;
             wave_sync();                                     // marks of C_{l-1} before they are read
-            const u64 pm0 = __ballot(lc_in[l - 1][0]) & hmask;
-            const u64 pm1 = __ballot(lc_in[l - 1][1]) & hmask;
-            const int np0 = __popcll(pm0);
+            const u64 pm = __ballot(lc_in[l - 1]) & hmask;
             const int np = lc_n[l - 1];
-            const bool prev2 = __any(pm1 != 0ull);           // members held in slot 1 too
             int nc = 0;
-            if (go && np <= 2 * MAXM && lc_fast[l - 1]) {
-                const bool two = __any(go && np > MAXM);     // candidates in slot 1 too
-                int c2[2], nv2[2][D] = {};
-                uint32_t cur[2];
-                bool add[2];
-                int64_t dsl = 0;
+            if (go && np <= MAXM && lc_fast[l - 1]) {
+                // candidates: member s = hl / (d+1) of this half's C_{l-1} (its lane found
+                // by a scan of the mask), j = 0 the member itself, j > 0 its j-th neighbour
+                const int sl = hl / DP1, j = hl - sl * DP1;
+                int src = lane;
+                u64 x = pm;
+                for (int q = 0; q < np; ++q) {
+                    const int pbit = __ffsll((unsigned long long)x) - 1;
+                    if (q == sl) src = pbit;
+                    x &= x - 1;
+                }
+                const int mc = __shfl(cand, src, 64);
+                int pn[D];
 #pragma unroll
-                for (int sl = 0; sl < 2; ++sl) {
-                    add[sl] = false;
-                    cur[sl] = 0u;
-                    c2[sl] = iv;
-                    if (sl == 1 && !two) continue;
-                    // candidate q of this half: member q / (d+1) of C_{l-1} (slot-0
-                    // members first), j = q mod (d+1): 0 the member, else its j-th neighbour
-                    const int q = sl * 32 + hl;
-                    const int mi = q / DP1, j = q - mi * DP1;
-                    const bool act2 = mi < np;
-                    const bool in1 = mi >= np0;
-                    u64 x = in1 ? pm1 : pm0;
-                    const int rank = in1 ? mi - np0 : mi;
-                    for (int z = 0; z < rank && z < 32; ++z) x &= x - 1;
-                    const int src = act2 ? __ffsll((unsigned long long)x) - 1 : lane;
-                    int mc = __shfl(cand[0], src, 64);
-                    int pn[D];
+                for (int e = 0; e < D; ++e) pn[e] = __shfl(nv[e], src, 64);
+                const bool act2 = sl < np;
+                int c2 = mc;
 #pragma unroll
-                    for (int e = 0; e < D; ++e) pn[e] = __shfl(nv[0][e], src, 64);
-                    if (prev2) {
-                        const int mc1 = __shfl(cand[1], src, 64);
-                        int pn1[D];
+                for (int e = 0; e < D; ++e)
+                    if (j == e + 1) c2 = pn[e];
+                if (!act2) c2 = iv;
+                int nv2[D];
+                nbrs(c2, nv2);
+                int ones = 0;
+                uint32_t am = 0, val;
 #pragma unroll
-                        for (int e = 0; e < D; ++e) pn1[e] = __shfl(nv[1][e], src, 64);
-                        if (in1) {
-                            mc = mc1;
-#pragma unroll
-                            for (int e = 0; e < D; ++e) pn[e] = pn1[e];
-                        }
-                    }
-                    int cc = mc;
-#pragma unroll
-                    for (int e = 0; e < D; ++e)
-                        if (j == e + 1) cc = pn[e];
-                    if (!act2) cc = iv;
-                    nbrs(cc, nv2[sl]);
-                    int ones = 0;
-                    uint32_t am = 0, val, mk;
-#pragma unroll
-                    for (int e = 0; e < D; ++e) {
-                        look(l - 1, nv2[sl][e], val, mk);
-                        ones += (int)val;
-                        am |= mk;
-                    }
-                    uint32_t own;
-                    look(l - 1, cc, own, mk);
+                for (int e = 0; e < D; ++e) {
+                    uint32_t mk;
+                    look(l - 1, nv2[e], val, mk);
+                    ones += (int)val;
                     am |= mk;
-                    if (h == 1 && act2 && am) conf = true;
-                    const uint32_t nb = maj(ones, own);
-                    cur[sl] = (lword(l, cc >> 5) >> (cc & 31)) & 1u;
-                    const bool chg = act2 && nb != cur[sl];
-                    const uint32_t bit = 1u << (cc & 31);
-                    add[sl] = chg;
-                    if (l == T) {
-                        if (chg) add[sl] = (atomicOr(&mword(l, cc >> 5, h), bit) & bit) == 0u;
-                    } else if (chg) {
-                        atomicOr(&mword(l, cc >> 5, h), bit);
-                    }
-                    c2[sl] = cc;
                 }
-#pragma unroll
-                for (int sl = 0; sl < 2; ++sl) {
-                    const u64 m = __ballot(add[sl]) & hmask;
-                    if (add[sl]) lsth[l * lc + nc + __popcll(m & ltmask)] = (uint32_t)c2[sl];
-                    nc += __popcll(m);
-                    dsl += 2 * ((int64_t)__popcll(__ballot(add[sl] && cur[sl] == 0u) & hmask) -
-                                (int64_t)__popcll(__ballot(add[sl] && cur[sl] != 0u) & hmask));
-                    cand[sl] = c2[sl];
-#pragma unroll
-                    for (int e = 0; e < D; ++e) nv[sl][e] = nv2[sl][e];
-                    lc_c[l][sl] = c2[sl];
-                    lc_v[l][sl] = cur[sl];
-                    lc_in[l][sl] = add[sl];
+                uint32_t own, mk;
+                look(l - 1, c2, own, mk);
+                am |= mk;
+                if (h == 1 && act2 && am) conf = true;
+                const uint32_t nb = maj(ones, own);
+                const uint32_t cur = (lword(l, c2 >> 5) >> (c2 & 31)) & 1u;
+                const bool chg = act2 && nb != cur;
+                const uint32_t bit = 1u << (c2 & 31);
+                bool add = chg;
+                if (l == T) {
+                    if (chg) add = (atomicOr(&mword(l, c2 >> 5, h), bit) & bit) == 0u;
+                } else if (chg) {
+                    atomicOr(&mword(l, c2 >> 5, h), bit);
                 }
-                if (l == T) ds = dsl;
+                const u64 m = __ballot(add);
+                if (add) lsth[l * lc + __popcll(m & hmask & ltmask)] = (uint32_t)c2;
+                nc = __popcll(m & hmask);
+                cand = c2;
+#pragma unroll
+                for (int e = 0; e < D; ++e) nv[e] = nv2[e];
+                lc_c[l] = c2;
+                lc_v[l] = cur;
+                lc_in[l] = add;
+                if (l == T) ds = 2 * ((int64_t)__popcll(__ballot(add && cur == 0u) & hmask) -
+                                      (int64_t)__popcll(__ballot(add && cur != 0u) & hmask));
             } else if (go) {
                 // this half's LDS-list path (its lists hold every level; deduped here)
                 const uint32_t* prev = lsth + (l - 1) * lc;
@@ -1276,17 +1239,14 @@ __global__ void __launch_bounds__(64) k_sa_lds_pair(const int32_t* __restrict__ 
         for (int l = 1; l <= T; ++l) {
             if (l <= last) {
                 if (lc_fast[l]) {
-#pragma unroll
-                    for (int sl = 0; sl < 2; ++sl) {
-                        if (lc_in[l][sl]) {
-                            const int v = lc_c[l][sl];
-                            const uint32_t bit = 1u << (v & 31);
-                            if (mine) {
-                                if (lc_v[l][sl]) atomicAnd(&lword(l, v >> 5), ~bit);
-                                else atomicOr(&lword(l, v >> 5), bit);
-                            }
-                            atomicAnd(&mword(l, v >> 5, h), ~bit);
+                    if (lc_in[l]) {
+                        const int v = lc_c[l];
+                        const uint32_t bit = 1u << (v & 31);
+                        if (mine) {
+                            if (lc_v[l]) atomicAnd(&lword(l, v >> 5), ~bit);
+                            else atomicOr(&lword(l, v >> 5), bit);
                         }
+                        atomicAnd(&mword(l, v >> 5, h), ~bit);
                     }
                 } else {
                     const uint32_t* cl = lsth + l * lc;

@@ -198,18 +198,13 @@ def gen_sa_full():
     for (n, d, p, gseed, nseed, nstat) in ((200, 4, 3, 1, 0, 1), (300, 3, 2, 2, 5, 1), (200, 4, 3, 3, 11, 2)):
         tmp = tempfile.mktemp(suffix=".npz")
         s = src
-        for old, new in (("n=10000", f"n={n}"), ("d=4", f"d={d}"), ("p=3", f"p={p}"), ("c=1 ", "c=1 "),
-                         ("N_stat=5", f"N_stat={nstat}")):
+        # c stays the script's c=1 in every run
+        for old, new in (("n=10000", f"n={n}"), ("d=4", f"d={d}"), ("p=3", f"p={p}"), ("N_stat=5", f"N_stat={nstat}")):
             assert old in s, old
             s = s.replace(old, new, 1)
-        if p == 2:
-            pass
         s = s.replace('#np.savez("MCMC_p3_d4.npz"', f'np.savez("{tmp}"')
         s = s.replace("for k in range(N_stat):", f"random.seed({gseed}); np.random.seed({nseed})\nfor k in range(N_stat):")
         s = "import random\n" + s
-        if d == 3:
-            # p+c for d=3 case: c stays 1 (p=2, c=1)
-            pass
         g = {"__name__": "ref_sa_full"}
         exec(compile(s, SA_PATH, "exec"), g)
         z = np.load(tmp)
