@@ -419,8 +419,8 @@ def bench_sa_consensus(args, rank, world, dist, dev):
         proposals per replica): wall time to consensus, the num_steps /
         mag_reached distributions (the script's np.savez keys);
       * script_size: the script's n = 1e4 for a fixed wall budget: there the
-        runs need 4.4e7 to >3.2e8 proposals per replica (round 3, 900 s on 64
-        replicas: 38 done, profiles/r03_sa_consensus_n1e4.log), so this
+        runs need 4.4e7 to >5.8e8 proposals per replica (round 3, 1000 s on 64
+        replicas: 50 done, profiles/r03_sa_consensus_n1e4_pair.log), so this
         reports the rate and how far the runs got."""
     import mjx
     d, p, c, R = 4, 3, 1, args.consensus_replicas

@@ -1,0 +1,4 @@
+#!/bin/bash
+# round 3, GPU session 23: record at HEAD after the LDS SA work — every -m gpu test, smoke, bench, kernel trace
+set -o pipefail
+STEPS="tests smoke bench prof" bash tools/gpu_check.sh || exit $?
