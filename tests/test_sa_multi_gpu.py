@@ -42,6 +42,9 @@ def _check(tr, conf, t, graphs, graph_of, seeds, p, c, K, replicas):
     (4, 300, 3, 1, 65, 300, {"lds_serial": True}, "lightcone", "lds"),     # the list-based LDS step
     (4, 300, 3, 1, 65, 300, {"lds_single": True}, "lightcone", "lds"),     # one proposal per LDS step
     (4, 64, 2, 2, 40, 400, {"lds_single": True}, "lightcone", "lds"),
+    (4, 150, 3, 2, 20, 300, {}, "lightcone", "lds"),                        # T = 4, pair and single
+    (4, 150, 3, 2, 20, 300, {"lds_single": True}, "lightcone", "lds"),
+    (3, 200, 2, 3, 20, 300, {}, "lightcone", "lds"),
     (3, 64, 2, 1, 40, 400, {}, "lightcone", "lds"),                         # small graph: many non-tree balls
     (4, 64, 2, 2, 40, 400, {}, "lightcone", "lds"),                         # T = 3, levels beyond one wave
     (4, 200, 1, 1, 5, 40, {}, "rollout", None),
