@@ -326,6 +326,16 @@ int mjx_hpr_new_biases(int dtype, void* biases, const void* marg, const double* 
  * nonzero = refresh node i's biases). */
 int mjx_hpr_new_biases_mask(int dtype, void* biases, const void* marg, const uint8_t* refresh, double pie,
                             int64_t n, int32_t* s, void* stream);
+
+/* One node step of the HPR main loop in one launch (code/HPR_pytorch_RRG.py:
+ * 147-167 node part, 137-145, and the bit packing of s for :352): node
+ * marginals from the edge Z sums in zwork (mjx_hpr_marginals_q with marg =
+ * NULL computes only those), the bias refresh where refresh[v] (as
+ * mjx_hpr_new_biases_mask), s[v] = +-1 and its node-packed bits (as
+ * mjx_pack_np).  Replaces mjx_hpr_marginals' node part + new_biases_mask +
+ * pack_np; same values. */
+int mjx_hpr_node_step(int dtype, const void* zwork, const int32_t* out_row, int64_t n, int d, void* marg,
+                      void* biases, const uint8_t* refresh, double pie, int32_t* s, uint64_t* bits, void* stream);
 /* The reference's torch.rand(n) per iteration (torch's CPU generator, :142) on the
  * device: state[624] (uint32) and left_next[2] = the CPU engine's `left`, `next`
  * (its get_state() fields); k iterations of n float64 uniforms u = ((y_hi<<32 |
@@ -376,7 +386,8 @@ int mjx_hpr_node_biases(int dtype, const void* src, const int64_t* idx, int64_t 
  * layout with the invalid-sender entries times scale.  mjx_hpr_update_q: HPr_dp on
  * the decay-split layout, *scale_in = chi_in's scale (dtype); chi_out's IV and II
  * quadrants are not written (they must already hold chi_0).  mjx_hpr_marginals_q:
- * marginals_comp of a decay-split chi with scale *scale. */
+ * marginals_comp of a decay-split chi with scale *scale (marg = NULL: only the
+ * edge Z sums into zwork, for mjx_hpr_node_step). */
 int mjx_hpr_q_supported(int dtype, int d, int p, int c);
 int mjx_hpr_qlayout(int dtype, const void* src, void* dst, int64_t rows, int p, int c, int attr_value, int to_q,
                     double scale, void* stream);

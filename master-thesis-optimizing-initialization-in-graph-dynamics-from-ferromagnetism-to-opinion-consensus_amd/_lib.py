@@ -66,6 +66,7 @@ SIGNATURES = {
     "mjx_hpr_marginals": [c_int, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_dbl, c_vp, c_vp, c_vp],
     "mjx_hpr_new_biases": [c_int, c_vp, c_vp, c_vp, c_dbl, c_dbl, c_i64, c_vp, c_vp],
     "mjx_hpr_new_biases_mask": [c_int, c_vp, c_vp, c_vp, c_dbl, c_i64, c_vp, c_vp],
+    "mjx_hpr_node_step": [c_int, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp, c_dbl, c_vp, c_vp, c_vp],
     "mjx_hpr_refresh_masks": [c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp],
     "mjx_mt_jump_geometry": [c_i64, c_int, c_int, c_vp, c_vp],
     "mjx_mt_jump_table_words": [c_i64, c_int, c_int],

@@ -87,6 +87,29 @@ extern "C" int mjx_hpr_new_biases(int dtype, void* biases, const void* marg, con
     return MJX_OK;
 }
 
+extern "C" int mjx_hpr_node_step(int dtype, const void* zwork, const int32_t* out_row, int64_t n, int d, void* marg,
+                                 void* biases, const uint8_t* refresh, double pie, int32_t* s, uint64_t* bits,
+                                 void* stream) {
+    if (n < 1 || d < 1 || !zwork || !out_row || !marg || !biases || !refresh || !s || !bits) return MJX_EINVAL;
+    if ((n * (int64_t)d) % 2) return MJX_EINVAL;
+    const int64_t E = n * (int64_t)d / 2;
+    hipStream_t st = as_stream(stream);
+    const unsigned grid = (unsigned)((n + 255) / 256);
+    if (dtype == MJX_F32) {
+        const float* zp = (const float*)zwork;
+        k_hpr_node_step<float><<<grid, 256, 0, st>>>(zp, zp + 2 * E, out_row, n, d, (float*)marg, (float*)biases,
+                                                     refresh, (float)pie, s, (u64*)bits);
+    } else if (dtype == MJX_F64) {
+        const double* zp = (const double*)zwork;
+        k_hpr_node_step<double><<<grid, 256, 0, st>>>(zp, zp + 2 * E, out_row, n, d, (double*)marg, (double*)biases,
+                                                      refresh, pie, s, (u64*)bits);
+    } else {
+        return MJX_EINVAL;
+    }
+    MJX_LAUNCH_CHECK("k_hpr_node_step");
+    return MJX_OK;
+}
+
 extern "C" int mjx_hpr_new_biases_mask(int dtype, void* biases, const void* marg, const uint8_t* refresh,
                                        double pie, int64_t n, int32_t* s, void* stream) {
     if (n < 1 || !biases || !marg || !refresh) return MJX_EINVAL;
@@ -199,6 +222,7 @@ static int marginals_q_impl(const void* chi, const int32_t* out_row, int64_t n, 
     }
 #undef MJX_EDGE_ZQ
     MJX_LAUNCH_CHECK("k_hpr_edge_z_q");
+    if (!marg) return MJX_OK;                 // the edge sums only (mjx_hpr_node_step follows)
     k_hpr_node_marg<S><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(zp, zm, out_row, n, d, (S*)marg);
     MJX_LAUNCH_CHECK("k_hpr_node_marg");
     return MJX_OK;
@@ -207,7 +231,7 @@ static int marginals_q_impl(const void* chi, const int32_t* out_row, int64_t n, 
 extern "C" int mjx_hpr_marginals_q(int dtype, const void* chi, const int32_t* out_row, int64_t n, int d, int p, int c,
                                    double eps, const void* scale, const void* ii, void* zwork, void* marg,
                                    void* stream) {
-    if (n < 1 || d < 1 || p < 1 || c < 1 || !chi || !out_row || !scale || !zwork || !marg) return MJX_EINVAL;
+    if (n < 1 || d < 1 || p < 1 || c < 1 || !chi || !out_row || !scale || !zwork) return MJX_EINVAL;
     if ((n * (int64_t)d) % 2) return MJX_EINVAL;
     hipStream_t st = as_stream(stream);
     if (dtype == MJX_F32) return marginals_q_impl<float>(chi, out_row, n, d, p + c, eps, scale, ii, zwork, marg, st);

@@ -913,6 +913,46 @@ __global__ void __launch_bounds__(256) k_hpr_new_biases_mask(S* __restrict__ bia
     if (s) s[i] = b0 > b1 ? 1 : -1;
 }
 
+// One node step of the main loop (code/HPR_pytorch_RRG.py:147-167 node part,
+// 137-145, and the packing of s for s_endstate at :352): the node marginal from
+// the edge Z sums (as k_hpr_node_marg), the bias refresh with the host- or
+// device-made decision (as k_hpr_new_biases_mask), the trial configuration s,
+// and s bit-packed for the rollout (bit = 1 <=> s = +1, one ballot per 64
+// nodes) -- three launches of the loop in one.
+template <typename S>
+__global__ void __launch_bounds__(256) k_hpr_node_step(const S* __restrict__ zp, const S* __restrict__ zm,
+                                                        const int32_t* __restrict__ out_row, int64_t n, int d,
+                                                        S* __restrict__ marg, S* __restrict__ biases,
+                                                        const uint8_t* __restrict__ refresh, S pie,
+                                                        int32_t* __restrict__ s, u64* __restrict__ bits) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    bool plus = false;
+    if (i < n) {
+        S p = 1, q = 1;
+        for (int m = 0; m < d; ++m) {
+            const int64_t r = out_row[i * d + m];
+            p *= zp[r];
+            q *= zm[r];
+        }
+        const S sum = p + q;
+        const S m0 = p / sum, m1 = q / sum;
+        marg[2 * i] = m0;
+        marg[2 * i + 1] = m1;
+        S b0 = biases[2 * i], b1 = biases[2 * i + 1];
+        if (refresh[i]) {
+            const bool minus = m1 >= m0;
+            b0 = minus ? pie : S(1) - pie;
+            b1 = minus ? S(1) - pie : pie;
+            biases[2 * i] = b0;
+            biases[2 * i + 1] = b1;
+        }
+        plus = b0 > b1;
+        s[i] = plus ? 1 : -1;
+    }
+    const u64 w = __ballot(plus);
+    if ((threadIdx.x & 63) == 0 && i < n) bits[i >> 6] = w;
+}
+
 // ---- dispatch --------------------------------------------------------------
 template <typename S, int T, int P, int D>
 static int launch_update(const void* chi_in, void* chi_out, const void* biases, const int32_t* nbr,

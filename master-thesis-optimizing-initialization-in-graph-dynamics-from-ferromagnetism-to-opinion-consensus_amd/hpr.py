@@ -253,9 +253,10 @@ class HPRState:
                   self.p, self.c, self.attr_value, 0, self.decay(self.t), _device.stream_handle())
         return out
 
-    def _update(self, src, dst, sc_in=None, sc_out=None):
+    def _update(self, src, dst, sc_in=None, sc_out=None, node=True):
         """HPr_dp src -> dst and marginals_comp(dst) (scales: device pointers,
-        decay-split layout)."""
+        decay-split layout; ``node=False``: only the edge Z sums of the
+        marginals, the node part left to mjx_hpr_node_step)."""
         st = _device.stream_handle()
         if self.layout == "q":
             plan = self.plan
@@ -266,7 +267,7 @@ class HPRState:
                       self.damppar, sc_in, st)
             _lib.call("mjx_hpr_marginals_q", _code(self.dtype), _device.ptr(dst), _device.ptr(plan.out_row), plan.n,
                       plan.d, self.p, self.c, 1e-15, sc_out, _device.ptr(self._ii), _device.ptr(self.zwork),
-                      _device.ptr(self.marg), st)
+                      _device.ptr(self.marg) if node else None, st)
         else:
             HPr_dp(src, self.biases, self.plan, self.p, self.c, self.attr_value, self.lmbd_in, self.damppar, out=dst)
             marginals_comp(dst, self.plan, self.p, self.c, zwork=self.zwork, out=self.marg)
@@ -313,13 +314,20 @@ class HPRState:
         n, T, st = self.plan.n, self.p + self.c - 1, _device.stream_handle()
         self._cnt.zero_()
         sz = self._scales.element_size()
+        q = self.layout == "q" and getattr(self, "fuse_node", True)
         for j in range(k):
             src, dst = (self.chi, self.chi_b) if j % 2 == 0 else (self.chi_b, self.chi)
             # decay-split layout: row j of self._scales is (1-damp)^(t+j), set before each replay
-            self._update(src, dst, self._scales.data_ptr() + j * sz, self._scales.data_ptr() + (j + 1) * sz)
-            _lib.call("mjx_hpr_new_biases_mask", _code(self.dtype), _device.ptr(self.biases), _device.ptr(self.marg),
-                      _device.ptr(self._mask[j]), self.pie, n, _device.ptr(self._s_hist[j]), st)
-            _lib.call("mjx_pack_np", _device.ptr(self._s_hist[j]), _lib.MJX_I32, n, _device.ptr(self._bits), st)
+            self._update(src, dst, self._scales.data_ptr() + j * sz, self._scales.data_ptr() + (j + 1) * sz, node=not q)
+            if q:
+                # node marginals, new_biases_i and the packed trial configuration in one launch
+                _lib.call("mjx_hpr_node_step", _code(self.dtype), _device.ptr(self.zwork), _device.ptr(self.plan.out_row),
+                          n, self.plan.d, _device.ptr(self.marg), _device.ptr(self.biases), _device.ptr(self._mask[j]),
+                          self.pie, _device.ptr(self._s_hist[j]), _device.ptr(self._bits), st)
+            else:
+                _lib.call("mjx_hpr_new_biases_mask", _code(self.dtype), _device.ptr(self.biases), _device.ptr(self.marg),
+                          _device.ptr(self._mask[j]), self.pie, n, _device.ptr(self._s_hist[j]), st)
+                _lib.call("mjx_pack_np", _device.ptr(self._s_hist[j]), _lib.MJX_I32, n, _device.ptr(self._bits), st)
             if T:
                 rollout(self.plan.graph, self._bits, T, out=self._rtmp[0], tmp=self._rtmp[1],
                         counts=self._cnt[j:j + 1])

@@ -104,7 +104,8 @@ def test_q_equals_ref_layout_at_c3_size(mjx_mod):
 
 
 def test_q_graph_batches_equal_eager(mjx_mod):
-    """hipGraph-replayed batches of the q layout equal the eager steps bit for bit."""
+    """hipGraph-replayed batches of the q layout (node step fused into one
+    launch) equal the eager steps bit for bit."""
     n, d, p, c = 2000, 3, 3, 1
     plan, mk = _pair(mjx_mod, n, d, p, c, seed=7)
     a, b = mk("q"), mk("q")
@@ -114,6 +115,8 @@ def test_q_graph_batches_equal_eager(mjx_mod):
     want = [b.step(generator=gb) for _ in range(12)]
     assert a.t == b.t == 12
     assert torch.equal(a.messages(), b.messages())
+    # the batches' fused node step (mjx_hpr_node_step) vs marginals + new_biases_i
+    assert torch.equal(a.biases, b.biases) and torch.equal(a.marg, b.marg) and torch.equal(a.s, b.s)
     assert int(sums[-1]) == want[-1]
 
 
