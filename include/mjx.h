@@ -179,13 +179,14 @@ typedef struct mjx_sa_state {
      * set them; nothing is read from the environment) */
     int32_t   opt_split;   /* waves per 64-replica word column: 1, 2, 4, ..., 64 */
     int32_t   opt_spec_k;  /* speculative batch width: 8 or 16 */
-    uint32_t  opt_flags;   /* MJX_SA_NO_SPEC | MJX_SA_NO_CONE2 | MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE */
+    uint32_t  opt_flags;   /* MJX_SA_NO_SPEC | MJX_SA_NO_CONE2 | MJX_SA_LDS_* */
 } mjx_sa_state;
 
 #define MJX_SA_NO_SPEC   1u   /* no speculative batches (k_sa_spec) */
 #define MJX_SA_NO_CONE2  2u   /* no one-round-trip step (k_sa_cone2) */
 #define MJX_SA_LDS_SERIAL 4u  /* LDS layout: the list-based step (k_sa_lds), not the lane-held one */
 #define MJX_SA_LDS_SINGLE 8u  /* LDS layout: one proposal per step (k_sa_lds_fast), not two (k_sa_lds_pair) */
+#define MJX_SA_LDS_PAIR  16u  /* LDS layout at p+c-1 = 1: two proposals per step, not eight (k_sa_lds_multi) */
 
 /* Seed replica r with seeds[r] (device uint32[R]), draw s0 into the
  * replica-packed spins s[n*W], set a=a0, b=b0, t=0, done=0, and

@@ -127,7 +127,7 @@ class MjxSaState(ctypes.Structure):
     ]
 
 
-MJX_SA_NO_SPEC, MJX_SA_NO_CONE2, MJX_SA_LDS_SERIAL, MJX_SA_LDS_SINGLE = 1, 2, 4, 8   # mjx_sa_state.opt_flags (include/mjx.h)
+MJX_SA_NO_SPEC, MJX_SA_NO_CONE2, MJX_SA_LDS_SERIAL, MJX_SA_LDS_SINGLE, MJX_SA_LDS_PAIR = 1, 2, 4, 8, 16  # opt_flags (include/mjx.h)
 
 
 class MjxError(RuntimeError):

@@ -2027,7 +2027,8 @@ static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d
     const int split = st.opt_split ? st.opt_split : lc_split(W, lds);
     if (split < 1 || split > 64 || (64 % split)) return MJX_EINVAL;
     if (st.opt_spec_k != 0 && st.opt_spec_k != 8 && st.opt_spec_k != 16) return MJX_EINVAL;
-    if (st.opt_flags & ~(MJX_SA_NO_SPEC | MJX_SA_NO_CONE2 | MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE)) return MJX_EINVAL;
+    if (st.opt_flags & ~(MJX_SA_NO_SPEC | MJX_SA_NO_CONE2 | MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE | MJX_SA_LDS_PAIR))
+        return MJX_EINVAL;
     // the one-trip and speculative kernels address a word column's cone slab
     // with 32-bit byte offsets (ConeRd)
     const bool slab32 = L.s0c && n * L.ns * 8 < (int64_t(1) << 31);

@@ -87,7 +87,7 @@ static bool geometry(int64_t n, int d, int T, Geo* g, int planes = 1) {
     g->off_lev0 = (int)off;  off += (int64_t)g->nw * 4;
     g->off_mt = (int)off;    off += MT_N * 4;
     g->off_list = (int)off;  off += (int64_t)planes * (T + 1) * g->lc * 4;
-    g->off_cnt = (int)off;   off += 16 * 4;
+    g->off_cnt = (int)off;   off += 32 * 4;
     g->bytes = (int)off;
     return (size_t)off <= kLdsMax;
 }
@@ -918,6 +918,22 @@ __global__ void __launch_bounds__(64) k_sa_lds_pair(const int32_t* __restrict__ 
     int done = st.done[r];
     int idx = st.mt_idx[r];
     int ties = 0;
+    // the pointers the write-back needs are parked in LDS for the steps: kept in
+    // scalar registers across the loop they spilled into VGPR lanes (restored by
+    // readlanes every step)
+    u64* park = reinterpret_cast<u64*>(smem + geo.off_cnt);
+    if (lane == 0) {
+        park[0] = (u64)s;
+        park[1] = (u64)st.mt;
+        park[2] = (u64)st.mt_idx;
+        park[3] = (u64)st.a;
+        park[4] = (u64)st.b;
+        park[5] = (u64)st.t;
+        park[6] = (u64)st.sum_end;
+        park[7] = (u64)st.done;
+        park[8] = (u64)st.tr_tie;
+        park[9] = (u64)W;
+    }
     const uint32_t rng = (uint32_t)(n - 1);
     uint32_t mask = rng;
     mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
@@ -1305,20 +1321,356 @@ __global__ void __launch_bounds__(64) k_sa_lds_pair(const int32_t* __restrict__ 
             if (st.tr_dE) st.tr_dE[k * R + r] = 0.0;
         }
     }
+    wave_sync();
+    u64* const ps = (u64*)park[0];
+    const int64_t Wp = (int64_t)park[9];
+    const int64_t rr = blockIdx.x;
     for (int64_t v0 = 0; v0 < n; v0 += 64) {
         const int v = (int)(v0 + lane);
         if (v < n && (((lword(0, v >> 5) ^ lev0s[v >> 5]) >> (v & 31)) & 1u))
-            atomicXor((unsigned long long*)&s[(int64_t)v * W + col], (unsigned long long)rbit);
+            atomicXor((unsigned long long*)&ps[(int64_t)v * Wp + (rr >> 6)], 1ull << (rr & 63));
     }
-    for (int q = lane; q < MT_N; q += 64) st.mt[r * MT_N + q] = mt[q];
+    uint32_t* const pmt = (uint32_t*)park[1];
+    for (int q = lane; q < MT_N; q += 64) pmt[rr * MT_N + q] = mt[q];
     if (lane == 0) {
-        st.mt_idx[r] = idx;
-        st.a[r] = a;
-        st.b[r] = b;
-        st.t[r] = t;
-        st.sum_end[r] = sum_end;
-        st.done[r] = done;
-        if (st.tr_tie) st.tr_tie[r] += ties;
+        ((int32_t*)park[2])[rr] = idx;
+        ((double*)park[3])[rr] = a;
+        ((double*)park[4])[rr] = b;
+        ((int64_t*)park[5])[rr] = t;
+        ((int64_t*)park[6])[rr] = sum_end;
+        ((int32_t*)park[7])[rr] = done;
+        int32_t* const tie = (int32_t*)park[8];
+        if (tie) tie[rr] += ties;
+    }
+}
+
+
+// ---------------------------------------------------------------------------
+// p + c - 1 = 1 (configs[0], SA_RRG.py with p = c = 1): NQ proposals per step
+// (k_sa_lds_multi<D, NQ>, NQ groups of 64/NQ >= d+1 lanes).  At one level the
+// light cone of proposal q is i_q and its neighbours (C_1 needs no marks:
+// those candidates are distinct) and what it reads is level 0 on the radius-2
+// ball and the cached level 1 of the radius-1 ball; an earlier proposal j
+// changes level 0 at i_j and level 1 only inside N[i_j], so q's evaluation
+// stands after an accepted j unless i_j is one of the nodes q's lanes read at
+// level 0 (a candidate or a neighbour of one) -- which also covers q's reads
+// of level 1 (a candidate in N[i_j] has i_j among its neighbours).  The taken
+// proposals are a prefix: the first one that conflicts with an accepted
+// earlier one, or follows a stop, and all after it are drawn again next step.
+template <int D, int NQ, bool TRACE>
+__global__ void __launch_bounds__(64) k_sa_lds_multi(const int32_t* __restrict__ adj, int64_t n, int64_t R,
+                                                     int64_t W, u64* __restrict__ s, mjx_sa_state st, int64_t nsteps,
+                                                     double par_a, double par_b, double a_cap, double b_cap,
+                                                     int64_t t_cap, Geo geo) {
+    static_assert(D >= 1 && D <= 4 && NQ >= 2 && 64 / NQ >= D + 1, "multi-proposal LDS SA: d <= 4, T = 1");
+    constexpr int G = 64 / NQ;
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int lane = threadIdx.x;
+    const int gq = lane / G, gl = lane % G;
+    const int64_t r = blockIdx.x;
+    const int nw = geo.nw;
+    uint16_t* rows = reinterpret_cast<uint16_t*>(smem);
+    uint32_t* lv = reinterpret_cast<uint32_t*>(smem + geo.off_lev);       // {level, marks} (marks unused)
+    uint32_t* lev0s = reinterpret_cast<uint32_t*>(smem + geo.off_lev0);
+    uint32_t* mt = reinterpret_cast<uint32_t*>(smem + geo.off_mt);
+    const int32_t* g = adj + (st.rep_graph ? (int64_t)st.rep_graph[r] : 0) * n * D;
+    auto lword = [&](int t, int w) -> uint32_t& { return lv[2 * (t * nw + w)]; };
+    auto bit_of = [&](int t, int v) -> uint32_t { return (lword(t, v >> 5) >> (v & 31)) & 1u; };
+    auto nbrs = [&](int v, int (&o)[D]) {
+        const uint2 x = *reinterpret_cast<const uint2*>(rows + v * 4);
+        o[0] = (int)(x.x & 0xffffu);
+        if constexpr (D > 1) o[1] = (int)(x.x >> 16);
+        if constexpr (D > 2) o[2] = (int)(x.y & 0xffffu);
+        if constexpr (D > 3) o[3] = (int)(x.y >> 16);
+    };
+    auto maj = [&](int ones, uint32_t own) -> uint32_t {       // always-stay majority (code/SA_RRG.py:19-20)
+        return (2 * ones > D) ? 1u : ((2 * ones < D) ? 0u : own);
+    };
+
+    // ---- launch setup (level 0 from s, level 1 by one sweep in LDS)
+    {
+        const int64_t col = r >> 6;
+        const u64 rbit = 1ull << (r & 63);
+        for (int64_t q = lane; q < n * D; q += 64) {
+            const int64_t v = q / D;
+            rows[v * 4 + (q - v * D)] = (uint16_t)g[q];
+        }
+        for (int k = lane; k < 2 * nw * 2; k += 64) lv[k] = 0u;
+        wave_sync();
+        for (int64_t v0 = 0; v0 < (int64_t)nw * 32; v0 += 64) {
+            const int64_t v = v0 + lane;
+            const bool b = v < n && (s[v * W + col] & rbit);
+            const u64 m = __ballot(b);
+            if (lane < 2) {
+                const uint32_t x = (uint32_t)(m >> (32 * lane));
+                lword(0, (int)(v0 >> 5) + lane) = x;
+                lev0s[(v0 >> 5) + lane] = x;
+            }
+        }
+        for (int k = lane; k < MT_N; k += 64) mt[k] = st.mt[r * MT_N + k];
+        wave_sync();
+        for (int64_t v0 = 0; v0 < (int64_t)nw * 32; v0 += 64) {
+            const int v = (int)(v0 + lane);
+            uint32_t nb = 0;
+            if (v < n) {
+                int nv[D];
+                nbrs(v, nv);
+                int ones = 0;
+#pragma unroll
+                for (int q = 0; q < D; ++q) ones += (int)bit_of(0, nv[q]);
+                nb = maj(ones, bit_of(0, v));
+            }
+            const u64 m = __ballot(nb != 0);
+            if (lane < 2) lword(1, (int)(v0 >> 5) + lane) = (uint32_t)(m >> (32 * lane));
+        }
+        wave_sync();
+    }
+
+    double a = st.a[r], b = st.b[r];
+    int64_t t = st.t[r], sum_end = st.sum_end[r];
+    int done = st.done[r];
+    int idx = st.mt_idx[r];
+    int ties = 0;
+    u64* park = reinterpret_cast<u64*>(smem + geo.off_cnt);     // write-back pointers, off the scalar file
+    if (lane == 0) {
+        park[0] = (u64)s;
+        park[1] = (u64)st.mt;
+        park[2] = (u64)st.mt_idx;
+        park[3] = (u64)st.a;
+        park[4] = (u64)st.b;
+        park[5] = (u64)st.t;
+        park[6] = (u64)st.sum_end;
+        park[7] = (u64)st.done;
+        park[8] = (u64)st.tr_tie;
+        park[9] = (u64)W;
+    }
+    const uint32_t rng = (uint32_t)(n - 1);
+    uint32_t mask = rng;
+    mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+    double inv_n = 1.0 / (double)n;
+    asm volatile("" : "+v"(a), "+v"(b), "+v"(par_a), "+v"(par_b), "+v"(a_cap), "+v"(b_cap), "+v"(inv_n));
+
+    int pb_i = 0, pb_end = 0;
+    uint32_t pb_w1 = 0, pb_w2 = 0;
+    double pb_u = 0.0;
+    int npend = 0, pk = 0;
+    auto parse = [&](bool one) {
+        for (;;) {
+            if (idx >= MT_N) {
+                if (one) break;
+                lds_twist(mt, lane);
+                idx = 0;
+            }
+            const int lim = (MT_N - idx < 64) ? MT_N - idx : 64;
+            uint32_t tw = 0, y = 0;
+            bool ok = false;
+            if (lane < lim) {
+                tw = mt_temper(mt[idx + lane]);
+                y = tw & mask;
+                ok = y <= rng;
+            }
+            const u64 okm = __ballot(ok);
+            int pos = 0, got = 0;
+            while (pos < 64 && npend < 64) {
+                const u64 m = okm >> pos;
+                if (!m) break;
+                const int f = pos + __ffsll((unsigned long long)m) - 1;
+                if (f + 2 >= lim) break;
+                const int iv = __builtin_amdgcn_readlane((int)y, f);
+                const uint32_t w1 = (uint32_t)__builtin_amdgcn_readlane((int)tw, f + 1);
+                const uint32_t w2 = (uint32_t)__builtin_amdgcn_readlane((int)tw, f + 2);
+                if (lane == npend) { pb_i = iv; pb_w1 = w1; pb_w2 = w2; pb_end = idx + f + 3; }
+                ++npend;
+                ++got;
+                pos = f + 3;
+            }
+            if (got > 0) { idx += pos; break; }
+            if (one) break;
+            if (!okm) { idx += lim; continue; }
+            const int f = __ffsll((unsigned long long)okm) - 1;
+            if (f > 0) { idx += f; continue; }
+            const int iv = __builtin_amdgcn_readlane((int)y, 0);
+            idx += 1;
+            if (idx >= MT_N) { lds_twist(mt, lane); idx = 0; }
+            const uint32_t w1 = mt_temper(mt[idx]);
+            idx += 1;
+            if (idx >= MT_N) { lds_twist(mt, lane); idx = 0; }
+            const uint32_t w2 = mt_temper(mt[idx]);
+            idx += 1;
+            if (lane == npend) { pb_i = iv; pb_w1 = w1; pb_w2 = w2; pb_end = idx; }
+            ++npend;
+            break;
+        }
+        pb_u = mt_double(pb_w1, pb_w2);
+    };
+
+    bool drew = false;
+    int64_t k = 0;
+    while (k < nsteps && done == 0) {
+        int avail = npend - pk;
+        if (avail < NQ && idx + 64 <= MT_N) {
+            // carry the unconsumed proposals to lanes 0.. and append one window
+            const int src = (lane + pk < 64) ? lane + pk : 63;
+            pb_i = __shfl(pb_i, src, 64);
+            pb_end = __shfl(pb_end, src, 64);
+            pb_w1 = (uint32_t)__shfl((int)pb_w1, src, 64);
+            pb_w2 = (uint32_t)__shfl((int)pb_w2, src, 64);
+            npend = avail;
+            pk = 0;
+            parse(true);
+            if (npend == 0) parse(false);
+        } else if (avail == 0) {
+            npend = 0;
+            pk = 0;
+            parse(false);
+        }
+        drew = true;
+        avail = npend - pk;
+        int nq = avail < NQ ? avail : NQ;
+        if ((int64_t)nq > nsteps - k) nq = (int)(nsteps - k);
+        // group gq's proposal
+        const bool act = gq < nq;
+        const int mine = __shfl(pb_i, pk + (act ? gq : 0), 64);
+        const uint64_t ub = __builtin_bit_cast(uint64_t, pb_u);
+        const uint32_t ulo = (uint32_t)__shfl((int)(uint32_t)ub, pk + (act ? gq : 0), 64);
+        const uint32_t uhi = (uint32_t)__shfl((int)(uint32_t)(ub >> 32), pk + (act ? gq : 0), 64);
+        const double u = __builtin_bit_cast(double, ((uint64_t)uhi << 32) | ulo);
+        const int iv = mine;
+        const uint32_t old_i = bit_of(0, iv);
+        // level 1: i and its neighbours, level 0 with i flipped
+        int ri[D];
+        nbrs(iv, ri);
+        int cand = iv;
+#pragma unroll
+        for (int q = 0; q < D; ++q)
+            if (gl == q + 1) cand = ri[q];
+        bool dup = gl > 0 && cand == iv;
+#pragma unroll
+        for (int q = 0; q < D; ++q)
+            if (q + 1 < gl) dup |= ri[q] == cand;
+        int nv[D];
+        nbrs(cand, nv);
+        const bool live = act && gl <= D && !dup;
+        int ones = 0;
+#pragma unroll
+        for (int e = 0; e < D; ++e) ones += (int)(bit_of(0, nv[e]) ^ (nv[e] == iv));
+        const uint32_t own = bit_of(0, cand) ^ (cand == iv);
+        const uint32_t nb = maj(ones, own);
+        const uint32_t cur = bit_of(1, cand);
+        const bool chg = live && nb != cur;
+        // conflicts with the earlier proposals of the step: bit j of cf = i_j read here
+        uint32_t cf = 0;
+#pragma unroll
+        for (int j = 0; j < NQ - 1; ++j) {
+            const int ij = __shfl(pb_i, pk + j, 64);
+            bool hit = cand == ij;
+#pragma unroll
+            for (int e = 0; e < D; ++e) hit |= nv[e] == ij;
+            if (live && j < gq && hit) cf |= 1u << j;
+        }
+        // per group: sum(s_end) change, conflicts (uniform masks, sliced per group below)
+        const u64 up = __ballot(chg && cur == 0u), dn = __ballot(chg && cur != 0u);
+        u64 cfm[NQ - 1];
+#pragma unroll
+        for (int j = 0; j < NQ - 1; ++j) cfm[j] = __ballot((cf >> j) & 1u);
+        const u64 gm = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << (gq * G);
+        const int64_t ds = 2 * ((int64_t)__popcll(up & gm) - (int64_t)__popcll(dn & gm));
+        // schedule value of step k + gq (code/SA_RRG.py:80-81), delta_H and the Metropolis test
+        double ag = a, bg = b;
+        for (int q = 0; q < gq; ++q) {
+            if (ag < a_cap) ag = par_a * ag;
+            if (bg < b_cap) bg = par_b * bg;
+        }
+        const double si = old_i ? 1.0 : -1.0;
+        const double t1 = (-2.0 * ag) * si;
+        const double t2 = bg * (double)(-ds);
+        const double num = t1 + t2;
+        const float xf = (float)(-num * inv_n);
+        const float ef = __expf(xf);
+        const float mg = ef * (1e-6f * (1.0f + fabsf(xf))) + 1e-37f;
+        bool acc, tie = false;
+        double dE = 0.0;
+        if (fabs(u - (double)ef) > (double)mg) {
+            acc = u < (double)ef;
+            if (TRACE && st.tr_dE) dE = num / (double)n;
+        } else {
+            dE = num / (double)n;
+            const double e = exp(-dE);
+            const double prob = (e < 1.0) ? e : 1.0;
+            acc = u < prob;
+            tie = e < 1.0 && fabs(u - e) <= 4.0 * (nextafter(e, 2.0) - e);
+        }
+        const u64 accm = __ballot(acc && gl == 0), tiem = __ballot(tie && gl == 0);
+        // ---- resolve in proposal order: the taken proposals are a prefix
+        int taken = 0;
+        uint32_t acc_taken = 0;
+        for (int q = 0; q < nq; ++q) {
+            if (done) break;
+            bool clash = false;
+            for (int j = 0; j < q; ++j)
+                if (((acc_taken >> j) & 1u) && ((cfm[j] >> (q * G)) & (G == 64 ? ~0ull : ((1ull << G) - 1ull))))
+                    clash = true;
+            if (clash) break;
+            const bool aq = (accm >> (q * G)) & 1ull;
+            const int64_t dq = 2 * ((int64_t)__popcll((up >> (q * G)) & (G == 64 ? ~0ull : ((1ull << G) - 1ull))) -
+                                    (int64_t)__popcll((dn >> (q * G)) & (G == 64 ? ~0ull : ((1ull << G) - 1ull))));
+            if (aq) { sum_end += dq; acc_taken |= 1u << q; }      // (code/SA_RRG.py:77)
+            if ((tiem >> (q * G)) & 1ull) ++ties;
+            if (a < a_cap) a = par_a * a;                           // (:80-81)
+            if (b < b_cap) b = par_b * b;
+            t += 1;                                                 // (:82)
+            if (t > t_cap) done = 2;                                // (:84)
+            else if (sum_end == n) done = 1;                        // m(s_endstate(s)) == 1
+            if (TRACE && lane == q * G) {
+                if (st.tr_i) st.tr_i[(k + q) * R + r] = iv;
+                if (st.tr_acc) st.tr_acc[(k + q) * R + r] = aq ? 1 : 0;
+                if (st.tr_sum) st.tr_sum[(k + q) * R + r] = sum_end;
+                if (st.tr_dE) st.tr_dE[(k + q) * R + r] = dE;
+            }
+            ++taken;
+        }
+        // ---- the accepted proposals among the taken ones: level 1 on their C_1, level 0 at i
+        if (gq < taken && ((acc_taken >> gq) & 1u)) {
+            if (chg) {
+                const uint32_t bit = 1u << (cand & 31);
+                if (cur) atomicAnd(&lword(1, cand >> 5), ~bit);
+                else atomicOr(&lword(1, cand >> 5), bit);
+            }
+            if (gl == 0) atomicXor(&lword(0, iv >> 5), 1u << (iv & 31));
+        }
+        k += taken;
+        pk += taken;
+        wave_sync();
+    }
+    if (drew) idx = __builtin_amdgcn_readlane(pb_end, pk - 1);
+    if (TRACE && lane == 0) {
+        for (; k < nsteps; ++k) {
+            if (st.tr_i) st.tr_i[k * R + r] = -1;
+            if (st.tr_acc) st.tr_acc[k * R + r] = -1;
+            if (st.tr_sum) st.tr_sum[k * R + r] = sum_end;
+            if (st.tr_dE) st.tr_dE[k * R + r] = 0.0;
+        }
+    }
+    wave_sync();
+    u64* const ps = (u64*)park[0];
+    const int64_t Wp = (int64_t)park[9];
+    const int64_t rr = blockIdx.x;
+    for (int64_t v0 = 0; v0 < n; v0 += 64) {
+        const int v = (int)(v0 + lane);
+        if (v < n && (((lword(0, v >> 5) ^ lev0s[v >> 5]) >> (v & 31)) & 1u))
+            atomicXor((unsigned long long*)&ps[(int64_t)v * Wp + (rr >> 6)], 1ull << (rr & 63));
+    }
+    uint32_t* const pmt = (uint32_t*)park[1];
+    for (int q = lane; q < MT_N; q += 64) pmt[rr * MT_N + q] = mt[q];
+    if (lane == 0) {
+        ((int32_t*)park[2])[rr] = idx;
+        ((double*)park[3])[rr] = a;
+        ((double*)park[4])[rr] = b;
+        ((int64_t*)park[5])[rr] = t;
+        ((int64_t*)park[6])[rr] = sum_end;
+        ((int32_t*)park[7])[rr] = done;
+        int32_t* const tie = (int32_t*)park[8];
+        if (tie) tie[rr] += ties;
     }
 }
 
@@ -1354,7 +1706,8 @@ extern "C" int mjx_sa_lds_steps(const int32_t* adj, int64_t n, int d, int p, int
     if (!salds::geometry(n, d, T, &g)) return MJX_ERANGE;
     const mjx_sa_state st = *stp;
     if (!st.mt || !st.mt_idx || !st.a || !st.b || !st.t || !st.sum_end || !st.done) return MJX_EINVAL;
-    if (st.opt_flags & ~(MJX_SA_NO_SPEC | MJX_SA_NO_CONE2 | MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE)) return MJX_EINVAL;
+    if (st.opt_flags & ~(MJX_SA_NO_SPEC | MJX_SA_NO_CONE2 | MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE | MJX_SA_LDS_PAIR))
+        return MJX_EINVAL;
     if (nsteps == 0) return MJX_OK;
     if (R > INT32_MAX) return MJX_ERANGE;
     const int64_t W = (R + 63) / 64;
@@ -1367,6 +1720,19 @@ extern "C" int mjx_sa_lds_steps(const int32_t* adj, int64_t n, int d, int p, int
         MJX_LAUNCH_CHECK("k_sa_lds");
         return MJX_OK;
     };
+    if (!(st.opt_flags & (MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE | MJX_SA_LDS_PAIR)) && (d == 3 || d == 4) && T == 1) {
+        const bool trm = st.tr_i || st.tr_acc || st.tr_sum || st.tr_dE;
+        auto gom = [&](auto kern) -> int {
+            MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, g.bytes),
+                    "sa_lds lds");
+            kern<<<(unsigned)R, 64, (size_t)g.bytes, hs>>>(adj, n, R, W, (u64*)s, st, nsteps, par_a, par_b, a_cap,
+                                                           b_cap, t_cap, g);
+            MJX_LAUNCH_CHECK("k_sa_lds_multi");
+            return MJX_OK;
+        };
+        if (d == 3) return trm ? gom(salds::k_sa_lds_multi<3, 8, true>) : gom(salds::k_sa_lds_multi<3, 8, false>);
+        return trm ? gom(salds::k_sa_lds_multi<4, 8, true>) : gom(salds::k_sa_lds_multi<4, 8, false>);
+    }
     salds::Geo g2;
     if (!(st.opt_flags & (MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE)) && (d == 3 || d == 4) && T <= 4 &&
         salds::geometry(n, d, T, &g2, 2)) {

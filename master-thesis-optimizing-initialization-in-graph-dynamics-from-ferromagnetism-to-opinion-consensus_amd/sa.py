@@ -47,7 +47,7 @@ def schedule_constants(n):
 
 
 KERNEL_FLAGS = {"no_spec": _lib.MJX_SA_NO_SPEC, "no_cone2": _lib.MJX_SA_NO_CONE2, "lds_serial": _lib.MJX_SA_LDS_SERIAL,
-                "lds_single": _lib.MJX_SA_LDS_SINGLE}
+                "lds_single": _lib.MJX_SA_LDS_SINGLE, "lds_pair": _lib.MJX_SA_LDS_PAIR}
 
 
 def _graph_stack(N, R, graph_of):
@@ -108,7 +108,7 @@ class SAReplicas:
         (mjx_sa_lightcone_steps); ``"auto"``: lds where it fits, else cone;
         same results in every layout.  ``kernel``: light-cone kernel
         selection passed to the ABI (tests, tuning): ``split`` (waves per word
-        column), ``spec_k`` (8 or 16), ``no_spec``, ``no_cone2``, ``lds_serial``, ``lds_single``; the results
+        column), ``spec_k`` (8 or 16), ``no_spec``, ``no_cone2``, ``lds_serial``, ``lds_single``, ``lds_pair``; the results
         never depend on it."""
         seeds = np.asarray(seeds, dtype=np.int64).reshape(-1)
         if seeds.size == 0 or seeds.min() < 0 or seeds.max() > 0xFFFFFFFF:

@@ -38,17 +38,19 @@ def _sa(mjx_mod, N, p, c, seeds, mode):
     """mode: "lightcone" (HBM cone layout, default tape), "lightcone-notape"
     (draws inside the step kernel), "lightcone-tape7" (tape chunks of 7
     steps), "lightcone-lds" (graph, levels and stream in LDS, two proposals per
-    step; "-ldssingle" one, "-ldsserial" the list-based step), "lightcone-rec"
+    step, eight at p+c-1 = 1; "-ldspair" two, "-ldssingle" one, "-ldsserial"
+    the list-based step), "lightcone-rec"
     (the cone with the adjacency rows in its records), "rollout"."""
     tape = {"lightcone-notape": 0, "lightcone-tape7": 7}.get(mode, 1024)
     layout = {"lightcone-lds": "lds", "lightcone-ldsserial": "lds", "lightcone-ldssingle": "lds",
-              "lightcone-rec": "rec"}.get(mode, "cone")
-    kernel = {"lightcone-ldsserial": {"lds_serial": True}, "lightcone-ldssingle": {"lds_single": True}}.get(mode)
+              "lightcone-ldspair": "lds", "lightcone-rec": "rec"}.get(mode, "cone")
+    kernel = {"lightcone-ldsserial": {"lds_serial": True}, "lightcone-ldssingle": {"lds_single": True},
+              "lightcone-ldspair": {"lds_pair": True}}.get(mode)
     return mjx_mod.SAReplicas(N, p, c, seeds, mode=mode.split("-")[0], tape=tape, layout=layout, kernel=kernel)
 
 
 MODES = ["lightcone", "lightcone-notape", "lightcone-tape7", "lightcone-lds", "lightcone-ldsserial",
-         "lightcone-ldssingle", "lightcone-rec", "rollout"]
+         "lightcone-ldssingle", "lightcone-ldspair", "lightcone-rec", "rollout"]
 
 
 @pytest.mark.parametrize("mode", MODES)
@@ -247,7 +249,8 @@ def test_sa_run_independent_per_replica_graphs(mjx_mod):
 
 
 @pytest.mark.parametrize("d,p,c,kern", [(4, 3, 1, None), (4, 3, 1, "lds_serial"), (4, 3, 1, "lds_single"),
-                                        (3, 2, 1, None), (4, 1, 1, None), (4, 1, 1, "lds_single")])
+                                        (3, 2, 1, None), (4, 1, 1, None), (4, 1, 1, "lds_single"),
+                                        (4, 1, 1, "lds_pair"), (3, 1, 1, None)])
 def test_sa_lds_stream_position_in_ragged_calls(mjx_mod, d, p, c, kern):
     """The LDS-resident steps parse the numpy stream 64 words at a time
     (the paired step carries a leftover proposal into the next window) and

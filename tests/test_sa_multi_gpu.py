@@ -36,6 +36,9 @@ def _check(tr, conf, t, graphs, graph_of, seeds, p, c, K, replicas):
     (6, 200, 2, 1, 20, 200, {}, "lightcone", "cone"),
     (3, 500, 2, 1, 70, 400, {}, "lightcone", "lds"),                        # LDS-resident replicas
     (4, 400, 1, 1, 130, 400, {}, "lightcone", "lds"),
+    (4, 400, 1, 1, 130, 400, {"lds_pair": True}, "lightcone", "lds"),
+    (3, 64, 1, 1, 70, 600, {}, "lightcone", "lds"),                          # eight proposals, many conflicts
+    (4, 64, 1, 1, 70, 600, {}, "lightcone", "lds"),
     (4, 300, 3, 1, 65, 300, {}, "lightcone", "lds"),
     (6, 200, 2, 1, 20, 200, {}, "lightcone", "lds"),
     (5, 200, 2, 2, 20, 200, {}, "lightcone", "lds"),                        # runtime degree, T = 3

@@ -11,9 +11,9 @@ import mjx  # noqa: E402
 n, d, R = 10_000, 4, 64
 graphs = [mjx.random_regular_graph(d, n, seed=7000 + k) for k in range(R)]
 for (p, c) in ((1, 1), (3, 1)):
-    for layout in ("lds", "lds-single", "cone"):
+    for layout in ("lds", "lds-pair", "lds-single", "cone"):
         K = 20000 if (layout.startswith("lds") or p == 1) else 1000
-        kern = {"lds_single": True} if layout == "lds-single" else None
+        kern = {"lds-single": {"lds_single": True}, "lds-pair": {"lds_pair": True}}.get(layout)
         sa = mjx.SAReplicas(graphs, p, c, list(range(R)), layout=layout.split("-")[0], kernel=kern)
         sa.steps(K)
         torch.cuda.synchronize()
