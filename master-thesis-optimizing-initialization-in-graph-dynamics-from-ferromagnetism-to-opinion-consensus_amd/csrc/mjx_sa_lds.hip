@@ -1506,6 +1506,9 @@ __global__ void __launch_bounds__(64) k_sa_lds_multi(const int32_t* __restrict__
 
     bool drew = false;
     int64_t k = 0;
+#ifdef MJX_SA_PROF
+    unsigned long long _acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, _t0 = __builtin_amdgcn_s_memtime();
+#endif
     while (k < nsteps && done == 0) {
         int avail = npend - pk;
         if (avail < NQ && idx + 64 <= MT_N) {
@@ -1525,6 +1528,7 @@ __global__ void __launch_bounds__(64) k_sa_lds_multi(const int32_t* __restrict__
             parse(false);
         }
         drew = true;
+        LDS_STAMP(0);
         avail = npend - pk;
         int nq = avail < NQ ? avail : NQ;
         if ((int64_t)nq > nsteps - k) nq = (int)(nsteps - k);
@@ -1573,6 +1577,7 @@ __global__ void __launch_bounds__(64) k_sa_lds_multi(const int32_t* __restrict__
         u64 cfm[NQ - 1];
 #pragma unroll
         for (int j = 0; j < NQ - 1; ++j) cfm[j] = __ballot((cf >> j) & 1u);
+        LDS_STAMP(1);
         const u64 gm = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << (gq * G);
         const int64_t ds = 2 * ((int64_t)__popcll(up & gm) - (int64_t)__popcll(dn & gm));
         // schedule value of step k + gq (code/SA_RRG.py:80-81), delta_H and the Metropolis test
@@ -1581,6 +1586,8 @@ __global__ void __launch_bounds__(64) k_sa_lds_multi(const int32_t* __restrict__
             if (ag < a_cap) ag = par_a * ag;
             if (bg < b_cap) bg = par_b * bg;
         }
+        const double an = (ag < a_cap) ? par_a * ag : ag;           // the schedule after this step
+        const double bn = (bg < b_cap) ? par_b * bg : bg;
         const double si = old_i ? 1.0 : -1.0;
         const double t1 = (-2.0 * ag) * si;
         const double t2 = bg * (double)(-ds);
@@ -1601,34 +1608,39 @@ __global__ void __launch_bounds__(64) k_sa_lds_multi(const int32_t* __restrict__
             tie = e < 1.0 && fabs(u - e) <= 4.0 * (nextafter(e, 2.0) - e);
         }
         const u64 accm = __ballot(acc && gl == 0), tiem = __ballot(tie && gl == 0);
-        // ---- resolve in proposal order: the taken proposals are a prefix
+        LDS_STAMP(5);
+        // ---- resolve in proposal order: the taken proposals are a prefix, ended by
+        // the first proposal that read an accepted earlier one's i (one ballot) or
+        // by a stop; the walk over the prefix is integer work only
+        constexpr u64 GM = (G == 64) ? ~0ull : ((1ull << G) - 1ull);
+        uint32_t accg = 0;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) accg |= (uint32_t)((accm >> (q * G)) & 1ull) << q;
+        const u64 clm = __ballot(live && (cf & accg) != 0u);
+        int qstop = nq;
+        if (clm) {
+            const int qc = (__ffsll((unsigned long long)clm) - 1) / G;
+            if (qc < qstop) qstop = qc;
+        }
         int taken = 0;
-        uint32_t acc_taken = 0;
-        for (int q = 0; q < nq; ++q) {
-            if (done) break;
-            bool clash = false;
-            for (int j = 0; j < q; ++j)
-                if (((acc_taken >> j) & 1u) && ((cfm[j] >> (q * G)) & (G == 64 ? ~0ull : ((1ull << G) - 1ull))))
-                    clash = true;
-            if (clash) break;
-            const bool aq = (accm >> (q * G)) & 1ull;
-            const int64_t dq = 2 * ((int64_t)__popcll((up >> (q * G)) & (G == 64 ? ~0ull : ((1ull << G) - 1ull))) -
-                                    (int64_t)__popcll((dn >> (q * G)) & (G == 64 ? ~0ull : ((1ull << G) - 1ull))));
-            if (aq) { sum_end += dq; acc_taken |= 1u << q; }      // (code/SA_RRG.py:77)
+        for (int q = 0; q < qstop; ++q) {
+            const bool aq = (accg >> q) & 1u;
+            if (aq) sum_end += 2 * ((int64_t)__popcll((up >> (q * G)) & GM) - (int64_t)__popcll((dn >> (q * G)) & GM));
             if ((tiem >> (q * G)) & 1ull) ++ties;
-            if (a < a_cap) a = par_a * a;                           // (:80-81)
-            if (b < b_cap) b = par_b * b;
-            t += 1;                                                 // (:82)
-            if (t > t_cap) done = 2;                                // (:84)
-            else if (sum_end == n) done = 1;                        // m(s_endstate(s)) == 1
+            t += 1;                                                 // (code/SA_RRG.py:77,82)
+            ++taken;
             if (TRACE && lane == q * G) {
                 if (st.tr_i) st.tr_i[(k + q) * R + r] = iv;
                 if (st.tr_acc) st.tr_acc[(k + q) * R + r] = aq ? 1 : 0;
                 if (st.tr_sum) st.tr_sum[(k + q) * R + r] = sum_end;
                 if (st.tr_dE) st.tr_dE[(k + q) * R + r] = dE;
             }
-            ++taken;
+            if (t > t_cap) { done = 2; break; }                     // (:84)
+            if (sum_end == n) { done = 1; break; }                  // m(s_endstate(s)) == 1
         }
+        const uint32_t acc_taken = accg & ((1u << taken) - 1u);
+        a = __shfl(an, (taken - 1) * G, 64);                        // (:80-81) after the taken steps
+        b = __shfl(bn, (taken - 1) * G, 64);
         // ---- the accepted proposals among the taken ones: level 1 on their C_1, level 0 at i
         if (gq < taken && ((acc_taken >> gq) & 1u)) {
             if (chg) {
@@ -1641,7 +1653,15 @@ __global__ void __launch_bounds__(64) k_sa_lds_multi(const int32_t* __restrict__
         k += taken;
         pk += taken;
         wave_sync();
+        LDS_STAMP(6);
+#ifdef MJX_SA_PROF
+        _acc[7] += 1000 * (unsigned long long)taken;
+#endif
     }
+#ifdef MJX_SA_PROF
+    if (lane == 0)
+        for (int q = 0; q < 8; ++q) atomicAdd(&mjx_sa_lds_prof[q], _acc[q]);
+#endif
     if (drew) idx = __builtin_amdgcn_readlane(pb_end, pk - 1);
     if (TRACE && lane == 0) {
         for (; k < nsteps; ++k) {

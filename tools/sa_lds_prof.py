@@ -12,11 +12,12 @@ import mjx  # noqa: E402
 
 mjx.load_library()
 raw = ctypes.CDLL(mjx.lib_path())
-names = ["refill+proposal", "level 1", "level 2", "level 3", "level 4", "dE+exp+accept", "apply+trace",
+# phases of k_sa_lds_multi (p+c-1 = 1): refill, level 1 + conflicts, resolution, -, -, dE + accept, apply
+names = ["refill+proposal", "level 1", "level 2 / resolve", "level 3", "level 4", "dE+exp+accept", "apply+trace",
          "pair code"]
 n, d, R = 10_000, 4, 64
 graphs = [mjx.random_regular_graph(d, n, seed=7000 + k) for k in range(R)]
-for (p, c, kern) in ((1, 1, None), (3, 1, None), (3, 1, {"lds_single": True})):
+for (p, c, kern) in ((1, 1, None), (1, 1, {"lds_pair": True}), (3, 1, None), (3, 1, {"lds_single": True})):
     sa = mjx.SAReplicas(graphs, p, c, list(range(R)), layout="lds", kernel=kern)
     K = 20000
     sa.steps(K)
