@@ -753,7 +753,7 @@ __global__ void __launch_bounds__(64) k_sa_lds_fast(const int32_t* __restrict__ 
                         if (lc_v[l]) atomicAnd(&lword(l, v >> 5), ~bit);
                         else atomicOr(&lword(l, v >> 5), bit);
                     }
-                    atomicAnd(&cword(l, v >> 5), ~bit);
+                    cword(l, v >> 5) = 0u;            // every mark of the word is this step's
                 }
             } else {
                 const uint32_t* cl = lst + l * lc;
@@ -761,7 +761,7 @@ __global__ void __launch_bounds__(64) k_sa_lds_fast(const int32_t* __restrict__ 
                     const int v = (int)cl[q];
                     const uint32_t bit = 1u << (v & 31);
                     if (acc) atomicXor(&lword(l, v >> 5), bit);
-                    atomicAnd(&cword(l, v >> 5), ~bit);
+                    cword(l, v >> 5) = 0u;            // every mark of the word is this step's
                 }
             }
         }
@@ -1212,6 +1212,8 @@ __global__ void __launch_bounds__(64) k_sa_lds_pair(const int32_t* __restrict__ 
         const double aB = (a < a_cap) ? par_a * a : a;               // the schedule after step A (:80-81)
         const double bB = (b < b_cap) ? par_b * b : b;
         const double ah = h ? aB : aA, bh = h ? bB : bA;
+        const double anx = (ah < a_cap) ? par_a * ah : ah;          // the schedule after this half's step
+        const double bnx = (bh < b_cap) ? par_b * bh : bh;
         const double si = old_i ? 1.0 : -1.0;
         const double t1 = (-2.0 * ah) * si;
         const double t2 = bh * (double)(-ds);
@@ -1262,7 +1264,7 @@ __global__ void __launch_bounds__(64) k_sa_lds_pair(const int32_t* __restrict__ 
                             if (lc_v[l]) atomicAnd(&lword(l, v >> 5), ~bit);
                             else atomicOr(&lword(l, v >> 5), bit);
                         }
-                        atomicAnd(&mword(l, v >> 5, h), ~bit);
+                        mword(l, v >> 5, h) = 0u;         // every mark of the word is this step's
                     }
                 } else {
                     const uint32_t* cl = lsth + l * lc;
@@ -1270,7 +1272,7 @@ __global__ void __launch_bounds__(64) k_sa_lds_pair(const int32_t* __restrict__ 
                         const int v = (int)cl[q];
                         const uint32_t bit = 1u << (v & 31);
                         if (mine) atomicXor(&lword(l, v >> 5), bit);
-                        atomicAnd(&mword(l, v >> 5, h), ~bit);
+                        mword(l, v >> 5, h) = 0u;         // every mark of the word is this step's
                     }
                 }
             }
@@ -1291,8 +1293,8 @@ __global__ void __launch_bounds__(64) k_sa_lds_pair(const int32_t* __restrict__ 
         ++pk;
         if (takeB) {
             if (accB) sum_end += dsB;
-            if (a < a_cap) a = par_a * a;
-            if (b < b_cap) b = par_b * b;
+            a = __shfl(anx, 32, 64);
+            b = __shfl(bnx, 32, 64);
             t += 1;
             if (t > t_cap) done = 2;
             else if (sum_end == n) done = 1;
