@@ -610,16 +610,14 @@ __global__ void __launch_bounds__(64) k_sa_lds_fast(const int32_t* __restrict__ 
             const int np = lc_n[l - 1];
             int nc = 0;
             if (fast && np <= MAXM) {
-                // candidates: member s = lane / (d+1) of C_{l-1} (its lane found by a
-                // scan of the mask), j = 0 the member itself, j > 0 its j-th neighbour
+                // candidates: member s = lane / (d+1) of C_{l-1}, j = 0 the member
+                // itself, j > 0 its j-th neighbour; member s's lane: every member
+                // pushes its lane id to lane (its rank) by ds_permute (others to an
+                // unused lane), lane s's entry is pulled by ds_bpermute
                 const int sl = lane / DP1, j = lane - sl * DP1;
-                int src = 0;
-                u64 x = pm;
-                for (int q = 0; q < np; ++q) {
-                    const int pbit = __ffsll((unsigned long long)x) - 1;
-                    if (q == sl) src = pbit;
-                    x &= x - 1;
-                }
+                const int rank = __popcll(pm & ((1ull << lane) - 1ull));
+                const int slot = __builtin_amdgcn_ds_permute((lc_in[l - 1] ? rank : 63) * 4, lane);
+                const int src = __builtin_amdgcn_ds_bpermute(sl * 4, slot) & 63;
                 const int mc = __shfl(cand, src, 64);
                 int pn[D];
 #pragma unroll
@@ -1100,16 +1098,14 @@ __global__ void __launch_bounds__(64) k_sa_lds_pair(const int32_t* __restrict__ 
             const int np = lc_n[l - 1];
             int nc = 0;
             if (go && np <= MAXM && lc_fast[l - 1]) {
-                // candidates: member s = hl / (d+1) of this half's C_{l-1} (its lane found
-                // by a scan of the mask), j = 0 the member itself, j > 0 its j-th neighbour
+                // candidates: member s = hl / (d+1) of this half's C_{l-1}, j = 0 the
+                // member itself, j > 0 its j-th neighbour; member s's lane: every member
+                // pushes its lane id to lane 32h + rank by ds_permute (the others to
+                // the half's unused lane 32h + 31), lane 32h + s's entry is pulled
                 const int sl = hl / DP1, j = hl - sl * DP1;
-                int src = lane;
-                u64 x = pm;
-                for (int q = 0; q < np; ++q) {
-                    const int pbit = __ffsll((unsigned long long)x) - 1;
-                    if (q == sl) src = pbit;
-                    x &= x - 1;
-                }
+                const int rank = __popcll(pm & ltmask);
+                const int slot = __builtin_amdgcn_ds_permute((h * 32 + (lc_in[l - 1] ? rank : 31)) * 4, lane);
+                const int src = __builtin_amdgcn_ds_bpermute((h * 32 + sl) * 4, slot) & 63;
                 const int mc = __shfl(cand, src, 64);
                 int pn[D];
 #pragma unroll
