@@ -187,6 +187,8 @@ typedef struct mjx_sa_state {
 #define MJX_SA_LDS_SERIAL 4u  /* LDS layout: the list-based step (k_sa_lds), not the lane-held one */
 #define MJX_SA_LDS_SINGLE 8u  /* LDS layout: one proposal per step (k_sa_lds_fast), not two (k_sa_lds_pair) */
 #define MJX_SA_LDS_PAIR  16u  /* LDS layout at p+c-1 = 1: two proposals per step, not eight (k_sa_lds_multi) */
+#define MJX_SA_LDS_WAVE  32u  /* LDS layout at p+c-1 >= 2: one wave per replica (k_sa_lds_pair), not the whole
+                                 CU (k_sa_lds_wg: opt_split = 4 or 8 waves, one proposal each; default 8) */
 
 /* Seed replica r with seeds[r] (device uint32[R]), draw s0 into the
  * replica-packed spins s[n*W], set a=a0, b=b0, t=0, done=0, and
@@ -288,6 +290,15 @@ int mjx_sa_rec_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int 
  * mjx_sa_lds_bytes: LDS bytes per replica, -1 if (n, d, p, c) does not fit
  * (n <= 65535, d <= 16, 1 <= p+c-1 <= 6, <= 160 KiB). */
 int64_t mjx_sa_lds_bytes(int64_t n, int d, int p, int c);
+/* LDS bytes per replica of the kernel mjx_sa_lds_steps selects for these
+ * kernel options (opt_flags, opt_split), its threads per workgroup in
+ * *threads (64, or 64 per wave of the whole-CU kernel); -1 if it does not fit. */
+int64_t mjx_sa_lds_plan(int64_t n, int d, int p, int c, uint32_t flags, int split, int* threads);
+
+/* Host-only self-check of the per-device memo tables (CU counts, occupancy,
+ * dynamic-LDS opt-ins are kept per device id, not per process): no HIP call,
+ * runs without a GPU; 0 = pass, else the number of the failed check. */
+int mjx_selftest_devmemo(void);
 int mjx_sa_lds_steps(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R, uint64_t* s,
                      mjx_sa_state* st, int64_t nsteps, double par_a, double par_b, double a_cap, double b_cap,
                      int64_t t_cap, void* stream);

@@ -49,6 +49,8 @@ SIGNATURES = {
     "mjx_sa_lightcone_steps": [c_vp, c_i64, c_int, c_int, c_int, c_i64, c_vp, c_vp, c_vp,
                                c_i64, c_dbl, c_dbl, c_dbl, c_dbl, c_i64, c_vp],
     "mjx_sa_lds_bytes": [c_i64, c_int, c_int, c_int],
+    "mjx_sa_lds_plan": [c_i64, c_int, c_int, c_int, ctypes.c_uint32, c_int, c_vp],
+    "mjx_selftest_devmemo": [],
     "mjx_sa_lds_steps": [c_vp, c_i64, c_int, c_int, c_int, c_i64, c_vp, c_vp, c_i64, c_dbl, c_dbl, c_dbl, c_dbl,
                          c_i64, c_vp],
     "mjx_sa_cone_words": [c_int, c_int],
@@ -105,7 +107,7 @@ SIGNATURES = {
     "mjx_sum_f64": [c_vp, c_i64, c_int, c_vp, c_vp, c_vp],
 }
 _RESTYPES = {"mjx_strerror": ctypes.c_char_p, "mjx_build_id": ctypes.c_char_p, "mjx_last_hip_error": ctypes.c_char_p,
-             "mjx_sa_lightcone_lds": c_i64, "mjx_sa_lds_bytes": c_i64, "mjx_bdcm_lds_bytes": c_i64, "mjx_bdcm_scratch_bytes": c_i64,
+             "mjx_sa_lightcone_lds": c_i64, "mjx_sa_lds_bytes": c_i64, "mjx_sa_lds_plan": c_i64, "mjx_bdcm_lds_bytes": c_i64, "mjx_bdcm_scratch_bytes": c_i64,
              "mjx_rrg_partner_host": c_i64, "mjx_er_work_bytes": c_i64, "mjx_hpr_er_scratch_bytes": c_i64,
              "mjx_mt_jump_table_words": c_i64}
 
@@ -128,6 +130,7 @@ class MjxSaState(ctypes.Structure):
 
 
 MJX_SA_NO_SPEC, MJX_SA_NO_CONE2, MJX_SA_LDS_SERIAL, MJX_SA_LDS_SINGLE, MJX_SA_LDS_PAIR = 1, 2, 4, 8, 16  # opt_flags (include/mjx.h)
+MJX_SA_LDS_WAVE = 32
 
 
 class MjxError(RuntimeError):

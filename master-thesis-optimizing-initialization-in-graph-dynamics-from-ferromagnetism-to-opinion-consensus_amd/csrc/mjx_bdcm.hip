@@ -425,12 +425,7 @@ __global__ void __launch_bounds__(256) k_sum_final(const double* __restrict__ pa
 
 template <typename K>
 static int set_lds(K kern) {
-    static bool done = false;                  // opt in to the whole LDS once per kernel
-    if (!done) {
-        MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds),
-                "bdcm set lds");
-        done = true;
-    }
+    MJX_HIP(set_max_lds(kern, (int)kMaxLds), "bdcm set lds");   // opt in to the whole LDS (once per device)
     return MJX_OK;
 }
 

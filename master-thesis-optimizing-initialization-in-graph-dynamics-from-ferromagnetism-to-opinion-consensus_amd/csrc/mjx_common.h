@@ -28,18 +28,27 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
     } while (0)
 
 constexpr int kBlock = 256;          // 4 waves of 64
-constexpr int kCUs = 256;            // MI355X: 8 XCDs x 32 CUs
+
+// Per-device facts and one-time settings, memoised per (device, kernel, ...):
+// a library caller may drive several devices (or a partitioned GPU) from one
+// process, so nothing here is a process-wide constant.
+int device_cus();                                        // CUs of the current device (256 on a whole MI355X)
+hipError_t set_max_lds(const void* kernel, int bytes);   // opt in to `bytes` of dynamic LDS, once per device
+template <typename K>
+inline hipError_t set_max_lds(K* kernel, int bytes) {
+    return set_max_lds(reinterpret_cast<const void*>(kernel), bytes);
+}
 
 inline int grid_for(int64_t items, int per_cu = 8) {
     int64_t g = (items + kBlock - 1) / kBlock;
-    int64_t cap = (int64_t)kCUs * per_cu;
+    int64_t cap = (int64_t)device_cus() * per_cu;
     if (g > cap) g = cap;
     if (g < 1) g = 1;
     return (int)g;
 }
 
 // Blocks of `kernel` (with `lds` dynamic LDS bytes) resident on one CU at once,
-// memoised per (kernel, block, lds); thread-safe.
+// memoised per (device, kernel, block, lds); thread-safe.
 int resident_blocks_per_cu(const void* kernel, int block, size_t lds);
 
 // Grid for a grid-stride loop over `items` threads' worth of work, capped at
@@ -51,7 +60,7 @@ template <typename K>
 inline int resident_grid(K* kernel, int block, size_t lds, int64_t items) {
     int per = resident_blocks_per_cu(reinterpret_cast<const void*>(kernel), block, lds);
     int64_t g = (items + block - 1) / block;
-    const int64_t cap = (int64_t)kCUs * per;
+    const int64_t cap = (int64_t)device_cus() * per;
     if (g > cap) g = cap;
     if (g < 1) g = 1;
     return (int)g;

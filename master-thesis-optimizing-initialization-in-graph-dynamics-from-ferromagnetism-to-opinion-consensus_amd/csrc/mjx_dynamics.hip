@@ -25,22 +25,99 @@ void set_hip_error(hipError_t e, const char* where) {
     snprintf(g_hip_err, sizeof(g_hip_err), "%s: %s (%d)", where, hipGetErrorString(e), (int)e);
 }
 
-int resident_blocks_per_cu(const void* kernel, int block, size_t lds) {
-    struct Entry { const void* k; int block; size_t lds; int per; };
-    static std::mutex mu;
-    static Entry cache[64];
-    static int used = 0;
-    std::lock_guard<std::mutex> lock(mu);
-    for (int i = 0; i < used; ++i)
-        if (cache[i].k == kernel && cache[i].block == block && cache[i].lds == lds) return cache[i].per;
-    int per = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, block, lds) != hipSuccess || per < 1) {
-        (void)hipGetLastError();
-        per = 1;
+// A small memo table keyed by (device, pointer, two integers); a value is
+// computed once under the lock, failed computations are not kept.
+struct DevMemo {
+    struct Entry { int dev; const void* k; int64_t a, b; int v; };
+    std::mutex mu;
+    Entry e[512];
+    int used = 0;
+    template <typename F>
+    int get(int dev, const void* k, int64_t a, int64_t b, F&& compute) {
+        std::lock_guard<std::mutex> lock(mu);
+        for (int i = 0; i < used; ++i)
+            if (e[i].dev == dev && e[i].k == k && e[i].a == a && e[i].b == b) return e[i].v;
+        bool ok = true;
+        const int v = compute(ok);
+        if (ok && used < 512) e[used++] = Entry{dev, k, a, b, v};
+        return v;
     }
-    if (used < 64) cache[used++] = Entry{kernel, block, lds, per};
-    return per;
+};
+
+static int current_device() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) {
+        (void)hipGetLastError();
+        dev = 0;
+    }
+    return dev;
 }
+
+static DevMemo& memo() {
+    static DevMemo m;
+    return m;
+}
+
+int device_cus() {
+    const int dev = current_device();
+    return memo().get(dev, nullptr, 0, 0, [&](bool& ok) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) {
+            (void)hipGetLastError();
+            ok = false;
+            return 256;                 // a whole MI355X (8 XCDs x 32 CUs)
+        }
+        return cus;
+    });
+}
+
+hipError_t set_max_lds(const void* kernel, int bytes) {
+    const int dev = current_device();
+    return (hipError_t)memo().get(dev, kernel, -1, bytes, [&](bool& ok) {
+        const hipError_t e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+        ok = e == hipSuccess;
+        return (int)e;
+    });
+}
+
+int resident_blocks_per_cu(const void* kernel, int block, size_t lds) {
+    const int dev = current_device();
+    return memo().get(dev, kernel, block, (int64_t)lds, [&](bool& ok) {
+        int per = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, block, lds) != hipSuccess || per < 1) {
+            (void)hipGetLastError();
+            ok = false;
+            per = 1;
+        }
+        return per;
+    });
+}
+
+}  // namespace mjx
+
+// Host-only check of the memo logic (no HIP calls; tests/test_abi.py): values
+// are computed once per (device, kernel, a, b), kept apart per device, and
+// failed computations are retried.  0 = pass, else the number of the failed check.
+extern "C" int mjx_selftest_devmemo(void) {
+    mjx::DevMemo m;
+    int calls = 0;
+    const int k1 = 0, k2 = 0;
+    auto f = [&](int v) { return [&calls, v](bool&) { ++calls; return v; }; };
+    if (m.get(0, &k1, 1, 2, f(10)) != 10 || calls != 1) return 1;
+    if (m.get(0, &k1, 1, 2, f(99)) != 10 || calls != 1) return 2;     // memoised
+    if (m.get(1, &k1, 1, 2, f(20)) != 20 || calls != 2) return 3;     // another device: its own entry
+    if (m.get(0, &k2, 1, 2, f(30)) != 30 || calls != 3) return 4;     // another kernel
+    if (m.get(0, &k1, 1, 3, f(40)) != 40 || calls != 4) return 5;     // another size
+    if (m.get(1, &k1, 1, 2, f(99)) != 20 || calls != 4) return 6;
+    int tries = 0;
+    auto bad = [&](bool& ok) { ++tries; ok = false; return 7; };
+    m.get(2, &k1, 0, 0, bad);
+    m.get(2, &k1, 0, 0, bad);
+    if (tries != 2) return 7;                                          // failures are not kept
+    return 0;
+}
+
+namespace mjx {
 
 // ---------------------------------------------------------------------------
 // pack / unpack
@@ -1042,7 +1119,7 @@ extern "C" int mjx_rollout_ell_rp_multi(const int32_t* adj, int64_t n, int d, in
     if (W > 65535) return MJX_ERANGE;
     hipStream_t st = as_stream(stream);
     int64_t gx = (n + 3) / 4;
-    const int64_t cap = std::max<int64_t>(1, (int64_t)kCUs * 8 / W);
+    const int64_t cap = std::max<int64_t>(1, (int64_t)device_cus() * 8 / W);
     if (gx > cap) gx = cap;
     const dim3 grid((unsigned)gx, (unsigned)W);
     auto sweep = [&](const u64* a, u64* b, unsigned long long* c) -> int {

@@ -253,12 +253,7 @@ static int update_impl(const void* chi_in, void* chi_out, const void* biases, co
                        const int32_t* inc_src, int64_t m, const Geo& g, double w_plus, double w_minus, double damp,
                        void* scratch, int64_t scratch_bytes, hipStream_t st) {
     auto kern = k_hpr_er_edge<S_>;
-    static bool attr_set = false;             // opt in to the whole LDS once per instantiation
-    if (!attr_set) {
-        MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds),
-                "hpr er set lds");
-        attr_set = true;
-    }
+    MJX_HIP(set_max_lds(kern, (int)kMaxLds), "hpr er set lds");   // opt in to the whole LDS (once per device)
     const bool in_lds = lds_bytes<S_>(g) <= kMaxLds;
     if (!in_lds && m_bytes<S_>(g) > kMaxLds) return MJX_ERANGE;
     // table in LDS: every message in one launch; else launches of as many

@@ -969,14 +969,9 @@ static int launch_update(const void* chi_in, void* chi_out, const void* biases, 
             {
                 using PC = PipeCfg<T, P, D>;
                 auto pk = k_hpr_update_pipe<T, P, D>;
-                static bool pattr = false;
-                if (!pattr) {
-                    MJX_HIP(hipFuncSetAttribute((const void*)pk, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                (int)PC::LDS), "hpr pipe set lds");
-                    pattr = true;
-                }
+                MJX_HIP(set_max_lds(pk, (int)PC::LDS), "hpr pipe set lds");
                 const int per = resident_blocks_per_cu((const void*)pk, 512, PC::LDS);
-                int64_t grid = (int64_t)kCUs * (per > 0 ? per : 1);
+                int64_t grid = (int64_t)device_cus() * (per > 0 ? per : 1);
                 if (grid > tiles) grid = tiles;
                 pk<<<(unsigned)grid, 512, PC::LDS, st>>>((const float*)chi_in, (float*)chi_out, (const float*)biases,
                                                          nbr, in_row, out_row, n, attr_plus, (float)w_plus,
@@ -986,12 +981,7 @@ static int launch_update(const void* chi_in, void* chi_out, const void* biases, 
             }
         }
         auto kern = k_hpr_update<S, T, P, D>;
-        static bool attr_set = false;   // per instantiation: opt in to > 64 KiB dynamic LDS once
-        if (!attr_set) {
-            MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS),
-                    "hpr set lds");
-            attr_set = true;
-        }
+        MJX_HIP(set_max_lds(kern, (int)C::LDS), "hpr set lds");   // opt in to > 64 KiB dynamic LDS
         kern<<<(unsigned)tiles, 64 * C::NW, C::LDS, st>>>((const S*)chi_in, (S*)chi_out, (const S*)biases, nbr,
                                                           in_row, out_row, n, attr_plus, (S)w_plus, (S)w_minus,
                                                           (S)damp);
@@ -1013,14 +1003,9 @@ static int launch_update_q(const void* chi_in, void* chi_out, const void* biases
         const int64_t tiles = (n + C::NT - 1) / C::NT;
         if (tiles > INT32_MAX) return MJX_ERANGE;
         auto pk = k_hpr_update_pipe_q<T, P, D>;
-        static bool pattr = false;
-        if (!pattr) {
-            MJX_HIP(hipFuncSetAttribute((const void*)pk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)PC::LDS),
-                    "hpr pipe q set lds");
-            pattr = true;
-        }
+        MJX_HIP(set_max_lds(pk, (int)PC::LDS), "hpr pipe q set lds");
         const int per = resident_blocks_per_cu((const void*)pk, 512, PC::LDS);
-        int64_t grid = (int64_t)kCUs * (per > 0 ? per : 1);
+        int64_t grid = (int64_t)device_cus() * (per > 0 ? per : 1);
         if (grid > tiles) grid = tiles;
         pk<<<(unsigned)grid, 512, PC::LDS, st>>>((const float*)chi_in, (float*)chi_out, (const float*)biases, nbr,
                                                  in_row, out_row, n, attr_plus, (float)w_plus, (float)w_minus,

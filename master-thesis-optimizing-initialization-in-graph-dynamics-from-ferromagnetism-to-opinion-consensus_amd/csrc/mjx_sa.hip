@@ -1864,7 +1864,7 @@ constexpr size_t kLcLdsMax = 150 * 1024;
 // waves per word column: fill the CUs with about two waves each (LDS allowing)
 static int lc_split(int64_t W, size_t lds) {
     const int64_t per_cu = (lds > 0) ? std::max<int64_t>(1, std::min<int64_t>(2, (int64_t)(160 * 1024) / (int64_t)lds)) : 2;
-    const int64_t target = (int64_t)kCUs * per_cu;
+    const int64_t target = (int64_t)device_cus() * per_cu;
     int s = 1;
     while (s < 64 && W * s * 2 <= target) s *= 2;
     return s;
@@ -2027,7 +2027,8 @@ static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d
     const int split = st.opt_split ? st.opt_split : lc_split(W, lds);
     if (split < 1 || split > 64 || (64 % split)) return MJX_EINVAL;
     if (st.opt_spec_k != 0 && st.opt_spec_k != 8 && st.opt_spec_k != 16) return MJX_EINVAL;
-    if (st.opt_flags & ~(MJX_SA_NO_SPEC | MJX_SA_NO_CONE2 | MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE | MJX_SA_LDS_PAIR))
+    if (st.opt_flags &
+        ~(MJX_SA_NO_SPEC | MJX_SA_NO_CONE2 | MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE | MJX_SA_LDS_PAIR | MJX_SA_LDS_WAVE))
         return MJX_EINVAL;
     // the one-trip and speculative kernels address a word column's cone slab
     // with 32-bit byte offsets (ConeRd)
@@ -2058,7 +2059,7 @@ static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d
     const int4* rows4 = (d == 4 || L.lo) ? (const int4*)adj : (const int4*)adj_pad;
     // 8 proposals per batch; 16 when 8 would leave CUs without a wave (few word columns):
     // configs[1] at R = 1024 3.05 -> 1.78 us per step, at R = 4096 16 is slower (3.76 vs 4.10)
-    const int spec_k = st.opt_spec_k ? st.opt_spec_k : ((W * 8 < kCUs) ? 16 : 8);
+    const int spec_k = st.opt_spec_k ? st.opt_spec_k : ((W * 8 < device_cus()) ? 16 : 8);
     const bool spec = tape && slab32 && rows4 && L.tab >= 0 && n < (int64_t(1) << (spec_k == 16 ? 27 : 28)) &&
                       !(st.opt_flags & MJX_SA_NO_SPEC) && ((d == 3 && (T == 1 || T == 2)) || (d == 4 && T == 1));
     const int hoff = slots * 64;

@@ -1692,6 +1692,559 @@ __global__ void __launch_bounds__(64) k_sa_lds_multi(const int32_t* __restrict__
     }
 }
 
+// ---------------------------------------------------------------------------
+// The whole CU for one replica (k_sa_lds_wg<D, T, NW>, d <= 4, 1 < T <= 4).
+// The one-wave kernels above leave 3 of a CU's 4 SIMDs idle: a replica's step
+// is a chain of dependent LDS round trips on one wave.  Here NW waves share the
+// replica's LDS image and evaluate NW consecutive proposals k, k+1, ..., k+NW-1
+// at once, each against the levels as they stand at the start of the round,
+// wave q exactly as k_sa_lds_fast evaluates one proposal.  The change marks
+// are one BYTE per (level, node): bit q = proposal q's C_t, so "level t as
+// proposal q sees it" is the level bit XOR mark bit q, and the bits below q in
+// the same byte say which EARLIER proposals changed that value.  A proposal q
+// stands unless an earlier proposal j of the round is taken and accepted and
+// changed something q read -- a node q reads at level l-1, or whose cached
+// level-l value it reads, changes under j only if it or a neighbour is in j's
+// C_{l-1}, i.e. only if q read j's mark at level l-1 (k_sa_lds_pair's rule;
+// level 0 by comparing with i_j).  Acceptance needs no order (delta_H of step
+// k+q depends on the schedule after q steps, computed by q multiplications as
+// the reference does, and on q's own sum change), so every wave decides its
+// own; the taken proposals are the prefix before the first conflict with a
+// taken accepted one, or up to the first stop (consensus, t cap).  Taken
+// accepted change sets are disjoint (a shared node would be a conflict), so
+// they are applied concurrently.  Workgroup barriers: one after the proposals
+// are published, one per level (marks of C_{l-1} before they are read), one
+// before the resolution.  Wave 0 parses the proposal windows (as
+// k_sa_lds_multi) into an LDS queue.  Same draws, accepts and state as k_sa_lds.
+struct GeoW {
+    int nw;        // uint32 bit words per level (even)
+    int lc;        // change-list capacity per level
+    int off_lev;   // (T+1) * nw level words
+    int off_mk;    // T * nw * 32 mark bytes (levels 1..T)
+    int off_lev0;  // nw words: level 0 at launch start
+    int off_mt;
+    int off_list;  // NW * (T+1) * lc list words (one set per wave)
+    int off_q;     // proposal queue: i[64], end[64], u[64]
+    int off_res;   // per proposal: packed word, schedule a, b after its step; control words
+    int bytes;
+};
+
+static bool geometry_wg(int64_t n, int d, int T, int NW, GeoW* g) {
+    if (n < 2 || n > 65535 || d < 1 || d > 4 || T < 1 || T > kMaxT || NW < 2 || NW > 8) return false;
+    g->nw = (int)(((n + 63) / 64) * 2);
+    int64_t lc = ball(d, T);
+    if (lc > n) lc = n;
+    lc = ((lc + 63) / 64) * 64;
+    if (lc > 4096) return false;
+    g->lc = (int)lc;
+    int64_t off = ((int64_t)n * 4 * 2 + 15) / 16 * 16;
+    g->off_lev = (int)off;   off += (int64_t)(T + 1) * g->nw * 4;
+    g->off_mk = (int)off;    off += (int64_t)T * g->nw * 32;
+    g->off_lev0 = (int)off;  off += (int64_t)g->nw * 4;
+    g->off_mt = (int)off;    off += MT_N * 4;
+    g->off_list = (int)off;  off += (int64_t)NW * (T + 1) * g->lc * 4;
+    off = (off + 15) / 16 * 16;
+    g->off_q = (int)off;     off += 64 * 4 + 64 * 4 + 64 * 8;
+    g->off_res = (int)off;   off += 8 * 4 + 8 * 8 + 8 * 8 + 4 * 4;
+    g->bytes = (int)off;
+    return (size_t)off <= kLdsMax;
+}
+
+template <int D, int T, int NW, bool TRACE>
+__global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict__ adj, int64_t n, int64_t R,
+                                                      int64_t W, u64* __restrict__ s, mjx_sa_state st, int64_t nsteps,
+                                                      double par_a, double par_b, double a_cap, double b_cap,
+                                                      int64_t t_cap, GeoW geo) {
+    static_assert(D >= 1 && D <= 4 && T >= 2 && T <= 4 && NW >= 2 && NW <= 8, "whole-CU LDS SA: d <= 4, 2 <= T <= 4");
+    constexpr int DP1 = D + 1;
+    constexpr int MAXM = 64 / DP1;                 // members of C_{t-1} one wave can expand
+    constexpr int NT = 64 * NW;
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int tid = threadIdx.x;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // this wave's proposal slot in a round
+    const int lane = tid & 63;
+    const u64 ltmask = (1ull << lane) - 1ull;
+    const int64_t r = blockIdx.x;
+    const int nw = geo.nw, lc = geo.lc;
+    const int mkl = nw * 32;                       // mark bytes per level
+    uint16_t* rows = reinterpret_cast<uint16_t*>(smem);
+    uint32_t* lev = reinterpret_cast<uint32_t*>(smem + geo.off_lev);
+    unsigned char* mk = smem + geo.off_mk;
+    uint32_t* lev0s = reinterpret_cast<uint32_t*>(smem + geo.off_lev0);
+    uint32_t* mt = reinterpret_cast<uint32_t*>(smem + geo.off_mt);
+    uint32_t* lst = reinterpret_cast<uint32_t*>(smem + geo.off_list) + w * (T + 1) * lc;   // this wave's lists
+    int* q_i = reinterpret_cast<int*>(smem + geo.off_q);
+    int* q_end = q_i + 64;
+    double* q_u = reinterpret_cast<double*>(q_end + 64);
+    uint32_t* res = reinterpret_cast<uint32_t*>(smem + geo.off_res);      // packed result per proposal
+    double* res_a = reinterpret_cast<double*>(res + 8);
+    double* res_b = res_a + 8;
+    int* ctl = reinterpret_cast<int*>(res_b + 8);
+    const uint32_t obit = 1u << w;                 // this proposal's mark bit
+    const uint32_t early = obit - 1u;              // the earlier proposals' mark bits
+
+    auto bit_of = [&](int t, int v) -> uint32_t { return (lev[t * nw + (v >> 5)] >> (v & 31)) & 1u; };
+    // node v at level t >= 1 as this proposal sees it; earlier proposals' marks into cfm
+    auto look = [&](int t, int v, uint32_t& cfm) -> uint32_t {
+        const uint32_t lw = lev[t * nw + (v >> 5)];
+        const uint32_t mb = mk[(t - 1) * mkl + v];
+        cfm |= mb & early;
+        return ((lw >> (v & 31)) ^ (mb >> w)) & 1u;
+    };
+    auto mark_word = [&](int t, int v) -> uint32_t* {
+        return reinterpret_cast<uint32_t*>(mk + (t - 1) * mkl + (v & ~3));
+    };
+    auto nbrs = [&](int v, int (&o)[D]) {
+        const uint2 x = *reinterpret_cast<const uint2*>(rows + v * 4);
+        o[0] = (int)(x.x & 0xffffu);
+        if constexpr (D > 1) o[1] = (int)(x.x >> 16);
+        if constexpr (D > 2) o[2] = (int)(x.y & 0xffffu);
+        if constexpr (D > 3) o[3] = (int)(x.y >> 16);
+    };
+    auto maj = [&](int ones, uint32_t own) -> uint32_t {       // always-stay majority (code/SA_RRG.py:19-20)
+        return (2 * ones > D) ? 1u : ((2 * ones < D) ? 0u : own);
+    };
+
+    // ---- launch setup: rows, level 0, marks cleared, MT state; levels 1..T by sweeps in LDS
+    {
+        const int32_t* g = adj + (st.rep_graph ? (int64_t)st.rep_graph[r] : 0) * n * D;
+        for (int64_t q = tid; q < n * D; q += NT) {
+            const int64_t v = q / D;
+            rows[v * 4 + (q - v * D)] = (uint16_t)g[q];
+        }
+        for (int q = tid; q < (T + 1) * nw; q += NT) lev[q] = 0u;
+        for (int q = tid; q < T * nw * 8; q += NT) reinterpret_cast<uint32_t*>(mk)[q] = 0u;
+        for (int q = tid; q < MT_N; q += NT) mt[q] = st.mt[r * MT_N + q];
+        const int64_t col = r >> 6;
+        const u64 rbit = 1ull << (r & 63);
+        __syncthreads();
+        for (int64_t v0 = (int64_t)w * 64; v0 < (int64_t)nw * 32; v0 += NT) {
+            const int64_t v = v0 + lane;
+            const bool b = v < n && (s[v * W + col] & rbit);
+            const u64 m = __ballot(b);
+            if (lane < 2) {
+                const uint32_t x = (uint32_t)(m >> (32 * lane));
+                lev[(v0 >> 5) + lane] = x;
+                lev0s[(v0 >> 5) + lane] = x;
+            }
+        }
+        __syncthreads();
+        for (int t = 1; t <= T; ++t) {
+            for (int64_t v0 = (int64_t)w * 64; v0 < (int64_t)nw * 32; v0 += NT) {
+                const int v = (int)(v0 + lane);
+                uint32_t nb = 0;
+                if (v < n) {
+                    int nv[D];
+                    nbrs(v, nv);
+                    int ones = 0;
+#pragma unroll
+                    for (int q = 0; q < D; ++q) ones += (int)bit_of(t - 1, nv[q]);
+                    nb = maj(ones, bit_of(t - 1, v));
+                }
+                const u64 m = __ballot(nb != 0);
+                if (lane < 2) lev[t * nw + (int)(v0 >> 5) + lane] = (uint32_t)(m >> (32 * lane));
+            }
+            __syncthreads();
+        }
+    }
+
+    double a = st.a[r], b = st.b[r];
+    int64_t t = st.t[r], sum_end = st.sum_end[r];
+    int done = st.done[r];
+    int idx = st.mt_idx[r];
+    int ties = 0;
+    const uint32_t rng = (uint32_t)(n - 1);
+    uint32_t mask = rng;
+    mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+    double inv_n = 1.0 / (double)n;
+    asm volatile("" : "+v"(a), "+v"(b), "+v"(par_a), "+v"(par_b), "+v"(a_cap), "+v"(b_cap), "+v"(inv_n));
+
+    // ---- proposal windows (wave 0): lane j holds proposal j, mirrored in the LDS queue
+    int pb_i = 0, pb_end = 0;
+    uint32_t pb_w1 = 0, pb_w2 = 0;
+    double pb_u = 0.0;
+    int npend = 0, pk = 0;
+    auto parse = [&](bool one) {
+        for (;;) {
+            if (idx >= MT_N) {
+                if (one) break;
+                lds_twist(mt, lane);
+                idx = 0;
+            }
+            const int lim = (MT_N - idx < 64) ? MT_N - idx : 64;
+            uint32_t tw = 0, y = 0;
+            bool ok = false;
+            if (lane < lim) {
+                tw = mt_temper(mt[idx + lane]);
+                y = tw & mask;
+                ok = y <= rng;
+            }
+            const u64 okm = __ballot(ok);
+            int pos = 0, got = 0;
+            while (pos < 64 && npend < 64) {
+                const u64 m = okm >> pos;
+                if (!m) break;
+                const int f = pos + __ffsll((unsigned long long)m) - 1;
+                if (f + 2 >= lim) break;
+                const int iv = __builtin_amdgcn_readlane((int)y, f);
+                const uint32_t w1 = (uint32_t)__builtin_amdgcn_readlane((int)tw, f + 1);
+                const uint32_t w2 = (uint32_t)__builtin_amdgcn_readlane((int)tw, f + 2);
+                if (lane == npend) { pb_i = iv; pb_w1 = w1; pb_w2 = w2; pb_end = idx + f + 3; }
+                ++npend;
+                ++got;
+                pos = f + 3;
+            }
+            if (got > 0) { idx += pos; break; }
+            if (one) break;
+            if (!okm) { idx += lim; continue; }
+            const int f = __ffsll((unsigned long long)okm) - 1;
+            if (f > 0) { idx += f; continue; }
+            // i is the window's first word and rand()'s two words cross the end of
+            // the state: the serial draw twists between them, as numpy does
+            const int iv = __builtin_amdgcn_readlane((int)y, 0);
+            idx += 1;
+            if (idx >= MT_N) { lds_twist(mt, lane); idx = 0; }
+            const uint32_t w1 = mt_temper(mt[idx]);
+            idx += 1;
+            if (idx >= MT_N) { lds_twist(mt, lane); idx = 0; }
+            const uint32_t w2 = mt_temper(mt[idx]);
+            idx += 1;
+            if (lane == npend) { pb_i = iv; pb_w1 = w1; pb_w2 = w2; pb_end = idx; }
+            ++npend;
+            break;
+        }
+        pb_u = mt_double(pb_w1, pb_w2);
+    };
+
+    int lc_c[T + 1];
+    uint32_t lc_v[T + 1];
+    bool lc_in[T + 1];
+    int lc_n[T + 1];
+    bool lc_fast[T + 1];
+    bool drew = false;
+    int64_t k = 0;
+    while (k < nsteps && done == 0) {
+        if (w == 0) {
+            const int avail = npend - pk;
+            bool re = false;
+            if (avail < NW && idx + 64 <= MT_N) {
+                // carry the unconsumed proposals to lanes 0.. and append one window
+                // (no twist can fall under a carried proposal)
+                const int src = (lane + pk < 64) ? lane + pk : 63;
+                pb_i = __shfl(pb_i, src, 64);
+                pb_end = __shfl(pb_end, src, 64);
+                pb_w1 = (uint32_t)__shfl((int)pb_w1, src, 64);
+                pb_w2 = (uint32_t)__shfl((int)pb_w2, src, 64);
+                npend = avail;
+                pk = 0;
+                parse(true);
+                if (npend == 0) parse(false);
+                re = true;
+            } else if (avail == 0) {
+                npend = 0;
+                pk = 0;
+                parse(false);
+                re = true;
+            }
+            if (re) {
+                q_i[lane] = pb_i;
+                q_u[lane] = pb_u;
+            }
+            if (lane == 0) {
+                ctl[0] = npend;
+                ctl[1] = pk;
+            }
+        }
+        __syncthreads();                                   // the round's proposals are published
+        drew = true;
+        const int npd = __builtin_amdgcn_readfirstlane(ctl[0]);
+        const int pks = __builtin_amdgcn_readfirstlane(ctl[1]);
+        int nq = npd - pks;
+        if (nq > NW) nq = NW;
+        if ((int64_t)nq > nsteps - k) nq = (int)(nsteps - k);
+        const bool act = w < nq;
+        const int iv = __builtin_amdgcn_readfirstlane(q_i[pks + (act ? w : 0)]);
+        const double u = q_u[pks + (act ? w : 0)];
+        int ip[NW - 1];                                    // the earlier proposals' i (level-0 conflicts)
+#pragma unroll
+        for (int j = 0; j < NW - 1; ++j) ip[j] = (act && j < w) ? q_i[pks + j] : -1;
+        const uint32_t old_i = bit_of(0, iv);
+        uint32_t cf = 0;                                   // bit j: read something proposal j changed
+        int cand, nv[D];
+        int last;
+        // ---- level 1: i and its neighbours, level 0 with i flipped
+        {
+            int ri[D];
+            nbrs(iv, ri);
+            cand = iv;
+#pragma unroll
+            for (int q = 0; q < D; ++q)
+                if (lane == q + 1) cand = ri[q];
+            bool dup = lane > 0 && cand == iv;
+#pragma unroll
+            for (int q = 0; q < D; ++q)
+                if (q + 1 < lane) dup |= ri[q] == cand;
+            nbrs(cand, nv);
+            const bool live = act && lane <= D && !dup;
+            int ones = 0;
+#pragma unroll
+            for (int e = 0; e < D; ++e) ones += (int)(bit_of(0, nv[e]) ^ (nv[e] == iv));
+#pragma unroll
+            for (int j = 0; j < NW - 1; ++j) {
+                bool hit = cand == ip[j];
+#pragma unroll
+                for (int e = 0; e < D; ++e) hit |= nv[e] == ip[j];
+                if (live && hit) cf |= 1u << j;
+            }
+            const uint32_t own = bit_of(0, cand) ^ (cand == iv);
+            const uint32_t nb = maj(ones, own);
+            const uint32_t cur = bit_of(1, cand);
+            const bool chg = live && nb != cur;
+            const u64 m = __ballot(chg);
+            if (chg) {
+                atomicOr(mark_word(1, cand), obit << (8 * (cand & 3)));
+                lst[lc + __popcll(m & ltmask)] = (uint32_t)cand;
+            }
+            lc_c[1] = cand;
+            lc_v[1] = cur;
+            lc_in[1] = chg;
+            lc_fast[1] = true;
+            lc_n[1] = __popcll(m);
+            last = lc_n[1] ? 1 : 0;
+        }
+        int64_t ds = 0;
+#pragma unroll
+        for (int l = 2; l <= T; ++l) {
+            lc_in[l] = false;
+            lc_fast[l] = true;
+            lc_n[l] = 0;
+            __syncthreads();                               // every proposal's marks of C_{l-1}
+            if (last != l - 1) continue;                   // (wave-uniform)
+            const int np = lc_n[l - 1];
+            int nc = 0;
+            if (np <= MAXM && lc_fast[l - 1]) {
+                // candidates: member sl = lane / (d+1) of C_{l-1}, j = 0 the member
+                // itself, j > 0 its j-th neighbour; member sl's lane found by
+                // ds_permute (every member pushes its lane id to lane rank) and
+                // ds_bpermute (lane sl's entry pulled)
+                const u64 pm = __ballot(lc_in[l - 1]);
+                const int sl = lane / DP1, j = lane - sl * DP1;
+                const int rank = __popcll(pm & ltmask);
+                const int slot = __builtin_amdgcn_ds_permute((lc_in[l - 1] ? rank : 63) * 4, lane);
+                const int src = __builtin_amdgcn_ds_bpermute(sl * 4, slot) & 63;
+                const int mc = __shfl(cand, src, 64);
+                int pn[D];
+#pragma unroll
+                for (int e = 0; e < D; ++e) pn[e] = __shfl(nv[e], src, 64);
+                const bool act2 = sl < np;
+                int c2 = mc;
+#pragma unroll
+                for (int e = 0; e < D; ++e)
+                    if (j == e + 1) c2 = pn[e];
+                if (!act2) c2 = iv;
+                int nv2[D];
+                nbrs(c2, nv2);
+                int ones = 0;
+                uint32_t cfm = 0;
+#pragma unroll
+                for (int e = 0; e < D; ++e) ones += (int)look(l - 1, nv2[e], cfm);
+                const uint32_t own = look(l - 1, c2, cfm);
+                if (act2) cf |= cfm;
+                const uint32_t nb = maj(ones, own);
+                const uint32_t cur = bit_of(l, c2);
+                const bool chg = act2 && nb != cur;
+                const uint32_t mb = obit << (8 * (c2 & 3));
+                bool add = chg;
+                if (l == T) {
+                    // the last level counts distinct nodes: the first mark wins
+                    if (chg) add = (atomicOr(mark_word(l, c2), mb) & mb) == 0u;
+                } else if (chg) {
+                    // inner levels keep repeats (marks, clears and the accepted values
+                    // are idempotent; the next level's dedup absorbs them)
+                    atomicOr(mark_word(l, c2), mb);
+                }
+                const u64 m = __ballot(add);
+                if (add) lst[l * lc + __popcll(m & ltmask)] = (uint32_t)c2;
+                nc = __popcll(m);
+                cand = c2;
+#pragma unroll
+                for (int e = 0; e < D; ++e) nv[e] = nv2[e];
+                lc_c[l] = c2;
+                lc_v[l] = cur;
+                lc_in[l] = add;
+                if (l == T) ds = 2 * ((int64_t)__popcll(__ballot(add && cur == 0u)) - (int64_t)__popcll(__ballot(add && cur != 0u)));
+            } else {
+                // this wave's LDS-list path (its lists hold every level; deduped here)
+                const uint32_t* prev = lst + (l - 1) * lc;
+                uint32_t* curl = lst + l * lc;
+                const int m = np * DP1;
+                int64_t dsl = 0;
+                for (int base = 0; base < m; base += 64) {
+                    const int q = base + lane;
+                    bool add = false;
+                    int cd = 0;
+                    uint32_t cur = 0;
+                    if (q < m) {
+                        const int slot = q / DP1, jj = q - slot * DP1;
+                        const int v = (int)prev[slot];
+                        cd = (jj == 0) ? v : (int)rows[v * 4 + jj - 1];
+                        int nv2[D];
+                        nbrs(cd, nv2);
+                        int ones = 0;
+                        uint32_t cfm = 0;
+#pragma unroll
+                        for (int e = 0; e < D; ++e) ones += (int)look(l - 1, nv2[e], cfm);
+                        const uint32_t own = look(l - 1, cd, cfm);
+                        cf |= cfm;
+                        const uint32_t nb = maj(ones, own);
+                        const uint32_t mb = obit << (8 * (cd & 3));
+                        cur = bit_of(l, cd);
+                        if (nb != cur) add = (atomicOr(mark_word(l, cd), mb) & mb) == 0u;
+                    }
+                    const u64 bal = __ballot(add);
+                    if (add) curl[nc + __popcll(bal & ltmask)] = (uint32_t)cd;
+                    nc += __popcll(bal);
+                    dsl += 2 * ((int64_t)__popcll(__ballot(add && cur == 0u)) - (int64_t)__popcll(__ballot(add && cur != 0u)));
+                }
+                if (l == T) ds = dsl;
+                lc_fast[l] = false;
+            }
+            lc_n[l] = nc;
+            if (nc > 0) last = l;
+        }
+        if (last != T) ds = 0;
+        // ---- delta_H and the Metropolis test of this wave's proposal, step k + w
+        // (code/SA_RRG.py:37,74-76); the schedule after w steps (:80-81)
+        double ah = a, bh = b;
+        for (int q = 0; q < w; ++q) {
+            if (ah < a_cap) ah = par_a * ah;
+            if (bh < b_cap) bh = par_b * bh;
+        }
+        const double anx = (ah < a_cap) ? par_a * ah : ah;          // the schedule after this step
+        const double bnx = (bh < b_cap) ? par_b * bh : bh;
+        const double si = old_i ? 1.0 : -1.0;
+        const double t1 = (-2.0 * ah) * si;
+        const double t2 = bh * (double)(-ds);
+        const double num = t1 + t2;
+        // u < min(1, exp(-dE)) by an fp32 exp where u is farther from it than that
+        // exp's error, else by the reference's float64 dE and exp (as k_sa_lds_fast)
+        const float xf = (float)(-num * inv_n);
+        const float ef = __expf(xf);
+        const float mg = ef * (1e-6f * (1.0f + fabsf(xf))) + 1e-37f;
+        bool acc, tie = false;
+        double dE = 0.0;
+        if (fabs(u - (double)ef) > (double)mg) {
+            acc = u < (double)ef;
+            if (TRACE && st.tr_dE) dE = num / (double)n;
+        } else {
+            dE = num / (double)n;
+            const double e = exp(-dE);
+            const double prob = (e < 1.0) ? e : 1.0;
+            acc = u < prob;
+            tie = e < 1.0 && fabs(u - e) <= 4.0 * (nextafter(e, 2.0) - e);
+        }
+        uint32_t cfw = 0;
+#pragma unroll
+        for (int j = 0; j < NW - 1; ++j)
+            if (__ballot((cf >> j) & 1u)) cfw |= 1u << j;
+        if (lane == 0) {
+            res[w] = cfw | (acc ? 0x100u : 0u) | (tie ? 0x200u : 0u) | ((uint32_t)(ds & 0xffff) << 16);
+            res_a[w] = anx;
+            res_b[w] = bnx;
+        }
+        __syncthreads();                                   // every proposal's result
+        // ---- resolve in proposal order (every wave alike): the taken proposals are
+        // the prefix before the first that read an accepted earlier one's change, or
+        // up to a stop
+        uint32_t accm = 0;
+        int taken = 0;
+        bool stop = false;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) {
+            if (q < nq && !stop) {
+                const uint32_t pq = res[q];
+                if (pq & accm & 0xffu) {
+                    stop = true;
+                } else {
+                    const bool aq = (pq >> 8) & 1u;
+                    if (aq) {
+                        sum_end += (int64_t)(int16_t)(pq >> 16);
+                        accm |= 1u << q;
+                    }
+                    ties += (int)((pq >> 9) & 1u);
+                    t += 1;                                             // (code/SA_RRG.py:77,82)
+                    ++taken;
+                    if (TRACE && w == q && lane == 0) {
+                        if (st.tr_i) st.tr_i[(k + q) * R + r] = iv;
+                        if (st.tr_acc) st.tr_acc[(k + q) * R + r] = aq ? 1 : 0;
+                        if (st.tr_sum) st.tr_sum[(k + q) * R + r] = sum_end;
+                        if (st.tr_dE) st.tr_dE[(k + q) * R + r] = dE;
+                    }
+                    if (t > t_cap) { done = 2; stop = true; }               // (:84)
+                    else if (sum_end == n) { done = 1; stop = true; }       // m(s_endstate(s)) == 1
+                }
+            }
+        }
+        a = res_a[taken - 1];                                       // (:80-81) after the taken steps
+        b = res_b[taken - 1];
+        // ---- the taken accepted proposals' changes; every proposal clears its marks
+        const bool mine = w < taken && ((accm >> w) & 1u);
+        if (mine && lane == 0) atomicXor(&lev[iv >> 5], 1u << (iv & 31));
+#pragma unroll
+        for (int l = 1; l <= T; ++l) {
+            if (l <= last) {
+                if (lc_fast[l]) {
+                    if (lc_in[l]) {
+                        const int v = lc_c[l];
+                        const uint32_t bt = 1u << (v & 31);
+                        if (mine) {
+                            if (lc_v[l]) atomicAnd(&lev[l * nw + (v >> 5)], ~bt);
+                            else atomicOr(&lev[l * nw + (v >> 5)], bt);
+                        }
+                        mk[(l - 1) * mkl + v] = 0;                  // every mark of the byte is this round's
+                    }
+                } else {
+                    const uint32_t* cl = lst + l * lc;
+                    for (int q = lane; q < lc_n[l]; q += 64) {
+                        const int v = (int)cl[q];
+                        if (mine) atomicXor(&lev[l * nw + (v >> 5)], 1u << (v & 31));
+                        mk[(l - 1) * mkl + v] = 0;
+                    }
+                }
+            }
+        }
+        k += taken;
+        pk += taken;
+    }
+    if (w == 0 && drew) idx = __builtin_amdgcn_readlane(pb_end, pk - 1);
+    if (TRACE && tid == 0) {
+        for (; k < nsteps; ++k) {
+            if (st.tr_i) st.tr_i[k * R + r] = -1;
+            if (st.tr_acc) st.tr_acc[k * R + r] = -1;
+            if (st.tr_sum) st.tr_sum[k * R + r] = sum_end;
+            if (st.tr_dE) st.tr_dE[k * R + r] = 0.0;
+        }
+    }
+    __syncthreads();
+    {
+        const int64_t col = r >> 6;
+        for (int64_t v = tid; v < n; v += NT) {
+            if (((lev[v >> 5] ^ lev0s[v >> 5]) >> (v & 31)) & 1u)
+                atomicXor((unsigned long long*)&s[v * W + col], 1ull << (r & 63));
+        }
+        for (int q = tid; q < MT_N; q += NT) st.mt[r * MT_N + q] = mt[q];
+    }
+    if (tid == 0) {
+        st.mt_idx[r] = idx;
+        st.a[r] = a;
+        st.b[r] = b;
+        st.t[r] = t;
+        st.sum_end[r] = sum_end;
+        st.done[r] = done;
+        if (st.tr_tie) st.tr_tie[r] += ties;
+    }
+}
+
 }  // namespace salds
 }  // namespace mjx
 
@@ -1715,6 +2268,34 @@ extern "C" int64_t mjx_sa_lds_bytes(int64_t n, int d, int p, int c) {
     return g.bytes;
 }
 
+// The LDS bytes and threads per workgroup of the kernel mjx_sa_lds_steps runs
+// for (n, d, p, c) and the kernel options (opt_flags, opt_split): the same
+// selection as mjx_sa_lds_steps below.
+extern "C" int64_t mjx_sa_lds_plan(int64_t n, int d, int p, int c, uint32_t flags, int split, int* threads) {
+    if (p < 0 || c < 0) return -1;
+    const int T = p + c - 1;
+    salds::Geo g;
+    if (!salds::geometry(n, d, T, &g)) return -1;
+    int th = 64;
+    int64_t bytes = g.bytes;
+    const bool small_d = d == 3 || d == 4;
+    salds::GeoW gw;
+    salds::Geo g2;
+    const int nwv = (split == 4) ? 4 : 8;
+    if (!(flags & (MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE | MJX_SA_LDS_PAIR)) && small_d && T == 1) {
+        // k_sa_lds_multi: the one-plane geometry
+    } else if (!(flags & (MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE | MJX_SA_LDS_WAVE)) && small_d && T >= 2 && T <= 4 &&
+               salds::geometry_wg(n, d, T, nwv, &gw)) {
+        th = 64 * nwv;
+        bytes = gw.bytes;
+    } else if (!(flags & (MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE)) && small_d && T <= 4 &&
+               salds::geometry(n, d, T, &g2, 2)) {
+        bytes = g2.bytes;
+    }
+    if (threads) *threads = th;
+    return bytes;
+}
+
 extern "C" int mjx_sa_lds_steps(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R, uint64_t* s,
                                 mjx_sa_state* stp, int64_t nsteps, double par_a, double par_b, double a_cap,
                                 double b_cap, int64_t t_cap, void* stream) {
@@ -1724,7 +2305,8 @@ extern "C" int mjx_sa_lds_steps(const int32_t* adj, int64_t n, int d, int p, int
     if (!salds::geometry(n, d, T, &g)) return MJX_ERANGE;
     const mjx_sa_state st = *stp;
     if (!st.mt || !st.mt_idx || !st.a || !st.b || !st.t || !st.sum_end || !st.done) return MJX_EINVAL;
-    if (st.opt_flags & ~(MJX_SA_NO_SPEC | MJX_SA_NO_CONE2 | MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE | MJX_SA_LDS_PAIR))
+    if (st.opt_flags &
+        ~(MJX_SA_NO_SPEC | MJX_SA_NO_CONE2 | MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE | MJX_SA_LDS_PAIR | MJX_SA_LDS_WAVE))
         return MJX_EINVAL;
     if (nsteps == 0) return MJX_OK;
     if (R > INT32_MAX) return MJX_ERANGE;
@@ -1750,6 +2332,33 @@ extern "C" int mjx_sa_lds_steps(const int32_t* adj, int64_t n, int d, int p, int
         };
         if (d == 3) return trm ? gom(salds::k_sa_lds_multi<3, 8, true>) : gom(salds::k_sa_lds_multi<3, 8, false>);
         return trm ? gom(salds::k_sa_lds_multi<4, 8, true>) : gom(salds::k_sa_lds_multi<4, 8, false>);
+    }
+    salds::GeoW gw;
+    const int nwv = (st.opt_split == 4) ? 4 : 8;
+    if (!(st.opt_flags & (MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE | MJX_SA_LDS_WAVE)) && (d == 3 || d == 4) && T >= 2 &&
+        T <= 4 && salds::geometry_wg(n, d, T, nwv, &gw)) {
+        const bool trw = st.tr_i || st.tr_acc || st.tr_sum || st.tr_dE;
+        auto gow = [&](auto kern) -> int {
+            MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, gw.bytes),
+                    "sa_lds lds");
+            kern<<<(unsigned)R, 64 * nwv, (size_t)gw.bytes, hs>>>(adj, n, R, W, (u64*)s, st, nsteps, par_a, par_b,
+                                                                 a_cap, b_cap, t_cap, gw);
+            MJX_LAUNCH_CHECK("k_sa_lds_wg");
+            return MJX_OK;
+        };
+#define MJX_LDS_WG3(DD, TT)                                                                                       \
+        if (nwv == 4) return trw ? gow(salds::k_sa_lds_wg<DD, TT, 4, true>) : gow(salds::k_sa_lds_wg<DD, TT, 4, false>); \
+        return trw ? gow(salds::k_sa_lds_wg<DD, TT, 8, true>) : gow(salds::k_sa_lds_wg<DD, TT, 8, false>);
+#define MJX_LDS_WG(DD)                       \
+        switch (T) {                         \
+            case 2: { MJX_LDS_WG3(DD, 2) }   \
+            case 3: { MJX_LDS_WG3(DD, 3) }   \
+            default: { MJX_LDS_WG3(DD, 4) }  \
+        }
+        if (d == 3) { MJX_LDS_WG(3) }
+        MJX_LDS_WG(4)
+#undef MJX_LDS_WG
+#undef MJX_LDS_WG3
     }
     salds::Geo g2;
     if (!(st.opt_flags & (MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE)) && (d == 3 || d == 4) && T <= 4 &&

@@ -47,7 +47,7 @@ def schedule_constants(n):
 
 
 KERNEL_FLAGS = {"no_spec": _lib.MJX_SA_NO_SPEC, "no_cone2": _lib.MJX_SA_NO_CONE2, "lds_serial": _lib.MJX_SA_LDS_SERIAL,
-                "lds_single": _lib.MJX_SA_LDS_SINGLE, "lds_pair": _lib.MJX_SA_LDS_PAIR}
+                "lds_single": _lib.MJX_SA_LDS_SINGLE, "lds_pair": _lib.MJX_SA_LDS_PAIR, "lds_wave": _lib.MJX_SA_LDS_WAVE}
 
 
 def _graph_stack(N, R, graph_of):
@@ -78,6 +78,11 @@ def _graph_stack(N, R, graph_of):
     n, d = next(iter(shapes))
     if all(isinstance(x, torch.Tensor) and x.is_cuda for x in gl):
         stack = torch.stack([x.to(torch.int32) for x in gl]).reshape(G * n, d).contiguous()
+        if stack.numel():
+            # the kernels index LDS and HBM with these entries: one device reduction
+            lo, hi = torch.aminmax(stack)
+            if int(lo.item()) < 0 or int(hi.item()) >= n:
+                raise ValueError("adjacency index out of range")
     else:
         a = np.stack([x.cpu().numpy() if isinstance(x, torch.Tensor) else np.asarray(x) for x in gl])
         if a.size and (a.min() < 0 or a.max() >= n):
@@ -108,7 +113,9 @@ class SAReplicas:
         (mjx_sa_lightcone_steps); ``"auto"``: lds where it fits, else cone;
         same results in every layout.  ``kernel``: light-cone kernel
         selection passed to the ABI (tests, tuning): ``split`` (waves per word
-        column), ``spec_k`` (8 or 16), ``no_spec``, ``no_cone2``, ``lds_serial``, ``lds_single``, ``lds_pair``; the results
+        column), ``spec_k`` (8 or 16), ``no_spec``, ``no_cone2``, ``lds_serial``, ``lds_single``, ``lds_pair``,
+        ``lds_wave`` (one wave per replica instead of the whole-CU kernel at
+        p+c-1 >= 2; ``split`` = 4 or 8 waves for the latter); the results
         never depend on it."""
         seeds = np.asarray(seeds, dtype=np.int64).reshape(-1)
         if seeds.size == 0 or seeds.min() < 0 or seeds.max() > 0xFFFFFFFF:
@@ -189,7 +196,10 @@ class SAReplicas:
         self.mode = mode
         if layout not in ("auto", "lds", "cone", "rec", "levels"):
             raise ValueError(f"unknown light-cone layout {layout!r}")
-        lds_bytes = _lib.load().mjx_sa_lds_bytes(n, self.d, self.p, self.c)
+        # the LDS bytes and workgroup size of the LDS kernel these options select
+        lds_threads = _lib.ctypes.c_int(64)
+        lds_bytes = _lib.load().mjx_sa_lds_plan(n, self.d, self.p, self.c, flags, self._state.opt_split,
+                                                _lib.ctypes.byref(lds_threads))
         lds_fits = 0 < lds_bytes <= 160 * 1024
         # A replica in LDS is one workgroup for a whole call: the lane-held step (d <= 4,
         # k_sa_lds_fast) runs SA_RRG.py's shapes fastest (d=4, n=1e4, 64 replicas: p=c=1
@@ -199,7 +209,8 @@ class SAReplicas:
         # record layout for one shared graph (configs[1]: 4.31 -> 4.20 us per step at
         # R = 4096 vs the plain cone, same box), else to the cone.
         spec = (self.d == 3 and T <= 2) or (self.d == 4 and T == 1)
-        one_round = lds_fits and R <= _device.cu_count() * max(1, (160 * 1024) // lds_bytes)
+        per_cu = max(1, min((160 * 1024) // max(lds_bytes, 1), 32 // max(1, lds_threads.value // 64)))
+        one_round = lds_fits and R <= _device.cu_count() * per_cu
         if layout == "auto":
             if lds_fits and (one_round or not spec):
                 layout = "lds"

@@ -111,3 +111,33 @@ def test_build_id_binds_library_to_its_sources(mjx_mod, tmp_path):
     hdr.write_text(hdr.read_text().replace("MJX_H", "MJX_H_"))
     with pytest.raises(mjx_mod.MjxError):
         _lib.verify_build_id(lib, str(csrc), str(inc))
+
+
+def test_device_memo_selftest_without_gpu(mjx_mod):
+    """CU counts, occupancy and dynamic-LDS opt-ins are memoised per device id,
+    not per process: the memo's host logic, no HIP call."""
+    lib = mjx_mod.load_library()
+    assert lib.mjx_selftest_devmemo() == 0
+
+
+def test_sa_lds_plan_names_the_kernel_that_runs(mjx_mod):
+    """mjx_sa_lds_plan reports the LDS bytes and workgroup size of the kernel
+    mjx_sa_lds_steps selects (the auto layout sized occupancy
+    with the one-plane bytes): the whole-CU kernel at p+c-1 >= 2 (8 or 4
+    waves), the paired one-wave kernel with lds_wave, the eight-proposal one at
+    p+c-1 = 1."""
+    import ctypes
+    lib = mjx_mod.load_library()
+    L = mjx_mod._lib
+    th = ctypes.c_int(0)
+    one = lib.mjx_sa_lds_bytes(10_000, 4, 3, 1)
+    wg8 = lib.mjx_sa_lds_plan(10_000, 4, 3, 1, 0, 0, ctypes.byref(th))
+    assert th.value == 512 and one < wg8 <= 160 * 1024
+    wg4 = lib.mjx_sa_lds_plan(10_000, 4, 3, 1, 0, 4, ctypes.byref(th))
+    assert th.value == 256 and wg4 < wg8
+    pair = lib.mjx_sa_lds_plan(10_000, 4, 3, 1, L.MJX_SA_LDS_WAVE, 0, ctypes.byref(th))
+    assert th.value == 64 and one < pair
+    assert lib.mjx_sa_lds_plan(10_000, 4, 3, 1, L.MJX_SA_LDS_SINGLE, 0, ctypes.byref(th)) == one and th.value == 64
+    assert lib.mjx_sa_lds_plan(10_000, 4, 1, 1, 0, 0, ctypes.byref(th)) == lib.mjx_sa_lds_bytes(10_000, 4, 1, 1)
+    assert th.value == 64
+    assert lib.mjx_sa_lds_plan(100_000, 4, 3, 1, 0, 0, ctypes.byref(th)) == -1

@@ -50,6 +50,12 @@ def _check(tr, conf, t, graphs, graph_of, seeds, p, c, K, replicas):
     (3, 200, 2, 3, 20, 300, {}, "lightcone", "lds"),
     (3, 64, 2, 1, 40, 400, {}, "lightcone", "lds"),                         # small graph: many non-tree balls
     (4, 64, 2, 2, 40, 400, {}, "lightcone", "lds"),                         # T = 3, levels beyond one wave
+    (4, 300, 3, 1, 65, 300, {"lds_wave": True}, "lightcone", "lds"),       # one wave per replica (pair)
+    (4, 300, 3, 1, 65, 300, {"split": 4}, "lightcone", "lds"),              # whole CU, 4 waves
+    (4, 64, 2, 2, 40, 400, {"lds_wave": True}, "lightcone", "lds"),
+    (3, 64, 2, 1, 40, 400, {"split": 4}, "lightcone", "lds"),               # many conflicts, 4 waves
+    (4, 40, 3, 1, 40, 600, {}, "lightcone", "lds"),                         # n=40: most rounds conflict
+    (3, 30, 2, 2, 40, 600, {}, "lightcone", "lds"),
     (4, 200, 1, 1, 5, 40, {}, "rollout", None),
 ])
 def test_distinct_graphs_match_oracle(mjx_mod, d, n, p, c, R, K, kernel, mode, layout):
@@ -122,3 +128,28 @@ def test_sa_run_distinct_graphs_to_consensus(mjx_mod, n, N_stat, seed, graph_see
         assert np.array_equal(res["conf"][k], o["conf"])
         assert res["mag_reached"][k] == o["mag_reached"]
         assert res["done"][k] == 1
+
+
+@pytest.mark.parametrize("d,n,p,c,kernel", [
+    (3, 64, 1, 1, {}), (4, 64, 1, 1, {}), (3, 1000, 1, 1, {}), (4, 1000, 1, 1, {}),   # k_sa_lds_multi<D,8,false>
+    (4, 64, 3, 1, {}), (4, 1000, 3, 1, {}), (3, 500, 2, 1, {}),                       # k_sa_lds_wg<D,T,8,false>
+    (4, 1000, 3, 1, {"split": 4}), (4, 1000, 3, 1, {"lds_wave": True}),
+])
+def test_lds_no_trace_matches_oracle(mjx_mod, d, n, p, c, kernel):
+    """The kernels run() and the bench use (no trace buffers: TRACE=false
+    instantiations) against the oracle on conf, t and the MT19937 stream each
+    replica hands back, over two ragged calls."""
+    R, K1, K2 = 70, 700, 233
+    graphs = _graphs(mjx_mod, d, n, R, 300)
+    seeds = list(range(2000, 2000 + R))
+    sa = mjx_mod.SAReplicas(graphs, p, c, seeds, layout="lds", kernel=kernel)
+    sa.steps(K1)
+    sa.steps(K2)
+    conf, t = sa.conf().cpu().numpy(), sa.t.cpu().numpy()
+    mt, idx = sa.mt_state()
+    for r in (0, 1, 35, 64, 69):
+        st = np.random.RandomState(seeds[r]).get_state()
+        o = fast.sa_loop(graphs[r], p, c, seeds[r], max_steps=K1 + K2, mt_state=(st[1], st[2]))
+        assert o["num_steps"] == t[r], r
+        assert np.array_equal(conf[r], o["conf"]), r
+        assert np.array_equal(mt[r], o["mt_state"][0]) and idx[r] == o["mt_state"][1], r

@@ -21,6 +21,13 @@ for s in $STEPS; do
       timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest ${PYTEST_PATHS:-tests} -m gpu -x -v --timeout 300 --timeout-method thread \
         ${PYTEST_ARGS:-} > $OUT/pytest_gpu.log 2>&1
       stop_if_fatal $? tests ;;
+    py)
+      # one probe script: PY="tools/sa_probe3.py --no-cone" PY_LOG=name
+      timeout -k 10 ${PY_TIMEOUT:-300} python -u $PY > $OUT/${PY_LOG:-py}.log 2>&1
+      stop_if_fatal $? "py $PY" ;;
+    py2)
+      timeout -k 10 ${PY2_TIMEOUT:-300} python -u $PY2 > $OUT/${PY2_LOG:-py2}.log 2>&1
+      stop_if_fatal $? "py2 $PY2" ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
       stop_if_fatal $? smoke ;;

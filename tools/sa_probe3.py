@@ -1,6 +1,10 @@
 """Step time of the light-cone SA at SA_RRG.py's shapes (d=4, N=1e4, 64
 replicas on distinct graphs): p=c=1 (configs[0]) and p=3, c=1 (the script),
-LDS-resident replicas vs the HBM cone layout."""
+LDS-resident replicas (every LDS kernel) vs the HBM cone layout.
+
+    python tools/sa_probe3.py [--no-cone] [--R 64] [--n 10000]
+"""
+import argparse
 import sys
 import time
 
@@ -8,18 +12,36 @@ sys.path.insert(0, ".")
 import torch  # noqa: E402
 import mjx  # noqa: E402
 
-n, d, R = 10_000, 4, 64
+ap = argparse.ArgumentParser()
+ap.add_argument("--no-cone", action="store_true")
+ap.add_argument("--R", type=int, default=64)
+ap.add_argument("--n", type=int, default=10_000)
+ap.add_argument("--pc", default="1,1;3,1")
+args = ap.parse_args()
+n, d, R = args.n, 4, args.R
 graphs = [mjx.random_regular_graph(d, n, seed=7000 + k) for k in range(R)]
-for (p, c) in ((1, 1), (3, 1)):
-    for layout in ("lds", "lds-pair", "lds-single", "cone"):
-        K = 20000 if (layout.startswith("lds") or p == 1) else 1000
-        kern = {"lds-single": {"lds_single": True}, "lds-pair": {"lds_pair": True}}.get(layout)
-        sa = mjx.SAReplicas(graphs, p, c, list(range(R)), layout=layout.split("-")[0], kernel=kern)
+VARIANTS = {
+    # name: (layout, kernel options)
+    "lds": ("lds", None),                                   # the default LDS kernel for (p, c)
+    "lds-wg4": ("lds", {"split": 4}),                       # whole CU, 4 waves (p+c-1 >= 2)
+    "lds-pair": ("lds", {"lds_wave": True, "lds_pair": True}),   # one wave, two proposals per step
+    "lds-single": ("lds", {"lds_single": True}),            # one wave, one proposal per step
+    "cone": ("cone", None),
+}
+for pc in args.pc.split(";"):
+    p, c = (int(x) for x in pc.split(","))
+    for name, (layout, kern) in VARIANTS.items():
+        if name == "cone" and args.no_cone:
+            continue
+        if name == "lds-wg4" and p + c - 1 < 2:
+            continue
+        K = 20000 if (layout == "lds" or p == 1) else 1000
+        sa = mjx.SAReplicas(graphs, p, c, list(range(R)), layout=layout, kernel=kern)
         sa.steps(K)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         sa.steps(K)
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
-        print(f"p={p} c={c} {layout}: {1e6 * el / K:.3f} us/step, {R * K / el:.3g} proposals/s, "
+        print(f"p={p} c={c} {name}: {1e6 * el / K:.3f} us/step, {R * K / el:.3g} proposals/s, "
               f"done {int((sa.done != 0).sum())}/{R}", flush=True)
