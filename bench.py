@@ -67,6 +67,11 @@ def parse():
     ap.add_argument("--consensus-script-s", type=float, default=20.0,
                     help="wall budget of the n=1e4 (SA_RRG.py's own size) leg")
     ap.add_argument("--no-consensus", action="store_true")
+    ap.add_argument("--global-n", type=int, default=1000,
+                    help="n of the sa_global leg (SA_RRG.py's own run: N_stat replicas back to back on one stream)")
+    ap.add_argument("--global-nstat", type=int, default=5)
+    ap.add_argument("--global-max-s", type=float, default=30.0, help="wall cap per replica of the sa_global leg")
+    ap.add_argument("--no-global", action="store_true")
     ap.add_argument("--no-sa", action="store_true")
     ap.add_argument("--giant-n", type=int, default=1_000_000_000)
     ap.add_argument("--giant-d", type=int, default=6)
@@ -434,6 +439,33 @@ def bench_sa_consensus(args, rank, world, dist, dev):
         seeds = list(range(10_000 + rank * R, 10_000 + (rank + 1) * R))
         out[tag] = {"n": n, **_sa_until_done(mjx, graphs, p, c, seeds, cap)}
     return out
+
+
+def bench_sa_global(args, rank, world, dist, dev):
+    """The reference's own run, literally (code/SA_RRG.py:44-92): N_stat = 5
+    replicas BACK TO BACK on ONE numpy stream seeded once, each on a fresh
+    d=4 random regular graph, p=3, c=1, until m_final = 1 -- mjx.sa_run(...,
+    stream="global"), replica k+1's draws continuing where replica k's last
+    rand() left the stream.  One replica at a time is one workgroup: the
+    whole-CU LDS kernel (k_sa_lds_wg).  Per replica: wall time to consensus,
+    num_steps, mag_reached, us per proposal.  (Each rank runs its own seed.)"""
+    import mjx
+    n, d, p, c = args.global_n, 4, 3, 1
+    seed, graph_seed = args.seed + 5 + 1000 * rank, args.seed + 70 + 1000 * rank
+    res = mjx.sa_run(d, n, p, c, N_stat=args.global_nstat, seed=seed, graph_seed=graph_seed, stream="global",
+                     max_seconds=args.global_max_s)
+    reps = []
+    for k in range(args.global_nstat):
+        st, w = float(res["num_steps"][k]), float(res["wall_s"][k])
+        if w == 0.0:
+            break                                       # not run: an earlier replica hit the wall cap
+        reps.append({"num_steps": st, "mag_reached": float(res["mag_reached"][k]), "done": int(res["done"][k]),
+                     "wall_s": w, "us_per_step": 1e6 * w / max(st, 1.0)})
+    return {"config": f"SA_RRG.py run: d={d} RRG n={n}, p={p} c={c}, N_stat={args.global_nstat} replicas back to "
+                      f"back on one numpy stream (np.random.seed({seed})), fresh graph per replica "
+                      f"(graph_seed {graph_seed}), until m_final = 1; wall cap {args.global_max_s} s per replica",
+            "replicas": reps, "replicas_done": sum(r["done"] == 1 for r in reps),
+            "wall_s_total": sum(r["wall_s"] for r in reps)}
 
 
 def bench_er(args, rank, world, dist, dev):
@@ -945,6 +977,9 @@ def main():
     cons = None
     if not args.no_sa and not args.no_consensus and args.consensus_replicas > 0:
         cons = bench_sa_consensus(args, rank, world, dist, dev)
+    sglob = None
+    if not args.no_sa and not args.no_global and args.global_nstat > 0:
+        sglob = bench_sa_global(args, rank, world, dist, dev)
 
     del s0, out, tmp, counts, chk, o2
     torch.cuda.empty_cache()
@@ -963,7 +998,7 @@ def main():
     if not args.no_giant and args.giant_n > 0:
         giant = bench_giant(args, rank, world, dist, dev)
 
-    for leg in (sa_res, c1, cons, er, hpr, bdcm, giant):
+    for leg in (sa_res, c1, cons, sglob, er, hpr, bdcm, giant):
         if leg is not None:
             leg["n_gpus"] = world
             leg["ranks"] = world
@@ -1002,6 +1037,7 @@ def main():
             "sa": sa_res,
             "sa_c1": c1,
             "sa_consensus": cons,
+            "sa_global": sglob,
             "er": er,
             "hpr": hpr,
             "bdcm": bdcm,

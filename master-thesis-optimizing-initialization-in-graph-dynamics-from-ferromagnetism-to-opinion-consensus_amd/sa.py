@@ -358,15 +358,18 @@ class SAReplicas:
         mt = self.mt.cpu().numpy().view(np.uint32).reshape(self.R, 624).copy()
         return mt, self.mt_idx.cpu().numpy().copy()
 
-    def run(self, max_steps=None, chunk=256, max_chunk=16384):
+    def run(self, max_steps=None, chunk=256, max_chunk=16384, max_seconds=None):
         """Step until every replica has reached consensus or the t cap
-        (``while(m_final<1)``, code/SA_RRG.py:72), or ``max_steps``.  The
-        done flags are read once per chunk; chunks grow from ``chunk`` to
-        ``max_chunk`` steps (a finished replica skips the rest of a chunk)."""
+        (``while(m_final<1)``, code/SA_RRG.py:72), or ``max_steps``, or
+        ``max_seconds`` of wall time.  The done flags are read once per
+        chunk; chunks grow from ``chunk`` to ``max_chunk`` steps (a finished
+        replica skips the rest of a chunk)."""
+        import time
+        t0 = time.perf_counter()
         taken = 0
         while not self.all_done():
             k = chunk if max_steps is None else min(chunk, max_steps - taken)
-            if k <= 0:
+            if k <= 0 or (max_seconds is not None and time.perf_counter() - t0 >= max_seconds):
                 break
             self.steps(k)
             taken += k
@@ -435,7 +438,7 @@ def _graph_list(d, n, N_stat, N, graphs, graph_seed):
 
 
 def sa_run(d, n, p, c, par_a=PAR_A, par_b=PAR_B, N_stat=5, seed=0, seeds=None, N=None, graph_seed=None,
-           max_steps=None, graphs=None, stream="independent", mode="auto"):
+           max_steps=None, graphs=None, stream="independent", mode="auto", max_seconds=None):
     """Drop-in for the SA_RRG.py experiment (code/SA_RRG.py:44-92).
 
     Returns the reference's output arrays ``mag_reached, num_steps, conf,
@@ -455,15 +458,23 @@ def sa_run(d, n, p, c, par_a=PAR_A, par_b=PAR_B, N_stat=5, seed=0, seeds=None, N
       * ``stream="independent"`` — replica k owns ``np.random.seed(seeds[k])``
         (default seed + k); all N_stat replicas run together, bit-packed, each
         on its own graph (graphs stacked in HBM, SAReplicas(graph_of=...)).
+
+    ``max_seconds``: wall budget per replica (global stream) or for the whole
+    run (independent streams); a replica stopped by it has ``done`` = 0, and
+    with the global stream the replicas after it are not run (their draws
+    would start where an unfinished run left the stream).  ``wall_s`` in the
+    result: seconds per replica (global) or for the run (independent).
     """
+    import time
     gl = _graph_list(d, n, N_stat, N, graphs, graph_seed)
     R = len(gl)
     res = {"mag_reached": np.zeros(R), "num_steps": np.zeros(R), "conf": np.zeros((R, n)),
-           "done": np.zeros(R, dtype=np.int32), "near_ties": np.zeros(R, dtype=np.int32)}
+           "done": np.zeros(R, dtype=np.int32), "near_ties": np.zeros(R, dtype=np.int32), "wall_s": np.zeros(R)}
 
     def store(k, out, j):
         for key in res:
-            res[key][k] = out[key][j]
+            if key in out:
+                res[key][k] = out[key][j]
 
     if stream == "global":
         # replica k+1's draws start where replica k's last rand() left the one
@@ -473,10 +484,17 @@ def sa_run(d, n, p, c, par_a=PAR_A, par_b=PAR_B, N_stat=5, seed=0, seeds=None, N
         for k, g in enumerate(gl):
             sa = SAReplicas(g, p, c, [int(seed) & 0xFFFFFFFF], par_a=par_a, par_b=par_b, mode=mode, tape=0,
                             mt_state=state)
-            sa.run(max_steps=max_steps)
-            store(k, sa.results(), 0)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            sa.run(max_steps=max_steps, max_seconds=max_seconds)
+            torch.cuda.synchronize()
+            res["wall_s"][k] = time.perf_counter() - t0
+            out = sa.results()
+            store(k, out, 0)
             state = sa.mt_state()
             del sa
+            if max_seconds is not None and out["done"][0] == 0 and (max_steps is None or out["num_steps"][0] < max_steps):
+                break                       # stopped by the wall budget: the stream cannot be handed on
     elif stream == "independent":
         if seeds is None:
             seeds = [seed + k for k in range(R)]
@@ -494,7 +512,11 @@ def sa_run(d, n, p, c, par_a=PAR_A, par_b=PAR_B, N_stat=5, seed=0, seeds=None, N
         src = stack[0] if len(stack) == 1 else stack
         sa = SAReplicas(src, p, c, seeds, par_a=par_a, par_b=par_b, mode=mode,
                         graph_of=None if len(stack) == 1 else graph_of)
-        sa.run(max_steps=max_steps)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        sa.run(max_steps=max_steps, max_seconds=max_seconds)
+        torch.cuda.synchronize()
+        res["wall_s"][:] = time.perf_counter() - t0
         out = sa.results()
         for k in range(R):
             store(k, out, k)

@@ -328,7 +328,10 @@ def gen_hpr_full():
     with open(HPR_PATH) as f:
         src = f.read()
     out = {}
-    for (n, d, p, c, TT, gseed, tseed) in ((40, 4, 1, 1, 300, 31, 7), (30, 3, 2, 1, 300, 32, 8)):
+    # p+c = 4 cases: the decay-split fp32 loop state (hpr_run's fp32 default) applies there
+    for (n, d, p, c, TT, gseed, tseed) in ((40, 4, 1, 1, 300, 31, 7), (30, 3, 2, 1, 300, 32, 8),
+                                           (40, 4, 2, 2, 300, 33, 9), (40, 3, 3, 1, 300, 34, 10),
+                                           (60, 4, 3, 1, 300, 35, 11)):
         tmp = tempfile.mktemp(suffix=".npz")
         s = src
         for old, new in (("n=10000", f"n={n}"), ("d=4", f"d={d}"), ("p=1", f"p={p}"), ("c=1", f"c={c}"),

@@ -193,3 +193,58 @@ def test_hpr_any_degree_through_the_class_kernel(mjx_mod, d, p, c):
         got = mjx_mod.HPr_dp(torch.tensor(chi, dtype=dtype, device="cuda"), torch.tensor(b, dtype=dtype, device="cuda"),
                              plan, p, c, 1, 25 * n, 0.4)
         assert rownorm_err(got[torch.from_numpy(rows).cuda()].cpu().numpy(), want) <= TOL[dtype], dtype
+
+
+def _fp64_min_margin(mjx_mod, plan, p, c, TT, tseed):
+    """The float64 device loop step by step on the reference's torch CPU stream
+    (hpr_run's draws): (iterations, min over iterations and nodes of
+    |marg+ - marg-| / (marg+ + marg-)), the margin of the decision
+    code/HPR_pytorch_RRG.py:138 takes."""
+    gen = torch.Generator().manual_seed(tseed)
+    nc = 4 ** (p + c)
+    chi0 = torch.rand((2 * plan.E, nc), dtype=torch.float64, generator=gen)
+    chi0 = chi0 / torch.sum(chi0, axis=1, keepdims=True)
+    b0 = torch.rand((plan.n, 2), dtype=torch.float64, generator=gen)
+    b0 = b0 / torch.sum(b0, axis=1, keepdims=True)
+    st = mjx_mod.HPRState(plan, p, c, chi0, b0, dtype=torch.float64, layout="ref")
+    st.s_from_biases()
+    m, margin = st.sum_end() / plan.n, float("inf")
+    while m < 1:
+        total = st.step(generator=gen)
+        mg = st.marg.double()
+        margin = min(margin, float(((mg[:, 1] - mg[:, 0]).abs() / mg.sum(dim=1)).min()))
+        m = 2 if st.t > TT else total / plan.n
+    return st.t, margin
+
+
+def test_hpr_full_script_float32_loop(mjx_mod):
+    """fp32 whole loop (hpr_run's default: the decay-split layout where p+c = 4,
+    the reference layout otherwise) against the reference's own whole-script
+    runs (code/HPR_pytorch_RRG.py:342-362, run in float64 by the reference,
+    :11).  Where the float64 loop's marginals never come within 1e-5 of a tie
+    (relative, the decision of :138), the fp32 run must reproduce num_steps and
+    conf exactly; runs with a near-tie are listed, and counted (VERDICT r03
+    item 4)."""
+    full = load_golden("hpr_fullscript.npz")
+    keys = sorted({k.rsplit("_", 1)[0] for k in full if k.endswith("_params")})
+    report, strict = [], 0
+    for key in keys:
+        n, d, p, c, TT, tseed = (int(x) for x in full[f"{key}_params"])
+        nbrs = full[f"{key}_graphs"][0].astype(np.int64)
+        plan = mjx_mod.HPRPlan(full[f"{key}_edges"], n, d, nbrs)
+        steps64, margin = _fp64_min_margin(mjx_mod, plan, p, c, TT, tseed)
+        res = mjx_mod.hpr_run(d, n, p, c, TT=TT, edges=full[f"{key}_edges"], nbrs=nbrs, seed=tseed,
+                              dtype=torch.float32)
+        same = (res["num_steps"][0] == full[f"{key}_num_steps"][0] and
+                np.array_equal(res["conf"][0], full[f"{key}_conf"][0]))
+        layout = "q" if mjx_mod._lib.load().mjx_hpr_q_supported(mjx_mod._lib.MJX_F32, d, p, c) == 1 else "ref"
+        near = margin < 1e-5
+        report.append(f"{key}: layout {layout}, fp64 steps {steps64}, min margin {margin:.3g}"
+                      f"{' NEAR-TIE' if near else ''}, fp32 {'equal' if same else 'differs'}")
+        if not near:
+            strict += 1
+            assert same, report[-1]
+    print("\nfp32 whole-loop vs reference script:\n  " + "\n  ".join(report))
+    print(f"  {strict} of {len(keys)} runs without a near-tie, all reproduced; "
+          f"{len(keys) - strict} near-tie runs listed")
+    assert strict >= 1

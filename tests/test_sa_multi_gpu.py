@@ -153,3 +153,25 @@ def test_lds_no_trace_matches_oracle(mjx_mod, d, n, p, c, kernel):
         assert o["num_steps"] == t[r], r
         assert np.array_equal(conf[r], o["conf"]), r
         assert np.array_equal(mt[r], o["mt_state"][0]) and idx[r] == o["mt_state"][1], r
+
+
+@pytest.mark.parametrize("n,N_stat,seed,graph_seed", [(1000, 2, 5, 70)])
+def test_sa_run_global_stream_to_consensus(mjx_mod, n, N_stat, seed, graph_seed):
+    """SA_RRG.py's own semantics at n = 1000: ONE numpy
+    stream seeded once, the replicas back to back on it, each on a fresh graph,
+    run to m_final = 1 at the script's p=3, c=1 (code/SA_RRG.py:58-88); the
+    whole-CU LDS kernel on one replica at a time.  Equal to the C oracle
+    continued on one MT19937 stream (4.4e4 + 4.5e4 proposals)."""
+    d, p, c = 4, 3, 1
+    res = mjx_mod.sa_run(d, n, p, c, N_stat=N_stat, seed=seed, graph_seed=graph_seed, stream="global")
+    st = np.random.RandomState(seed).get_state()
+    state = (st[1], st[2])
+    for k in range(N_stat):
+        g = mjx_mod.random_regular_graph(d, n, seed=graph_seed + k)
+        o = fast.sa_loop(g, p, c, seed, mt_state=state)
+        state = o["mt_state"]
+        assert o["done"] == 1 and res["done"][k] == 1
+        assert res["num_steps"][k] == o["num_steps"], k
+        assert np.array_equal(res["conf"][k], o["conf"]), k
+        assert res["mag_reached"][k] == o["mag_reached"], k
+        assert res["wall_s"][k] > 0
