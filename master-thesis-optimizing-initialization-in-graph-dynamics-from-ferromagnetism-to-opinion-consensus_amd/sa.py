@@ -233,20 +233,14 @@ class SAReplicas:
             # levels s_1..s_T = onestep^t(s); the rollout ping-pong buffers are reused
             self._levels = [self.tmp1, self.tmp2][:T] + [torch.empty_like(self.s) for _ in range(T - 2)]
             self._lvl = (_lib.ctypes.c_void_p * T)(*[t.data_ptr() for t in self._levels])
-            _lib.call("mjx_sa_lightcone_prepare", _device.ptr(self.adj), n, self.d, self.p, self.c, R,
-                      _device.ptr(self.rep_graph) if self.rep_graph is not None else None,
-                      _device.ptr(self.s), self._lvl, _device.stream_handle())
             if layout == "cone":
                 lv = _lib.load().mjx_sa_cone_words(self.p, self.c)
                 self.cone = torch.empty(n * W * lv, dtype=i64, device=dev)
-                _lib.call("mjx_sa_cone_pack", n, self.p, self.c, R, _device.ptr(self.s), self._lvl,
-                          _device.ptr(self.cone), _device.stream_handle())
             elif layout == "rec":
                 # the cone with each node's adjacency row in front of its levels
                 lv = _lib.load().mjx_sa_rec_words(self.d, self.p, self.c)
                 self.cone = torch.empty(n * W * lv, dtype=i64, device=dev)
-                _lib.call("mjx_sa_rec_pack", _device.ptr(self.adj), n, self.d, self.p, self.c, R,
-                          _device.ptr(self.s), self._lvl, _device.ptr(self.cone), _device.stream_handle())
+            self._build_levels()
             if layout == "cone" and self.d == 3:
                 # rows padded to 16 B: one load per row in the one-round-trip step
                 # (graph g of a stack at rows g*n .. g*n + n - 1)
@@ -261,6 +255,70 @@ class SAReplicas:
                 self.tape_u = torch.empty(self.tape_cap * R, dtype=torch.float64, device=dev)
                 self._state.tape_i, self._state.tape_u = self.tape_i.data_ptr(), self.tape_u.data_ptr()
                 self._state.tape_cap = self.tape_cap
+
+    def _build_levels(self):
+        """The cached levels onestep^t(s), t = 1..T, from s (light-cone layouts
+        other than lds, which rebuilds them in LDS every call), packed into the
+        cone / record layout when in use."""
+        n, R = self.n, self.R
+        _lib.call("mjx_sa_lightcone_prepare", _device.ptr(self.adj), n, self.d, self.p, self.c, R,
+                  _device.ptr(self.rep_graph) if self.rep_graph is not None else None,
+                  _device.ptr(self.s), self._lvl, _device.stream_handle())
+        if self.layout == "cone":
+            _lib.call("mjx_sa_cone_pack", n, self.p, self.c, R, _device.ptr(self.s), self._lvl,
+                      _device.ptr(self.cone), _device.stream_handle())
+        elif self.layout == "rec":
+            _lib.call("mjx_sa_rec_pack", _device.ptr(self.adj), n, self.d, self.p, self.c, R,
+                      _device.ptr(self.s), self._lvl, _device.ptr(self.cone), _device.stream_handle())
+
+    # -- checkpoint / resume (long runs to consensus: SA_RRG.py's n = 1e4 runs
+    # take 1e7-1e9 proposals per replica) -------------------------------------
+    _CKPT_STATE = ("s", "mt", "mt_idx", "a", "b", "t", "sum_end", "done", "ties")
+
+    def checkpoint(self):
+        """Everything a resumed run needs, as host arrays: the configuration
+        (replica-packed bits), every replica's MT19937 stream (numpy's state,
+        exactly), a, b, t, sum(s_end), the done flags (code/SA_RRG.py:65-85's
+        loop state) and the parameters.  ``resume`` continues it bit for bit."""
+        if self.mode == "lightcone" and getattr(self, "tape_cap", 0):
+            raise ValueError("the proposal tape draws ahead: checkpoint needs tape=0 (or the lds / rollout modes)")
+        torch.cuda.current_stream().synchronize()
+        out = {k: getattr(self, k).cpu().numpy().copy() for k in self._CKPT_STATE}
+        out["params"] = np.array([self.n, self.d, self.p, self.c, self.R], dtype=np.int64)
+        out["schedule"] = np.array([self.par_a, self.par_b, self.a0, self.b0, self.a_cap, self.b_cap],
+                                   dtype=np.float64)
+        out["t_cap"] = np.array(self.t_cap, dtype=np.int64)
+        return out
+
+    def save_checkpoint(self, path):
+        np.savez(path, **self.checkpoint())
+
+    @classmethod
+    def resume(cls, N, ckpt, graph_of=None, mode="auto", layout="auto", kernel=None, tape=0):
+        """A run continued from ``checkpoint()`` (a dict, or the path of a
+        ``save_checkpoint`` file) on the same graphs ``N``: the same proposals,
+        accepts and final state as the uninterrupted run."""
+        if not isinstance(ckpt, dict):
+            with np.load(ckpt, allow_pickle=False) as z:
+                ckpt = {k: z[k] for k in z.files}
+        n, d, p, c, R = (int(x) for x in ckpt["params"])
+        par_a, par_b, a0, b0 = (float(x) for x in ckpt["schedule"][:4])
+        sa = cls(N, p, c, np.zeros(R, dtype=np.int64), par_a=par_a, par_b=par_b, a0=a0, b0=b0, mode=mode,
+                 tape=tape, layout=layout, graph_of=graph_of, kernel=kernel)
+        if (sa.n, sa.d, sa.R) != (n, d, R):
+            raise ValueError(f"checkpoint of n={n}, d={d}, R={R} does not fit these graphs (n={sa.n}, d={sa.d})")
+        sa.t_cap = int(ckpt["t_cap"])
+        for k in cls._CKPT_STATE:
+            dst = getattr(sa, k)
+            src = torch.from_numpy(np.ascontiguousarray(ckpt[k])).to(dst.device)
+            if src.shape != dst.shape or src.dtype != dst.dtype:
+                raise ValueError(f"checkpoint field {k}: {tuple(src.shape)} {src.dtype}, expected "
+                                 f"{tuple(dst.shape)} {dst.dtype}")
+            dst.copy_(src)
+        if sa.mode == "lightcone" and sa.layout != "lds":
+            sa._build_levels()
+        torch.cuda.current_stream().synchronize()
+        return sa
 
     # -- stepping -----------------------------------------------------------
     def steps(self, k, trace=False):

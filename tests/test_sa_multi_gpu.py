@@ -6,6 +6,7 @@ code/SA_RRG.py:63-88) on ITS graph: proposals, accepts, sum(s_end), delta_H,
 final conf and step count."""
 import numpy as np
 import pytest
+import torch
 
 from oracle import fast
 
@@ -175,3 +176,36 @@ def test_sa_run_global_stream_to_consensus(mjx_mod, n, N_stat, seed, graph_seed)
         assert np.array_equal(res["conf"][k], o["conf"]), k
         assert res["mag_reached"][k] == o["mag_reached"], k
         assert res["wall_s"][k] > 0
+
+
+@pytest.mark.parametrize("d,n,p,c,mode,layout", [
+    (4, 300, 3, 1, "lightcone", "lds"),          # whole-CU kernel
+    (4, 400, 1, 1, "lightcone", "lds"),          # eight proposals per step
+    (3, 500, 2, 1, "lightcone", "cone"),         # HBM levels rebuilt from s on resume
+    (4, 200, 1, 1, "rollout", None),
+])
+def test_checkpoint_resume_equals_uninterrupted(mjx_mod, tmp_path, d, n, p, c, mode, layout):
+    """A long SA run (SA_RRG.py's n = 1e4 runs take 1e7-1e9 proposals per
+    replica) checkpointed after K1 proposals and resumed in a new object from
+    the file makes exactly the uninterrupted run's proposals: same conf, t,
+    a, b, sum(s_end) and MT19937 streams after K1 + K2."""
+    R, K1, K2 = 20, 600, 500
+    graphs = _graphs(mjx_mod, d, n, R, 500)
+    seeds = list(range(77, 77 + R))
+    kw = dict(mode=mode, layout=layout or "auto", tape=0)
+    ref = mjx_mod.SAReplicas(graphs, p, c, seeds, **kw)
+    ref.steps(K1)
+    ref.steps(K2)
+    run = mjx_mod.SAReplicas(graphs, p, c, seeds, **kw)
+    run.steps(K1)
+    path = tmp_path / "sa_ckpt.npz"
+    run.save_checkpoint(path)
+    del run
+    res = mjx_mod.SAReplicas.resume(graphs, str(path), mode=mode, layout=layout or "auto")
+    res.steps(K2)
+    for k in ("t", "a", "b", "sum_end", "done"):
+        assert torch.equal(getattr(res, k), getattr(ref, k)), k
+    assert torch.equal(res.conf(), ref.conf())
+    m1, i1 = res.mt_state()
+    m2, i2 = ref.mt_state()
+    assert np.array_equal(m1, m2) and np.array_equal(i1, i2)

@@ -1,5 +1,5 @@
 #!/bin/bash
-# PMC passes (one counter group per run) over the C5 binned sweep (tools/bin_exp.py).
+# PMC passes (one counter group per run) over the C5 binned sweep (tools/giant_time.py).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd)
@@ -12,7 +12,7 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CU_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_A
            "GRBM_GUI_ACTIVE GRBM_COUNT"; do
   i=$((i+1))
   ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 90 rocprofv3 --pmc $grp -d "$R/$OUT/p$i" -o run \
-      --output-format csv -- python3 "$R/tools/bin_exp.py" 1e9 6 0 ) > $OUT/p$i.log 2>&1 || { echo "pmc pass $i failed $?"; tail -5 $OUT/p$i.log; exit 1; }
+      --output-format csv -- python3 "$R/tools/giant_time.py" 1e9 6 3 ) > $OUT/p$i.log 2>&1 || { echo "pmc pass $i failed $?"; tail -5 $OUT/p$i.log; exit 1; }
 done
 python3 - <<'PY'
 import csv, glob

@@ -1,4 +1,5 @@
-"""Light-cone SA step time vs waves per word column (MJX_LC_SPLIT) at configs[1]."""
+"""Light-cone SA step time vs waves per word column (kernel option ``split``) at
+configs[1], cone layout, one-trip step (no speculative batches)."""
 import os
 import sys
 import time
@@ -12,8 +13,8 @@ n, d, p, c, R = 1_000_000, 3, 2, 1, 4096
 adj = mjx.random_regular_graph(d, n, seed=7)
 ref = None
 for sp in (1, 2, 4, 8, 16):
-    os.environ["MJX_LC_SPLIT"] = str(sp)
-    sa = mjx.SAReplicas(adj, p, c, np.arange(R), mode="lightcone")
+    sa = mjx.SAReplicas(adj, p, c, np.arange(R), mode="lightcone", layout="cone",
+                        kernel={"split": sp, "no_spec": True})
     tr = sa.steps(200, trace=True)
     acc = tr["accept"].cpu().numpy()
     if ref is None:
