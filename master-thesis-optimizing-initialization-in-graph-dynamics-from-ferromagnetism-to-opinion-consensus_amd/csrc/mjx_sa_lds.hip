@@ -2245,6 +2245,408 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
     }
 }
 
+// ---------------------------------------------------------------------------
+// The whole CU at p + c - 1 = 1 (k_sa_lds_wg1<D, NW, NQ>, configs[0]'s
+// SA_RRG.py p = c = 1): NW waves of NQ lane groups, k_sa_lds_multi's step in
+// every wave, K = NW * NQ consecutive proposals per round.  Proposal q's
+// evaluation stands after an accepted earlier j unless i_j is one of the nodes
+// q's lanes read at level 0 (k_sa_lds_multi's rule); across waves that test is
+// a TAG word per node: bit j of tag[v] = (i_j == v), set by each proposal with
+// one LDS atomic before the round's reads, so a lane ORs the tags of the nodes
+// it reads.  The resolution is lane-parallel: proposal q's packed result sits
+// in lane q, one ballot finds the first proposal that read an accepted
+// earlier one's i, a prefix sum the first stop.  Rounds: proposals published
+// (wave 0 parses up to three stream windows), tags set, level 1 evaluated and
+// results written, each behind a workgroup barrier.
+struct GeoW1 {
+    int nw;
+    int off_lev;    // 2 * nw level words (levels 0 and 1)
+    int off_lev0;
+    int off_tag;    // nw * 32 tag words
+    int off_mt;
+    int off_q;      // i[64], u[64]
+    int off_res;    // per proposal: packed word, a, b after its step, dE
+    int bytes;
+};
+
+static bool geometry_wg1(int64_t n, int d, int K, GeoW1* g) {
+    if (n < 2 || n > 65535 || d < 1 || d > 4 || K < 2 || K > 32) return false;
+    g->nw = (int)(((n + 63) / 64) * 2);
+    int64_t off = ((int64_t)n * 4 * 2 + 15) / 16 * 16;
+    g->off_lev = (int)off;   off += (int64_t)2 * g->nw * 4;
+    g->off_lev0 = (int)off;  off += (int64_t)g->nw * 4;
+    g->off_tag = (int)off;   off += (int64_t)g->nw * 32 * 4;
+    g->off_mt = (int)off;    off += MT_N * 4;
+    off = (off + 15) / 16 * 16;
+    g->off_q = (int)off;     off += 64 * 4 + 64 * 8;
+    g->off_res = (int)off;   off += 64 * 4 + 64 * 8 * 3 + 4 * 4;
+    g->bytes = (int)off;
+    return (size_t)off <= kLdsMax;
+}
+
+template <int D, int NW, int NQ, bool TRACE>
+__global__ void __launch_bounds__(64 * NW) k_sa_lds_wg1(const int32_t* __restrict__ adj, int64_t n, int64_t R,
+                                                       int64_t W, u64* __restrict__ s, mjx_sa_state st,
+                                                       int64_t nsteps, double par_a, double par_b, double a_cap,
+                                                       double b_cap, int64_t t_cap, GeoW1 geo) {
+    constexpr int G = 64 / NQ;                     // lanes per proposal
+    constexpr int K = NW * NQ;                     // proposals per round
+    static_assert(D >= 1 && D <= 4 && G >= D + 1 && K <= 32 && NW >= 2, "whole-CU LDS SA at T = 1");
+    constexpr int NT = 64 * NW;
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int tid = threadIdx.x;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lane = tid & 63;
+    const int gq = lane / G, gl = lane % G;
+    const int qi = w * NQ + gq;                    // this lane group's proposal in the round
+    const int64_t r = blockIdx.x;
+    const int nw = geo.nw;
+    uint16_t* rows = reinterpret_cast<uint16_t*>(smem);
+    uint32_t* lev = reinterpret_cast<uint32_t*>(smem + geo.off_lev);
+    uint32_t* lev0s = reinterpret_cast<uint32_t*>(smem + geo.off_lev0);
+    uint32_t* tag = reinterpret_cast<uint32_t*>(smem + geo.off_tag);
+    uint32_t* mt = reinterpret_cast<uint32_t*>(smem + geo.off_mt);
+    int* q_i = reinterpret_cast<int*>(smem + geo.off_q);
+    double* q_u = reinterpret_cast<double*>(q_i + 64);
+    uint32_t* res = reinterpret_cast<uint32_t*>(smem + geo.off_res);
+    double* res_a = reinterpret_cast<double*>(res + 64);
+    double* res_b = res_a + 64;
+    double* res_e = res_b + 64;
+    int* ctl = reinterpret_cast<int*>(res_e + 64);
+    auto bit_of = [&](int t, int v) -> uint32_t { return (lev[t * nw + (v >> 5)] >> (v & 31)) & 1u; };
+    auto nbrs = [&](int v, int (&o)[D]) {
+        const uint2 x = *reinterpret_cast<const uint2*>(rows + v * 4);
+        o[0] = (int)(x.x & 0xffffu);
+        if constexpr (D > 1) o[1] = (int)(x.x >> 16);
+        if constexpr (D > 2) o[2] = (int)(x.y & 0xffffu);
+        if constexpr (D > 3) o[3] = (int)(x.y >> 16);
+    };
+    auto maj = [&](int ones, uint32_t own) -> uint32_t {       // always-stay majority (code/SA_RRG.py:19-20)
+        return (2 * ones > D) ? 1u : ((2 * ones < D) ? 0u : own);
+    };
+
+    // ---- launch setup: rows, level 0, tags cleared, MT state; level 1 by one sweep
+    {
+        const int32_t* g = adj + (st.rep_graph ? (int64_t)st.rep_graph[r] : 0) * n * D;
+        for (int64_t q = tid; q < n * D; q += NT) {
+            const int64_t v = q / D;
+            rows[v * 4 + (q - v * D)] = (uint16_t)g[q];
+        }
+        for (int q = tid; q < 2 * nw; q += NT) lev[q] = 0u;
+        for (int q = tid; q < nw * 32; q += NT) tag[q] = 0u;
+        for (int q = tid; q < MT_N; q += NT) mt[q] = st.mt[r * MT_N + q];
+        const int64_t col = r >> 6;
+        const u64 rbit = 1ull << (r & 63);
+        __syncthreads();
+        for (int64_t v0 = (int64_t)w * 64; v0 < (int64_t)nw * 32; v0 += NT) {
+            const int64_t v = v0 + lane;
+            const bool b = v < n && (s[v * W + col] & rbit);
+            const u64 m = __ballot(b);
+            if (lane < 2) {
+                const uint32_t x = (uint32_t)(m >> (32 * lane));
+                lev[(v0 >> 5) + lane] = x;
+                lev0s[(v0 >> 5) + lane] = x;
+            }
+        }
+        __syncthreads();
+        for (int64_t v0 = (int64_t)w * 64; v0 < (int64_t)nw * 32; v0 += NT) {
+            const int v = (int)(v0 + lane);
+            uint32_t nb = 0;
+            if (v < n) {
+                int nv[D];
+                nbrs(v, nv);
+                int ones = 0;
+#pragma unroll
+                for (int q = 0; q < D; ++q) ones += (int)bit_of(0, nv[q]);
+                nb = maj(ones, bit_of(0, v));
+            }
+            const u64 m = __ballot(nb != 0);
+            if (lane < 2) lev[nw + (int)(v0 >> 5) + lane] = (uint32_t)(m >> (32 * lane));
+        }
+        __syncthreads();
+    }
+
+    double a = st.a[r], b = st.b[r];
+    int64_t t = st.t[r], sum_end = st.sum_end[r];
+    int done = st.done[r];
+    int idx = st.mt_idx[r];
+    int ties = 0;
+    const uint32_t rng = (uint32_t)(n - 1);
+    uint32_t mask = rng;
+    mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+    double inv_n = 1.0 / (double)n;
+    asm volatile("" : "+v"(a), "+v"(b), "+v"(par_a), "+v"(par_b), "+v"(a_cap), "+v"(b_cap), "+v"(inv_n));
+
+    // ---- proposal windows (wave 0), as k_sa_lds_multi
+    int pb_i = 0, pb_end = 0;
+    uint32_t pb_w1 = 0, pb_w2 = 0;
+    double pb_u = 0.0;
+    int npend = 0, pk = 0;
+    auto parse = [&](bool one) {
+        for (;;) {
+            if (idx >= MT_N) {
+                if (one) break;
+                lds_twist(mt, lane);
+                idx = 0;
+            }
+            const int lim = (MT_N - idx < 64) ? MT_N - idx : 64;
+            uint32_t tw = 0, y = 0;
+            bool ok = false;
+            if (lane < lim) {
+                tw = mt_temper(mt[idx + lane]);
+                y = tw & mask;
+                ok = y <= rng;
+            }
+            const u64 okm = __ballot(ok);
+            int pos = 0, got = 0;
+            while (pos < 64 && npend < 64) {
+                const u64 m = okm >> pos;
+                if (!m) break;
+                const int f = pos + __ffsll((unsigned long long)m) - 1;
+                if (f + 2 >= lim) break;
+                const int iv = __builtin_amdgcn_readlane((int)y, f);
+                const uint32_t w1 = (uint32_t)__builtin_amdgcn_readlane((int)tw, f + 1);
+                const uint32_t w2 = (uint32_t)__builtin_amdgcn_readlane((int)tw, f + 2);
+                if (lane == npend) { pb_i = iv; pb_w1 = w1; pb_w2 = w2; pb_end = idx + f + 3; }
+                ++npend;
+                ++got;
+                pos = f + 3;
+            }
+            if (got > 0) { idx += pos; break; }
+            if (one) break;
+            if (!okm) { idx += lim; continue; }
+            const int f = __ffsll((unsigned long long)okm) - 1;
+            if (f > 0) { idx += f; continue; }
+            const int iv = __builtin_amdgcn_readlane((int)y, 0);
+            idx += 1;
+            if (idx >= MT_N) { lds_twist(mt, lane); idx = 0; }
+            const uint32_t w1 = mt_temper(mt[idx]);
+            idx += 1;
+            if (idx >= MT_N) { lds_twist(mt, lane); idx = 0; }
+            const uint32_t w2 = mt_temper(mt[idx]);
+            idx += 1;
+            if (lane == npend) { pb_i = iv; pb_w1 = w1; pb_w2 = w2; pb_end = idx; }
+            ++npend;
+            break;
+        }
+        pb_u = mt_double(pb_w1, pb_w2);
+    };
+
+    bool drew = false;
+    int64_t k = 0;
+    while (k < nsteps && done == 0) {
+        if (w == 0) {
+            const int avail = npend - pk;
+            bool re = false;
+            if (avail < K && idx + 64 <= MT_N) {
+                // carry the unconsumed proposals to lanes 0.. and append whole
+                // windows while no twist can fall under a carried proposal
+                const int src = (lane + pk < 64) ? lane + pk : 63;
+                pb_i = __shfl(pb_i, src, 64);
+                pb_end = __shfl(pb_end, src, 64);
+                pb_w1 = (uint32_t)__shfl((int)pb_w1, src, 64);
+                pb_w2 = (uint32_t)__shfl((int)pb_w2, src, 64);
+                npend = avail;
+                pk = 0;
+                while (npend < K && npend <= 64 - 22 && idx + 64 <= MT_N) {
+                    const int before = npend;
+                    parse(true);
+                    if (npend == before) break;
+                }
+                if (npend == 0) parse(false);
+                re = true;
+            } else if (avail == 0) {
+                npend = 0;
+                pk = 0;
+                parse(false);
+                re = true;
+            }
+            if (re) {
+                pb_u = mt_double(pb_w1, pb_w2);
+                q_i[lane] = pb_i;
+                q_u[lane] = pb_u;
+            }
+            if (lane == 0) {
+                ctl[0] = npend;
+                ctl[1] = pk;
+            }
+        }
+        __syncthreads();                                   // the round's proposals are published
+        drew = true;
+        const int npd = __builtin_amdgcn_readfirstlane(ctl[0]);
+        const int pks = __builtin_amdgcn_readfirstlane(ctl[1]);
+        int nq = npd - pks;
+        if (nq > K) nq = K;
+        if ((int64_t)nq > nsteps - k) nq = (int)(nsteps - k);
+        const bool act = qi < nq;
+        const int iv = q_i[pks + (act ? qi : 0)];
+        const double u = q_u[pks + (act ? qi : 0)];
+        if (act && gl == 0) atomicOr(&tag[iv], 1u << qi);
+        __syncthreads();                                   // every proposal's tag
+        const uint32_t old_i = bit_of(0, iv);
+        // level 1: i and its neighbours, level 0 with i flipped
+        int ri[D];
+        nbrs(iv, ri);
+        int cand = iv;
+#pragma unroll
+        for (int q = 0; q < D; ++q)
+            if (gl == q + 1) cand = ri[q];
+        bool dup = gl > 0 && cand == iv;
+#pragma unroll
+        for (int q = 0; q < D; ++q)
+            if (q + 1 < gl) dup |= ri[q] == cand;
+        int nv[D];
+        nbrs(cand, nv);
+        const bool live = act && gl <= D && !dup;
+        int ones = 0;
+        uint32_t tg = tag[cand];
+#pragma unroll
+        for (int e = 0; e < D; ++e) {
+            ones += (int)(bit_of(0, nv[e]) ^ (nv[e] == iv));
+            tg |= tag[nv[e]];
+        }
+        const uint32_t own = bit_of(0, cand) ^ (cand == iv);
+        const uint32_t nb = maj(ones, own);
+        const uint32_t cur = bit_of(1, cand);
+        const bool chg = live && nb != cur;
+        const uint32_t cf = live ? (tg & ((1u << qi) - 1u)) : 0u;  // earlier proposals whose i this lane read
+        // per group: sum(s_end) change and conflicts
+        const u64 up = __ballot(chg && cur == 0u), dn = __ballot(chg && cur != 0u);
+        const u64 gm = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << (gq * G);
+        const int64_t ds = 2 * ((int64_t)__popcll(up & gm) - (int64_t)__popcll(dn & gm));
+        uint32_t cfg = cf;                                 // OR over the group's lanes
+#pragma unroll
+        for (int o = 1; o < G; o <<= 1) cfg |= (uint32_t)__shfl_xor((int)cfg, o, G);
+        // schedule of step k + qi (code/SA_RRG.py:80-81): qi multiplications until
+        // both reach their caps (~1.2e4 steps into a run), then constant
+        double ag = a, bg = b;
+        if (!(ag >= a_cap && bg >= b_cap)) {
+            for (int q = 0; q < qi; ++q) {
+                if (ag < a_cap) ag = par_a * ag;
+                if (bg < b_cap) bg = par_b * bg;
+            }
+        }
+        const double an = (ag < a_cap) ? par_a * ag : ag;
+        const double bn = (bg < b_cap) ? par_b * bg : bg;
+        const double si = old_i ? 1.0 : -1.0;
+        const double t1 = (-2.0 * ag) * si;
+        const double t2 = bg * (double)(-ds);
+        const double num = t1 + t2;
+        const float xf = (float)(-num * inv_n);
+        const float ef = __expf(xf);
+        const float mg = ef * (1e-6f * (1.0f + fabsf(xf))) + 1e-37f;
+        bool acc, tie = false;
+        double dE = 0.0;
+        if (fabs(u - (double)ef) > (double)mg) {
+            acc = u < (double)ef;
+            if (TRACE && st.tr_dE) dE = num / (double)n;
+        } else {
+            dE = num / (double)n;
+            const double e = exp(-dE);
+            const double prob = (e < 1.0) ? e : 1.0;
+            acc = u < prob;
+            tie = e < 1.0 && fabs(u - e) <= 4.0 * (nextafter(e, 2.0) - e);
+        }
+        if (gl == 0) {
+            // proposal qi: the earlier proposals it read (bits < qi), accept and tie
+            // flags, sum(s_end) change, the schedule after its step, delta_H
+            res[qi] = cfg;
+            res[32 + qi] = (acc ? 1u : 0u) | (tie ? 2u : 0u);
+            res_a[qi] = an;
+            res_b[qi] = bn;
+            res_e[qi] = (double)ds;
+            if (TRACE) res_e[32 + qi] = dE;
+        }
+        __syncthreads();                                   // every proposal's result
+        // ---- resolve (every wave alike, lane-parallel over the K proposals): lane q
+        // holds proposal q
+        const bool lq = lane < nq;
+        const uint32_t cfq = lq ? res[lane] : 0u;
+        const uint32_t fl = lq ? res[32 + lane] : 0u;
+        const bool accq = fl & 1u;
+        const u64 accm = __ballot(accq);
+        const u64 clm = __ballot(lq && (cfq & (uint32_t)accm) != 0u);   // read an accepted earlier one's i
+        int qstop = nq;
+        if (clm) {
+            const int qc = __ffsll((unsigned long long)clm) - 1;
+            if (qc < qstop) qstop = qc;
+        }
+        // sum(s_end) after each proposal (prefix over the accepted ones), and stops
+        int64_t pre = (lq && accq) ? (int64_t)res_e[lane] : 0;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int64_t v = __shfl_up(pre, o, 64);
+            if (lane >= o) pre += v;
+        }
+        const int64_t sum_after = sum_end + pre;
+        const int dn_q = (t + lane + 1 > t_cap) ? 2 : ((sum_after == n) ? 1 : 0);
+        const u64 stm = __ballot(lane < qstop && dn_q != 0);
+        int taken = qstop;
+        if (stm) {
+            const int qs = __ffsll((unsigned long long)stm) - 1;
+            if (qs + 1 < taken) taken = qs + 1;
+        }
+        const u64 tk = (taken >= 64) ? ~0ull : ((1ull << taken) - 1ull);
+        ties += __popcll(__ballot((fl & 2u) != 0u) & tk);
+        if (TRACE && w == 0 && lane < taken) {
+            const int64_t kk = k + lane;
+            if (st.tr_i) st.tr_i[kk * R + r] = q_i[pks + lane];
+            if (st.tr_acc) st.tr_acc[kk * R + r] = accq ? 1 : 0;
+            if (st.tr_sum) st.tr_sum[kk * R + r] = sum_after;
+            if (st.tr_dE) st.tr_dE[kk * R + r] = res_e[32 + lane];
+        }
+        {
+            const int src = taken - 1;
+            sum_end = __shfl(sum_after, src, 64);
+            done = __shfl(dn_q, src, 64);
+        }
+        t += taken;
+        a = res_a[taken - 1];
+        b = res_b[taken - 1];
+        // ---- the taken accepted proposals: level 1 on their C_1, level 0 at i;
+        // every proposal clears its tag
+        const bool mine = qi < taken && ((accm >> qi) & 1ull);
+        if (mine) {
+            if (chg) {
+                const uint32_t bt = 1u << (cand & 31);
+                if (cur) atomicAnd(&lev[nw + (cand >> 5)], ~bt);
+                else atomicOr(&lev[nw + (cand >> 5)], bt);
+            }
+            if (gl == 0) atomicXor(&lev[iv >> 5], 1u << (iv & 31));
+        }
+        if (act && gl == 0) tag[iv] = 0u;
+        k += taken;
+        pk += taken;
+    }
+    if (w == 0 && drew) idx = __builtin_amdgcn_readlane(pb_end, pk - 1);
+    if (TRACE && tid == 0) {
+        for (; k < nsteps; ++k) {
+            if (st.tr_i) st.tr_i[k * R + r] = -1;
+            if (st.tr_acc) st.tr_acc[k * R + r] = -1;
+            if (st.tr_sum) st.tr_sum[k * R + r] = sum_end;
+            if (st.tr_dE) st.tr_dE[k * R + r] = 0.0;
+        }
+    }
+    __syncthreads();
+    {
+        const int64_t col = r >> 6;
+        for (int64_t v = tid; v < n; v += NT) {
+            if (((lev[v >> 5] ^ lev0s[v >> 5]) >> (v & 31)) & 1u)
+                atomicXor((unsigned long long*)&s[v * W + col], 1ull << (r & 63));
+        }
+        for (int q = tid; q < MT_N; q += NT) st.mt[r * MT_N + q] = mt[q];
+    }
+    if (tid == 0) {
+        st.mt_idx[r] = idx;
+        st.a[r] = a;
+        st.b[r] = b;
+        st.t[r] = t;
+        st.sum_end[r] = sum_end;
+        st.done[r] = done;
+        if (st.tr_tie) st.tr_tie[r] += ties;
+    }
+}
+
 }  // namespace salds
 }  // namespace mjx
 
@@ -2282,7 +2684,12 @@ extern "C" int64_t mjx_sa_lds_plan(int64_t n, int d, int p, int c, uint32_t flag
     salds::GeoW gw;
     salds::Geo g2;
     const int nwv = (split == 4) ? 4 : 8;
-    if (!(flags & (MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE | MJX_SA_LDS_PAIR)) && small_d && T == 1) {
+    salds::GeoW1 gw1;
+    if (!(flags & (MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE | MJX_SA_LDS_PAIR | MJX_SA_LDS_WAVE)) && small_d && T == 1 &&
+        salds::geometry_wg1(n, d, 32, &gw1)) {
+        th = 256;                                   // k_sa_lds_wg1: 4 waves x 8 proposals
+        bytes = gw1.bytes;
+    } else if (!(flags & (MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE | MJX_SA_LDS_PAIR)) && small_d && T == 1) {
         // k_sa_lds_multi: the one-plane geometry
     } else if (!(flags & (MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE | MJX_SA_LDS_WAVE)) && small_d && T >= 2 && T <= 4 &&
                salds::geometry_wg(n, d, T, nwv, &gw)) {
@@ -2320,6 +2727,20 @@ extern "C" int mjx_sa_lds_steps(const int32_t* adj, int64_t n, int d, int p, int
         MJX_LAUNCH_CHECK("k_sa_lds");
         return MJX_OK;
     };
+    salds::GeoW1 gw1;
+    if (!(st.opt_flags & (MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE | MJX_SA_LDS_PAIR | MJX_SA_LDS_WAVE)) &&
+        (d == 3 || d == 4) && T == 1 && salds::geometry_wg1(n, d, 32, &gw1)) {
+        const bool trw = st.tr_i || st.tr_acc || st.tr_sum || st.tr_dE;
+        auto gow1 = [&](auto kern) -> int {
+            MJX_HIP(set_max_lds(kern, gw1.bytes), "sa_lds lds");
+            kern<<<(unsigned)R, 256, (size_t)gw1.bytes, hs>>>(adj, n, R, W, (u64*)s, st, nsteps, par_a, par_b, a_cap,
+                                                              b_cap, t_cap, gw1);
+            MJX_LAUNCH_CHECK("k_sa_lds_wg1");
+            return MJX_OK;
+        };
+        if (d == 3) return trw ? gow1(salds::k_sa_lds_wg1<3, 4, 8, true>) : gow1(salds::k_sa_lds_wg1<3, 4, 8, false>);
+        return trw ? gow1(salds::k_sa_lds_wg1<4, 4, 8, true>) : gow1(salds::k_sa_lds_wg1<4, 4, 8, false>);
+    }
     if (!(st.opt_flags & (MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE | MJX_SA_LDS_PAIR)) && (d == 3 || d == 4) && T == 1) {
         const bool trm = st.tr_i || st.tr_acc || st.tr_sum || st.tr_dE;
         auto gom = [&](auto kern) -> int {
@@ -2339,8 +2760,7 @@ extern "C" int mjx_sa_lds_steps(const int32_t* adj, int64_t n, int d, int p, int
         T <= 4 && salds::geometry_wg(n, d, T, nwv, &gw)) {
         const bool trw = st.tr_i || st.tr_acc || st.tr_sum || st.tr_dE;
         auto gow = [&](auto kern) -> int {
-            MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, gw.bytes),
-                    "sa_lds lds");
+            MJX_HIP(set_max_lds(kern, gw.bytes), "sa_lds lds");
             kern<<<(unsigned)R, 64 * nwv, (size_t)gw.bytes, hs>>>(adj, n, R, W, (u64*)s, st, nsteps, par_a, par_b,
                                                                  a_cap, b_cap, t_cap, gw);
             MJX_LAUNCH_CHECK("k_sa_lds_wg");

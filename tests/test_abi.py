@@ -124,8 +124,8 @@ def test_sa_lds_plan_names_the_kernel_that_runs(mjx_mod):
     """mjx_sa_lds_plan reports the LDS bytes and workgroup size of the kernel
     mjx_sa_lds_steps selects (the auto layout sized occupancy
     with the one-plane bytes): the whole-CU kernel at p+c-1 >= 2 (8 or 4
-    waves), the paired one-wave kernel with lds_wave, the eight-proposal one at
-    p+c-1 = 1."""
+    waves), the paired one-wave kernel with lds_wave; at p+c-1 = 1 the
+    whole-CU 32-proposal kernel, or the one-wave eight-proposal one."""
     import ctypes
     lib = mjx_mod.load_library()
     L = mjx_mod._lib
@@ -138,6 +138,8 @@ def test_sa_lds_plan_names_the_kernel_that_runs(mjx_mod):
     pair = lib.mjx_sa_lds_plan(10_000, 4, 3, 1, L.MJX_SA_LDS_WAVE, 0, ctypes.byref(th))
     assert th.value == 64 and one < pair
     assert lib.mjx_sa_lds_plan(10_000, 4, 3, 1, L.MJX_SA_LDS_SINGLE, 0, ctypes.byref(th)) == one and th.value == 64
-    assert lib.mjx_sa_lds_plan(10_000, 4, 1, 1, 0, 0, ctypes.byref(th)) == lib.mjx_sa_lds_bytes(10_000, 4, 1, 1)
-    assert th.value == 64
+    wg1 = lib.mjx_sa_lds_plan(10_000, 4, 1, 1, 0, 0, ctypes.byref(th))          # 4 waves x 8 proposals
+    assert th.value == 256 and lib.mjx_sa_lds_bytes(10_000, 4, 1, 1) < wg1 <= 160 * 1024
+    assert lib.mjx_sa_lds_plan(10_000, 4, 1, 1, L.MJX_SA_LDS_WAVE, 0, ctypes.byref(th)) == \
+        lib.mjx_sa_lds_bytes(10_000, 4, 1, 1) and th.value == 64                    # one wave x 8 proposals
     assert lib.mjx_sa_lds_plan(100_000, 4, 3, 1, 0, 0, ctypes.byref(th)) == -1

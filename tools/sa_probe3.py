@@ -24,6 +24,7 @@ VARIANTS = {
     # name: (layout, kernel options)
     "lds": ("lds", None),                                   # the default LDS kernel for (p, c)
     "lds-wg4": ("lds", {"split": 4}),                       # whole CU, 4 waves (p+c-1 >= 2)
+    "lds-wave": ("lds", {"lds_wave": True}),                # one wave: 8 proposals (T = 1) / 2 (T >= 2) per step
     "lds-pair": ("lds", {"lds_wave": True, "lds_pair": True}),   # one wave, two proposals per step
     "lds-single": ("lds", {"lds_single": True}),            # one wave, one proposal per step
     "cone": ("cone", None),
