@@ -22,12 +22,17 @@ for s in $STEPS; do
         ${PYTEST_ARGS:-} > $OUT/pytest_gpu.log 2>&1
       stop_if_fatal $? tests ;;
     py)
-      # one probe script: PY="tools/sa_probe3.py --no-cone" PY_LOG=name
-      timeout -k 10 ${PY_TIMEOUT:-300} python -u $PY > $OUT/${PY_LOG:-py}.log 2>&1
-      stop_if_fatal $? "py $PY" ;;
-    py2)
-      timeout -k 10 ${PY2_TIMEOUT:-300} python -u $PY2 > $OUT/${PY2_LOG:-py2}.log 2>&1
-      stop_if_fatal $? "py2 $PY2" ;;
+      # probe scripts, ";;"-separated: PY="tools/sa_probe3.py --no-cone ;; tools/hpr_q_time.py"
+      # (logs py_1.log, py_2.log, ...; PY_LOG=name for a single one)
+      k=0
+      IFS=$'\n'; for cmd in $(echo "$PY" | sed 's/ *;; */\n/g'); do
+        unset IFS
+        k=$((k+1))
+        log=${PY_LOG:-py_$k}
+        timeout -k 10 ${PY_TIMEOUT:-300} python -u $cmd > $OUT/$log.log 2>&1
+        stop_if_fatal $? "py $cmd"
+      done
+      unset IFS ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
       stop_if_fatal $? smoke ;;
