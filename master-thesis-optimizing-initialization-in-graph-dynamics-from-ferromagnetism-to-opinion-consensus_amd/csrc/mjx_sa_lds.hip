@@ -1880,21 +1880,38 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
                 ok = y <= rng;
             }
             const u64 okm = __ballot(ok);
+            // proposal starts by a scalar walk over the ballot (each: the first
+            // acceptable word at or after the previous end, then rand()'s two
+            // words); the start lanes push their lane ids to their target lanes,
+            // which pull i, w1, w2 (lane-parallel: no readlane per proposal)
+            u64 stm = 0;
             int pos = 0, got = 0;
-            while (pos < 64 && npend < 64) {
+            while (pos < 64 && npend + got < 63) {
                 const u64 m = okm >> pos;
                 if (!m) break;
                 const int f = pos + __ffsll((unsigned long long)m) - 1;
                 if (f + 2 >= lim) break;
-                const int iv = __builtin_amdgcn_readlane((int)y, f);
-                const uint32_t w1 = (uint32_t)__builtin_amdgcn_readlane((int)tw, f + 1);
-                const uint32_t w2 = (uint32_t)__builtin_amdgcn_readlane((int)tw, f + 2);
-                if (lane == npend) { pb_i = iv; pb_w1 = w1; pb_w2 = w2; pb_end = idx + f + 3; }
-                ++npend;
+                stm |= 1ull << f;
                 ++got;
                 pos = f + 3;
             }
-            if (got > 0) { idx += pos; break; }
+            if (got > 0) {
+                const bool isst = (stm >> lane) & 1ull;
+                const int tgt = isst ? npend + __popcll(stm & ((1ull << lane) - 1ull)) : 63;
+                const int src = __builtin_amdgcn_ds_permute(tgt * 4, lane) & 63;
+                const int yi = __builtin_amdgcn_ds_bpermute(src * 4, (int)y);
+                const int x1 = __builtin_amdgcn_ds_bpermute((src + 1) * 4, (int)tw);
+                const int x2 = __builtin_amdgcn_ds_bpermute((src + 2) * 4, (int)tw);
+                if (lane >= npend && lane < npend + got) {
+                    pb_i = yi;
+                    pb_w1 = (uint32_t)x1;
+                    pb_w2 = (uint32_t)x2;
+                    pb_end = idx + src + 3;
+                }
+                npend += got;
+                idx += pos;
+                break;
+            }
             if (one) break;
             if (!okm) { idx += lim; continue; }
             const int f = __ffsll((unsigned long long)okm) - 1;
@@ -1923,6 +1940,9 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
     bool lc_fast[T + 1];
     bool drew = false;
     int64_t k = 0;
+#ifdef MJX_SA_PROF
+    unsigned long long _acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, _t0 = __builtin_amdgcn_s_memtime();
+#endif
     while (k < nsteps && done == 0) {
         if (w == 0) {
             const int avail = npend - pk;
@@ -1956,6 +1976,7 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
             }
         }
         __syncthreads();                                   // the round's proposals are published
+        LDS_STAMP(0);
         drew = true;
         const int npd = __builtin_amdgcn_readfirstlane(ctl[0]);
         const int pks = __builtin_amdgcn_readfirstlane(ctl[1]);
@@ -2012,6 +2033,7 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
             lc_n[1] = __popcll(m);
             last = lc_n[1] ? 1 : 0;
         }
+        LDS_STAMP(1);
         int64_t ds = 0;
 #pragma unroll
         for (int l = 2; l <= T; ++l) {
@@ -2019,7 +2041,10 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
             lc_fast[l] = true;
             lc_n[l] = 0;
             __syncthreads();                               // every proposal's marks of C_{l-1}
-            if (last != l - 1) continue;                   // (wave-uniform)
+            if (last != l - 1) {                           // (wave-uniform)
+                LDS_STAMP(l < 4 ? l : 3);
+                continue;
+            }
             const int np = lc_n[l - 1];
             int nc = 0;
             if (np <= MAXM && lc_fast[l - 1]) {
@@ -2111,14 +2136,17 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
             }
             lc_n[l] = nc;
             if (nc > 0) last = l;
+            LDS_STAMP(l < 4 ? l : 3);
         }
         if (last != T) ds = 0;
         // ---- delta_H and the Metropolis test of this wave's proposal, step k + w
         // (code/SA_RRG.py:37,74-76); the schedule after w steps (:80-81)
         double ah = a, bh = b;
-        for (int q = 0; q < w; ++q) {
-            if (ah < a_cap) ah = par_a * ah;
-            if (bh < b_cap) bh = par_b * bh;
+        if (!(ah >= a_cap && bh >= b_cap)) {                         // both capped after ~1.2e4 steps
+            for (int q = 0; q < w; ++q) {
+                if (ah < a_cap) ah = par_a * ah;
+                if (bh < b_cap) bh = par_b * bh;
+            }
         }
         const double anx = (ah < a_cap) ? par_a * ah : ah;          // the schedule after this step
         const double bnx = (bh < b_cap) ? par_b * bh : bh;
@@ -2152,41 +2180,55 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
             res_a[w] = anx;
             res_b[w] = bnx;
         }
+        LDS_STAMP(4);
         __syncthreads();                                   // every proposal's result
+        LDS_STAMP(5);
         // ---- resolve in proposal order (every wave alike): the taken proposals are
         // the prefix before the first that read an accepted earlier one's change, or
         // up to a stop
-        uint32_t accm = 0;
-        int taken = 0;
-        bool stop = false;
+        // lane-parallel over the NW proposals: lane q holds proposal q's result
+        const bool lq = lane < nq;
+        const uint32_t pq = lq ? res[lane & 7] : 0u;
+        const bool aq = (pq >> 8) & 1u;
+        const uint32_t accm = (uint32_t)__ballot(lq && aq);
+        const u64 clm = __ballot(lq && (pq & accm & 0xffu) != 0u);     // read a taken... accepted earlier one
+        int qstop = nq;
+        if (clm) {
+            const int qc = __ffsll((unsigned long long)clm) - 1;
+            if (qc < qstop) qstop = qc;
+        }
+        // sum(s_end) after each proposal: prefix over the accepted ones (8 lanes)
+        int pre = (lq && aq) ? (int)(int16_t)(pq >> 16) : 0;
 #pragma unroll
-        for (int q = 0; q < NW; ++q) {
-            if (q < nq && !stop) {
-                const uint32_t pq = res[q];
-                if (pq & accm & 0xffu) {
-                    stop = true;
-                } else {
-                    const bool aq = (pq >> 8) & 1u;
-                    if (aq) {
-                        sum_end += (int64_t)(int16_t)(pq >> 16);
-                        accm |= 1u << q;
-                    }
-                    ties += (int)((pq >> 9) & 1u);
-                    t += 1;                                             // (code/SA_RRG.py:77,82)
-                    ++taken;
-                    if (TRACE && w == q && lane == 0) {
-                        if (st.tr_i) st.tr_i[(k + q) * R + r] = iv;
-                        if (st.tr_acc) st.tr_acc[(k + q) * R + r] = aq ? 1 : 0;
-                        if (st.tr_sum) st.tr_sum[(k + q) * R + r] = sum_end;
-                        if (st.tr_dE) st.tr_dE[(k + q) * R + r] = dE;
-                    }
-                    if (t > t_cap) { done = 2; stop = true; }               // (:84)
-                    else if (sum_end == n) { done = 1; stop = true; }       // m(s_endstate(s)) == 1
-                }
+        for (int o = 1; o < 8; o <<= 1) {
+            const int v = __shfl_up(pre, o, 8);
+            if ((lane & 7) >= o) pre += v;
+        }
+        const int64_t sum_after = sum_end + (int64_t)pre;
+        const int dnq = (t + lane + 1 > t_cap) ? 2 : ((sum_after == n) ? 1 : 0);
+        const u64 stq = __ballot(lane < qstop && dnq != 0);            // (code/SA_RRG.py:84), m == 1
+        int taken = qstop;
+        if (stq) {
+            const int qs = __ffsll((unsigned long long)stq) - 1;
+            if (qs + 1 < taken) taken = qs + 1;
+        }
+        ties += __popcll(__ballot(lane < taken && ((pq >> 9) & 1u)));
+        if constexpr (TRACE) {
+            const int64_t my_sum = __shfl(sum_after, w, 64);        // sum(s_end) after this wave's step
+            if (w < taken && lane == 0) {
+                const int64_t kk = k + w;
+                if (st.tr_i) st.tr_i[kk * R + r] = iv;
+                if (st.tr_acc) st.tr_acc[kk * R + r] = ((accm >> w) & 1u) ? 1 : 0;
+                if (st.tr_sum) st.tr_sum[kk * R + r] = my_sum;
+                if (st.tr_dE) st.tr_dE[kk * R + r] = dE;
             }
         }
-        a = res_a[taken - 1];                                       // (:80-81) after the taken steps
-        b = res_b[taken - 1];
+        const double ra = res_a[lane & 7], rb = res_b[lane & 7];
+        sum_end = __shfl(sum_after, taken - 1, 64);
+        done = __shfl(dnq, taken - 1, 64);
+        t += taken;                                                 // (code/SA_RRG.py:77,82)
+        a = __shfl(ra, taken - 1, 64);                              // (:80-81) after the taken steps
+        b = __shfl(rb, taken - 1, 64);
         // ---- the taken accepted proposals' changes; every proposal clears its marks
         const bool mine = w < taken && ((accm >> w) & 1u);
         if (mine && lane == 0) atomicXor(&lev[iv >> 5], 1u << (iv & 31));
@@ -2215,7 +2257,15 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
         }
         k += taken;
         pk += taken;
+        LDS_STAMP(6);
+#ifdef MJX_SA_PROF
+        _acc[7] += 1;                                      // rounds (every wave counts)
+#endif
     }
+#ifdef MJX_SA_PROF
+    if (lane == 0)
+        for (int q = 0; q < 8; ++q) atomicAdd(&mjx_sa_lds_prof[q], _acc[q]);
+#endif
     if (w == 0 && drew) idx = __builtin_amdgcn_readlane(pb_end, pk - 1);
     if (TRACE && tid == 0) {
         for (; k < nsteps; ++k) {
@@ -2398,21 +2448,38 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg1(const int32_t* __restric
                 ok = y <= rng;
             }
             const u64 okm = __ballot(ok);
+            // proposal starts by a scalar walk over the ballot (each: the first
+            // acceptable word at or after the previous end, then rand()'s two
+            // words); the start lanes push their lane ids to their target lanes,
+            // which pull i, w1, w2 (lane-parallel: no readlane per proposal)
+            u64 stm = 0;
             int pos = 0, got = 0;
-            while (pos < 64 && npend < 64) {
+            while (pos < 64 && npend + got < 63) {
                 const u64 m = okm >> pos;
                 if (!m) break;
                 const int f = pos + __ffsll((unsigned long long)m) - 1;
                 if (f + 2 >= lim) break;
-                const int iv = __builtin_amdgcn_readlane((int)y, f);
-                const uint32_t w1 = (uint32_t)__builtin_amdgcn_readlane((int)tw, f + 1);
-                const uint32_t w2 = (uint32_t)__builtin_amdgcn_readlane((int)tw, f + 2);
-                if (lane == npend) { pb_i = iv; pb_w1 = w1; pb_w2 = w2; pb_end = idx + f + 3; }
-                ++npend;
+                stm |= 1ull << f;
                 ++got;
                 pos = f + 3;
             }
-            if (got > 0) { idx += pos; break; }
+            if (got > 0) {
+                const bool isst = (stm >> lane) & 1ull;
+                const int tgt = isst ? npend + __popcll(stm & ((1ull << lane) - 1ull)) : 63;
+                const int src = __builtin_amdgcn_ds_permute(tgt * 4, lane) & 63;
+                const int yi = __builtin_amdgcn_ds_bpermute(src * 4, (int)y);
+                const int x1 = __builtin_amdgcn_ds_bpermute((src + 1) * 4, (int)tw);
+                const int x2 = __builtin_amdgcn_ds_bpermute((src + 2) * 4, (int)tw);
+                if (lane >= npend && lane < npend + got) {
+                    pb_i = yi;
+                    pb_w1 = (uint32_t)x1;
+                    pb_w2 = (uint32_t)x2;
+                    pb_end = idx + src + 3;
+                }
+                npend += got;
+                idx += pos;
+                break;
+            }
             if (one) break;
             if (!okm) { idx += lim; continue; }
             const int f = __ffsll((unsigned long long)okm) - 1;

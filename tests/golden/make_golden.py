@@ -332,10 +332,16 @@ def gen_hpr_full():
     for (n, d, p, c, TT, gseed, tseed) in ((40, 4, 1, 1, 300, 31, 7), (30, 3, 2, 1, 300, 32, 8),
                                            (40, 4, 2, 2, 300, 33, 9), (40, 3, 3, 1, 300, 34, 10),
                                            (60, 4, 3, 1, 300, 35, 11)):
+        key = f"n{n}_d{d}_p{p}c{c}"
+        only = os.environ.get("HPR_FULL_ONLY")
+        if only and key not in only.split(","):
+            continue
         tmp = tempfile.mktemp(suffix=".npz")
         s = src
-        for old, new in (("n=10000", f"n={n}"), ("d=4", f"d={d}"), ("p=1", f"p={p}"), ("c=1", f"c={c}"),
-                         ("TT=10000", f"TT={TT}"),
+        # whole-line anchors: "p=1 c=1" also occurs in a comment above the
+        # parameter block (code/HPR_pytorch_RRG.py:65, 224-237)
+        for old, new in (("\nn=10000\n", f"\nn={n}\n"), ("\nd=4\n", f"\nd={d}\n"), ("\np=1\n", f"\np={p}\n"),
+                         ("\nc=1\n", f"\nc={c}\n"), ("\nTT=10000", f"\nTT={TT}"),
                          ("device = torch.device('cuda' if torch.cuda.is_available() else 'cpu')",
                           "device = torch.device('cpu')"),
                          (".to(device='cuda')", ".to(device=device)"),
@@ -347,7 +353,6 @@ def gen_hpr_full():
         t0 = time.time()
         exec(compile(s, HPR_PATH, "exec"), g)
         z = np.load(tmp)
-        key = f"n{n}_d{d}_p{p}c{c}"
         for k in z.files:
             if k != "time":
                 out[f"{key}_{k}"] = z[k]
@@ -358,7 +363,11 @@ def gen_hpr_full():
         out[f"{key}_params"] = np.array([n, d, p, c, TT, tseed])
         os.unlink(tmp)
         print("hpr full script", key, "steps", z["num_steps"], "m", z["mag_reached"], f"({time.time() - t0:.1f}s)")
-    np.savez_compressed(os.path.join(OUT, "hpr_fullscript.npz"), **out)
+    path = os.path.join(OUT, "hpr_fullscript.npz")
+    if os.environ.get("HPR_FULL_ONLY") and os.path.exists(path):
+        with np.load(path) as old:                  # keep the other cases
+            out = {**{k: old[k] for k in old.files}, **out}
+    np.savez_compressed(path, **out)
 
 
 # ---------------------------------------------------------------------------

@@ -90,6 +90,15 @@ def main():
         sa.steps(args.sa_steps)
         torch.cuda.synchronize()
         del sa
+        # the LDS-resident whole-CU kernels at SA_RRG.py's shapes (d=4, n=1e4, 64
+        # replicas on their own graphs): p=c=1 (configs[0], k_sa_lds_wg1) and the
+        # script's p=3, c=1 (k_sa_lds_wg), and the one-wave pair kernel beside them
+        gl = [mjx.random_regular_graph(4, 10_000, seed=7000 + k) for k in range(64)]
+        for (p_, c_, kern) in ((1, 1, None), (3, 1, None), (3, 1, {"lds_wave": True})):
+            sa = mjx.SAReplicas(gl, p_, c_, np.arange(64), layout="lds", kernel=kern)
+            sa.steps(20 * args.sa_steps)
+            torch.cuda.synchronize()
+            del sa
         print("pmc_run sa done", flush=True)
     if not args.no_er:
         # configs[3]: ER mean degree 5, N=1e7, 4096 replicas: the degree-class
