@@ -331,7 +331,7 @@ def gen_hpr_full():
     # p+c = 4 cases: the decay-split fp32 loop state (hpr_run's fp32 default) applies there
     for (n, d, p, c, TT, gseed, tseed) in ((40, 4, 1, 1, 300, 31, 7), (30, 3, 2, 1, 300, 32, 8),
                                            (40, 4, 2, 2, 300, 33, 9), (40, 3, 3, 1, 300, 34, 10),
-                                           (60, 4, 3, 1, 300, 35, 11)):
+                                           (60, 4, 3, 1, 120, 35, 11)):
         key = f"n{n}_d{d}_p{p}c{c}"
         only = os.environ.get("HPR_FULL_ONLY")
         if only and key not in only.split(","):
