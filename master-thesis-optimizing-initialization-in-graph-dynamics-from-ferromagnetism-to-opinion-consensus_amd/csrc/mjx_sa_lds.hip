@@ -2035,16 +2035,26 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
         }
         LDS_STAMP(1);
         int64_t ds = 0;
+        // the nodes this wave read at each level l >= 2 (a candidate and its
+        // neighbours per lane): checked against the earlier proposals' marks of
+        // level l-1 once every wave is through its levels (no barrier per level)
+        int rd_c[T + 1], rd_n[T + 1][D];
+        bool rd_on[T + 1];
+        bool rd_all = false;                               // a list level: conflicts with every earlier one
 #pragma unroll
         for (int l = 2; l <= T; ++l) {
             lc_in[l] = false;
             lc_fast[l] = true;
             lc_n[l] = 0;
-            __syncthreads();                               // every proposal's marks of C_{l-1}
+            rd_on[l] = false;
+            rd_c[l] = 0;
+#pragma unroll
+            for (int e = 0; e < D; ++e) rd_n[l][e] = 0;
             if (last != l - 1) {                           // (wave-uniform)
                 LDS_STAMP(l < 4 ? l : 3);
                 continue;
             }
+            wave_sync();                                   // this wave's marks of C_{l-1}
             const int np = lc_n[l - 1];
             int nc = 0;
             if (np <= MAXM && lc_fast[l - 1]) {
@@ -2070,11 +2080,14 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
                 int nv2[D];
                 nbrs(c2, nv2);
                 int ones = 0;
-                uint32_t cfm = 0;
+                uint32_t cfm = 0;                          // (the other waves' marks may still be coming)
 #pragma unroll
                 for (int e = 0; e < D; ++e) ones += (int)look(l - 1, nv2[e], cfm);
                 const uint32_t own = look(l - 1, c2, cfm);
-                if (act2) cf |= cfm;
+                rd_on[l] = act2;
+                rd_c[l] = c2;
+#pragma unroll
+                for (int e = 0; e < D; ++e) rd_n[l][e] = nv2[e];
                 const uint32_t nb = maj(ones, own);
                 const uint32_t cur = bit_of(l, c2);
                 const bool chg = act2 && nb != cur;
@@ -2099,7 +2112,10 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
                 lc_in[l] = add;
                 if (l == T) ds = 2 * ((int64_t)__popcll(__ballot(add && cur == 0u)) - (int64_t)__popcll(__ballot(add && cur != 0u)));
             } else {
-                // this wave's LDS-list path (its lists hold every level; deduped here)
+                // this wave's LDS-list path (its lists hold every level; deduped here);
+                // its reads are not kept: the proposal stands only as the round's first
+                // taken one or after rejected ones (conflict with every earlier one)
+                rd_all = true;
                 const uint32_t* prev = lst + (l - 1) * lc;
                 uint32_t* curl = lst + l * lc;
                 const int m = np * DP1;
@@ -2120,7 +2136,6 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
 #pragma unroll
                         for (int e = 0; e < D; ++e) ones += (int)look(l - 1, nv2[e], cfm);
                         const uint32_t own = look(l - 1, cd, cfm);
-                        cf |= cfm;
                         const uint32_t nb = maj(ones, own);
                         const uint32_t mb = obit << (8 * (cd & 3));
                         cur = bit_of(l, cd);
@@ -2171,6 +2186,19 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
             acc = u < prob;
             tie = e < 1.0 && fabs(u - e) <= 4.0 * (nextafter(e, 2.0) - e);
         }
+        LDS_STAMP(4);
+        __syncthreads();                                   // every proposal's marks of every level
+        // what this proposal read at level l-1 that an earlier one changed
+#pragma unroll
+        for (int l = 2; l <= T; ++l) {
+            if (rd_on[l]) {
+                uint32_t mb = mk[(l - 2) * mkl + rd_c[l]];
+#pragma unroll
+                for (int e = 0; e < D; ++e) mb |= mk[(l - 2) * mkl + rd_n[l][e]];
+                cf |= mb & early;
+            }
+        }
+        if (rd_all) cf |= early;
         uint32_t cfw = 0;
 #pragma unroll
         for (int j = 0; j < NW - 1; ++j)
@@ -2180,7 +2208,6 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
             res_a[w] = anx;
             res_b[w] = bnx;
         }
-        LDS_STAMP(4);
         __syncthreads();                                   // every proposal's result
         LDS_STAMP(5);
         // ---- resolve in proposal order (every wave alike): the taken proposals are

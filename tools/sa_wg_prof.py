@@ -14,7 +14,7 @@ import torch  # noqa: E402
 import mjx  # noqa: E402
 
 lib = mjx._lib.load()
-names = ["B0 (wave 0 parses)", "level 1", "level 2", "level 3", "dE+accept+result", "result barrier",
+names = ["B0 (wave 0 parses)", "level 1", "level 2", "level 3", "dE+accept", "barrier+mark check+result+barrier",
          "resolve+apply"]
 n, d, R = 10_000, 4, 64
 graphs = [mjx.random_regular_graph(d, n, seed=7000 + k) for k in range(R)]
