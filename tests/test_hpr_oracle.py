@@ -104,3 +104,47 @@ def test_torch_cpu_restatement_equals_numpy_oracle():
     got = hpr_torch.HPr_dp(torch.from_numpy(z["chi0"]), torch.from_numpy(z["biases0"]), inr, src, n, d, p, c, 1,
                            25 * n, 0.4, rows)
     assert np.max(np.abs(got.numpy() - want)) < 1e-13
+
+
+def test_numpy_oracle_loop_reproduces_reference_whole_script():
+    """The oracle's HPR functions chained as the reference's main loop
+    (code/HPR_pytorch_RRG.py:327-362: torch's CPU stream for chi0, biases0 and
+    the per-iteration rand(n), float64) reproduce the reference's own
+    whole-script runs exactly -- num_steps and conf for every fixture key,
+    including the p+c = 4 runs and the d = 3 runs whose marginals tie exactly
+    (the numpy sums break those ties as torch's do).  Pins the oracle to the
+    reference's end-to-end output, not only to single steps."""
+    import torch
+    from oracle import majority
+    z = load_golden("hpr_fullscript.npz")
+    keys = sorted({k.rsplit("_", 1)[0] for k in z if k.endswith("_params")})
+    assert len(keys) >= 4
+    for key in keys:
+        n, d, p, c, TT, tseed = (int(x) for x in z[f"{key}_params"])
+        nbrs = z[f"{key}_graphs"][0].astype(np.int64)
+        edges = z[f"{key}_edges"]
+        inr, src = hpr.incoming_rows(edges, nbrs)
+        ep = hpr.edges_pos(edges, nbrs)
+        g = torch.Generator().manual_seed(tseed)
+        chi = torch.rand((2 * len(edges), 4 ** (p + c)), dtype=torch.float64, generator=g)
+        chi = (chi / chi.sum(1, keepdim=True)).numpy()
+        b = torch.rand((n, 2), dtype=torch.float64, generator=g)
+        b = (b / b.sum(1, keepdim=True)).numpy()
+        s = 2 * (b[:, 0] > b[:, 1]).astype(np.int32) - 1
+
+        def m_end(x):
+            x = x.astype(np.int64)
+            for _ in range(p + c - 1):
+                x = majority.onestep_majority(nbrs, x)
+            return x.sum() / n
+
+        t, m = 0, m_end(s)
+        while m < 1:                                                  # code/HPR_pytorch_RRG.py:344-356
+            chi = hpr.HPr_dp(chi, b, inr, src, n, d, p, c, 1, 25 * n, 0.4)
+            marg = hpr.marginals_comp(chi, ep, p, c)
+            u = torch.rand(n, dtype=torch.float64, generator=g).numpy()
+            b, s = hpr.new_biases_i(b, 0.3, 0.1, marg, t, u)
+            t += 1
+            m = 2 if t > TT else m_end(s)
+        assert t == z[f"{key}_num_steps"][0], key
+        assert np.array_equal(s, z[f"{key}_conf"][0]), key
