@@ -2332,16 +2332,21 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
 // one LDS atomic before the round's reads, so a lane ORs the tags of the nodes
 // it reads.  The resolution is lane-parallel: proposal q's packed result sits
 // in lane q, one ballot finds the first proposal that read an accepted
-// earlier one's i, a prefix sum the first stop.  Rounds: proposals published
-// (wave 0 parses up to three stream windows), tags set, level 1 evaluated and
-// results written, each behind a workgroup barrier.
+// earlier one's i, a prefix sum the first stop.  Rounds: proposals published,
+// tags set, level 1 evaluated and results written, each behind a workgroup
+// barrier.  A wave of its own (wave NW) parses the numpy stream into a ring of
+// proposals indexed by their absolute number while the others evaluate (32
+// proposals a round: the parse in wave 0 was 60 % of a round); it may run past
+// an MT twist with proposals of the old state unconsumed, keeping that state,
+// so the stream handed back is numpy's at the end of the last proposal taken.
 struct GeoW1 {
     int nw;
     int off_lev;    // 2 * nw level words (levels 0 and 1)
     int off_lev0;
     int off_tag;    // nw * 32 tag words
     int off_mt;
-    int off_q;      // i[64], u[64]
+    int off_mtb;    // the MT state before the parser's latest twist
+    int off_q;      // ring: i[64], u[64], end[64]
     int off_res;    // per proposal: packed word, a, b after its step, dE
     int bytes;
 };
@@ -2354,28 +2359,33 @@ static bool geometry_wg1(int64_t n, int d, int K, GeoW1* g) {
     g->off_lev0 = (int)off;  off += (int64_t)g->nw * 4;
     g->off_tag = (int)off;   off += (int64_t)g->nw * 32 * 4;
     g->off_mt = (int)off;    off += MT_N * 4;
+    g->off_mtb = (int)off;   off += MT_N * 4;
     off = (off + 15) / 16 * 16;
-    g->off_q = (int)off;     off += 64 * 4 + 64 * 8;
+    g->off_q = (int)off;     off += 64 * 4 + 64 * 8 + 64 * 4;
     g->off_res = (int)off;   off += 64 * 4 + 64 * 8 * 3 + 4 * 4;
     g->bytes = (int)off;
     return (size_t)off <= kLdsMax;
 }
 
 template <int D, int NW, int NQ, bool TRACE>
-__global__ void __launch_bounds__(64 * NW) k_sa_lds_wg1(const int32_t* __restrict__ adj, int64_t n, int64_t R,
+__global__ void __launch_bounds__(64 * (NW + 1)) k_sa_lds_wg1(const int32_t* __restrict__ adj, int64_t n, int64_t R,
                                                        int64_t W, u64* __restrict__ s, mjx_sa_state st,
                                                        int64_t nsteps, double par_a, double par_b, double a_cap,
                                                        double b_cap, int64_t t_cap, GeoW1 geo) {
     constexpr int G = 64 / NQ;                     // lanes per proposal
     constexpr int K = NW * NQ;                     // proposals per round
     static_assert(D >= 1 && D <= 4 && G >= D + 1 && K <= 32 && NW >= 2, "whole-CU LDS SA at T = 1");
-    constexpr int NT = 64 * NW;
+    constexpr int NT = 64 * (NW + 1);
+    constexpr int RCAP = 63;                       // ring entries ahead of the consumer (64 slots)
+    constexpr int TARGET = 60;                     // the parser keeps this many proposals ahead
     extern __shared__ __align__(16) unsigned char smem[];
     const int tid = threadIdx.x;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool parser = w == NW;                   // wave NW parses the stream
     const int lane = tid & 63;
+    const u64 ltmask = (1ull << lane) - 1ull;
     const int gq = lane / G, gl = lane % G;
-    const int qi = w * NQ + gq;                    // this lane group's proposal in the round
+    const int qi = parser ? 31 : w * NQ + gq;      // this lane group's proposal in the round
     const int64_t r = blockIdx.x;
     const int nw = geo.nw;
     uint16_t* rows = reinterpret_cast<uint16_t*>(smem);
@@ -2383,8 +2393,10 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg1(const int32_t* __restric
     uint32_t* lev0s = reinterpret_cast<uint32_t*>(smem + geo.off_lev0);
     uint32_t* tag = reinterpret_cast<uint32_t*>(smem + geo.off_tag);
     uint32_t* mt = reinterpret_cast<uint32_t*>(smem + geo.off_mt);
+    uint32_t* mtb = reinterpret_cast<uint32_t*>(smem + geo.off_mtb);
     int* q_i = reinterpret_cast<int*>(smem + geo.off_q);
     double* q_u = reinterpret_cast<double*>(q_i + 64);
+    int* q_end = reinterpret_cast<int*>(q_u + 64);
     uint32_t* res = reinterpret_cast<uint32_t*>(smem + geo.off_res);
     double* res_a = reinterpret_cast<double*>(res + 64);
     double* res_b = res_a + 64;
@@ -2412,6 +2424,7 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg1(const int32_t* __restric
         for (int q = tid; q < 2 * nw; q += NT) lev[q] = 0u;
         for (int q = tid; q < nw * 32; q += NT) tag[q] = 0u;
         for (int q = tid; q < MT_N; q += NT) mt[q] = st.mt[r * MT_N + q];
+        for (int q = tid; q < 64; q += NT) q_i[q] = 0;
         const int64_t col = r >> 6;
         const u64 rbit = 1ull << (r & 63);
         __syncthreads();
@@ -2454,17 +2467,30 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg1(const int32_t* __restric
     double inv_n = 1.0 / (double)n;
     asm volatile("" : "+v"(a), "+v"(b), "+v"(par_a), "+v"(par_b), "+v"(a_cap), "+v"(b_cap), "+v"(inv_n));
 
-    // ---- proposal windows (wave 0), as k_sa_lds_multi
-    int pb_i = 0, pb_end = 0;
-    uint32_t pb_w1 = 0, pb_w2 = 0;
-    double pb_u = 0.0;
-    int npend = 0, pk = 0;
-    auto parse = [&](bool one) {
-        for (;;) {
+    int64_t k = 0;                                 // proposals taken in this launch (absolute ring index)
+    // ---- the parser wave: randint(0, n) + rand() pairs (code/SA_RRG.py:73,76) into
+    // the ring, one 64-word window per call (as k_sa_lds_wg's wave 0 parses them)
+    const int idx0 = idx;
+    int64_t produced = 0;                          // proposals in the ring (absolute count)
+    int64_t bak_at = -1;                           // proposals >= bak_at end after the latest twist
+    auto twist = [&]() {
+        for (int q = lane; q < MT_N; q += 64) mtb[q] = mt[q];   // the state of the proposals before it
+        bak_at = produced;
+        wave_sync();
+        lds_twist(mt, lane);
+        idx = 0;
+    };
+    // a second twist while proposals drawn before the first are still to be taken
+    // would lose their state (never: a state yields >= 100 proposals, the ring
+    // holds 63; the last clause keeps the ring from ever running dry)
+    auto can_twist = [&]() -> bool { return bak_at < 0 || k > bak_at || produced == k; };
+    auto refill = [&](int windows) {
+        for (int wd = 0; wd < windows; ++wd) {
+            const int room = (int)(k + RCAP - produced);
+            if (room <= 0 || produced - k >= TARGET) return;
             if (idx >= MT_N) {
-                if (one) break;
-                lds_twist(mt, lane);
-                idx = 0;
+                if (!can_twist()) return;
+                twist();
             }
             const int lim = (MT_N - idx < 64) ? MT_N - idx : 64;
             uint32_t tw = 0, y = 0;
@@ -2475,13 +2501,9 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg1(const int32_t* __restric
                 ok = y <= rng;
             }
             const u64 okm = __ballot(ok);
-            // proposal starts by a scalar walk over the ballot (each: the first
-            // acceptable word at or after the previous end, then rand()'s two
-            // words); the start lanes push their lane ids to their target lanes,
-            // which pull i, w1, w2 (lane-parallel: no readlane per proposal)
             u64 stm = 0;
             int pos = 0, got = 0;
-            while (pos < 64 && npend + got < 63) {
+            while (pos < 64 && got < room) {
                 const u64 m = okm >> pos;
                 if (!m) break;
                 const int f = pos + __ffsll((unsigned long long)m) - 1;
@@ -2490,93 +2512,65 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg1(const int32_t* __restric
                 ++got;
                 pos = f + 3;
             }
+            const uint32_t x1 = (uint32_t)__shfl((int)tw, lane + 1 < 64 ? lane + 1 : 63, 64);
+            const uint32_t x2 = (uint32_t)__shfl((int)tw, lane + 2 < 64 ? lane + 2 : 63, 64);
             if (got > 0) {
-                const bool isst = (stm >> lane) & 1ull;
-                const int tgt = isst ? npend + __popcll(stm & ((1ull << lane) - 1ull)) : 63;
-                const int src = __builtin_amdgcn_ds_permute(tgt * 4, lane) & 63;
-                const int yi = __builtin_amdgcn_ds_bpermute(src * 4, (int)y);
-                const int x1 = __builtin_amdgcn_ds_bpermute((src + 1) * 4, (int)tw);
-                const int x2 = __builtin_amdgcn_ds_bpermute((src + 2) * 4, (int)tw);
-                if (lane >= npend && lane < npend + got) {
-                    pb_i = yi;
-                    pb_w1 = (uint32_t)x1;
-                    pb_w2 = (uint32_t)x2;
-                    pb_end = idx + src + 3;
+                if ((stm >> lane) & 1ull) {
+                    const int e = (int)((produced + __popcll(stm & ltmask)) & 63);
+                    q_i[e] = (int)y;
+                    q_u[e] = mt_double(x1, x2);
+                    q_end[e] = idx + lane + 3;
                 }
-                npend += got;
+                produced += got;
                 idx += pos;
-                break;
+                continue;
             }
-            if (one) break;
             if (!okm) { idx += lim; continue; }
             const int f = __ffsll((unsigned long long)okm) - 1;
             if (f > 0) { idx += f; continue; }
+            // i is the window's first word and rand()'s two words cross the end of
+            // the state: the serial draw twists between them, as numpy does
+            if (!can_twist()) return;
             const int iv = __builtin_amdgcn_readlane((int)y, 0);
             idx += 1;
-            if (idx >= MT_N) { lds_twist(mt, lane); idx = 0; }
+            if (idx >= MT_N) twist();
             const uint32_t w1 = mt_temper(mt[idx]);
             idx += 1;
-            if (idx >= MT_N) { lds_twist(mt, lane); idx = 0; }
+            if (idx >= MT_N) twist();
             const uint32_t w2 = mt_temper(mt[idx]);
             idx += 1;
-            if (lane == npend) { pb_i = iv; pb_w1 = w1; pb_w2 = w2; pb_end = idx; }
-            ++npend;
-            break;
+            if (lane == 0) {
+                const int e = (int)(produced & 63);
+                q_i[e] = iv;
+                q_u[e] = mt_double(w1, w2);
+                q_end[e] = idx;
+            }
+            produced += 1;
         }
-        pb_u = mt_double(pb_w1, pb_w2);
     };
 
-    bool drew = false;
-    int64_t k = 0;
+#ifdef MJX_SA_PROF
+    unsigned long long _acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, _t0 = __builtin_amdgcn_s_memtime();
+#endif
     while (k < nsteps && done == 0) {
-        if (w == 0) {
-            const int avail = npend - pk;
-            bool re = false;
-            if (avail < K && idx + 64 <= MT_N) {
-                // carry the unconsumed proposals to lanes 0.. and append whole
-                // windows while no twist can fall under a carried proposal
-                const int src = (lane + pk < 64) ? lane + pk : 63;
-                pb_i = __shfl(pb_i, src, 64);
-                pb_end = __shfl(pb_end, src, 64);
-                pb_w1 = (uint32_t)__shfl((int)pb_w1, src, 64);
-                pb_w2 = (uint32_t)__shfl((int)pb_w2, src, 64);
-                npend = avail;
-                pk = 0;
-                while (npend < K && npend <= 64 - 22 && idx + 64 <= MT_N) {
-                    const int before = npend;
-                    parse(true);
-                    if (npend == before) break;
-                }
-                if (npend == 0) parse(false);
-                re = true;
-            } else if (avail == 0) {
-                npend = 0;
-                pk = 0;
-                parse(false);
-                re = true;
-            }
-            if (re) {
-                pb_u = mt_double(pb_w1, pb_w2);
-                q_i[lane] = pb_i;
-                q_u[lane] = pb_u;
-            }
-            if (lane == 0) {
-                ctl[0] = npend;
-                ctl[1] = pk;
-            }
+        if (parser) {
+            refill(2);
+            if (lane == 0) ctl[0] = (int)(produced - k);   // proposals ready for this round
         }
         __syncthreads();                                   // the round's proposals are published
-        drew = true;
-        const int npd = __builtin_amdgcn_readfirstlane(ctl[0]);
-        const int pks = __builtin_amdgcn_readfirstlane(ctl[1]);
-        int nq = npd - pks;
+        LDS_STAMP(0);
+        const int nready = __builtin_amdgcn_readfirstlane(ctl[0]);   // (rewritten before the next publish)
+        int nq = nready;
         if (nq > K) nq = K;
         if ((int64_t)nq > nsteps - k) nq = (int)(nsteps - k);
-        const bool act = qi < nq;
-        const int iv = q_i[pks + (act ? qi : 0)];
-        const double u = q_u[pks + (act ? qi : 0)];
+        const bool act = !parser && qi < nq;
+        const int iv = act ? q_i[(k + qi) & 63] : 0;
+        const double u = act ? q_u[(k + qi) & 63] : 0.0;
         if (act && gl == 0) atomicOr(&tag[iv], 1u << qi);
+        if (parser) refill(2);                             // while the proposal waves evaluate
+        LDS_STAMP(3);
         __syncthreads();                                   // every proposal's tag
+        LDS_STAMP(1);
         const uint32_t old_i = bit_of(0, iv);
         // level 1: i and its neighbours, level 0 with i flipped
         int ri[D];
@@ -2641,7 +2635,7 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg1(const int32_t* __restric
             acc = u < prob;
             tie = e < 1.0 && fabs(u - e) <= 4.0 * (nextafter(e, 2.0) - e);
         }
-        if (gl == 0) {
+        if (gl == 0 && !parser) {
             // proposal qi: the earlier proposals it read (bits < qi), accept and tie
             // flags, sum(s_end) change, the schedule after its step, delta_H
             res[qi] = cfg;
@@ -2651,7 +2645,9 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg1(const int32_t* __restric
             res_e[qi] = (double)ds;
             if (TRACE) res_e[32 + qi] = dE;
         }
+        LDS_STAMP(4);
         __syncthreads();                                   // every proposal's result
+        LDS_STAMP(5);
         // ---- resolve (every wave alike, lane-parallel over the K proposals): lane q
         // holds proposal q
         const bool lq = lane < nq;
@@ -2684,22 +2680,26 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg1(const int32_t* __restric
         ties += __popcll(__ballot((fl & 2u) != 0u) & tk);
         if (TRACE && w == 0 && lane < taken) {
             const int64_t kk = k + lane;
-            if (st.tr_i) st.tr_i[kk * R + r] = q_i[pks + lane];
+            if (st.tr_i) st.tr_i[kk * R + r] = q_i[(k + lane) & 63];
             if (st.tr_acc) st.tr_acc[kk * R + r] = accq ? 1 : 0;
             if (st.tr_sum) st.tr_sum[kk * R + r] = sum_after;
             if (st.tr_dE) st.tr_dE[kk * R + r] = res_e[32 + lane];
         }
         {
-            const int src = taken - 1;
-            sum_end = __shfl(sum_after, src, 64);
-            done = __shfl(dn_q, src, 64);
+            const int src = taken > 0 ? taken - 1 : 0;
+            const int64_t sum_n = __shfl(sum_after, src, 64);
+            const int done_n = __shfl(dn_q, src, 64);
+            if (taken > 0) {                               // (a round without proposals: none)
+                sum_end = sum_n;
+                done = done_n;
+                t += taken;
+                a = res_a[taken - 1];
+                b = res_b[taken - 1];
+            }
         }
-        t += taken;
-        a = res_a[taken - 1];
-        b = res_b[taken - 1];
         // ---- the taken accepted proposals: level 1 on their C_1, level 0 at i;
         // every proposal clears its tag
-        const bool mine = qi < taken && ((accm >> qi) & 1ull);
+        const bool mine = !parser && qi < taken && ((accm >> qi) & 1ull);
         if (mine) {
             if (chg) {
                 const uint32_t bt = 1u << (cand & 31);
@@ -2710,9 +2710,16 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg1(const int32_t* __restric
         }
         if (act && gl == 0) tag[iv] = 0u;
         k += taken;
-        pk += taken;
+        LDS_STAMP(6);
+#ifdef MJX_SA_PROF
+        _acc[7] += 1;                                      // rounds (every wave counts)
+#endif
     }
-    if (w == 0 && drew) idx = __builtin_amdgcn_readlane(pb_end, pk - 1);
+#ifdef MJX_SA_PROF
+    if (lane == 0)
+        for (int q = 0; q < 8; ++q) atomicAdd(&mjx_sa_lds_prof[q], _acc[q]);
+#endif
+
     if (TRACE && tid == 0) {
         for (; k < nsteps; ++k) {
             if (st.tr_i) st.tr_i[k * R + r] = -1;
@@ -2728,10 +2735,17 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg1(const int32_t* __restric
             if (((lev[v >> 5] ^ lev0s[v >> 5]) >> (v & 31)) & 1u)
                 atomicXor((unsigned long long*)&s[v * W + col], 1ull << (r & 63));
         }
-        for (int q = tid; q < MT_N; q += NT) st.mt[r * MT_N + q] = mt[q];
+    }
+    if (parser) {
+        // the stream numpy holds after the last proposal taken (before the first:
+        // the launch's position), in the state it was drawn from
+        const int64_t L = k - 1;
+        const int end = (L < 0) ? idx0 : q_end[L & 63];
+        const bool useb = bak_at >= 0 && L < bak_at;
+        for (int q = lane; q < MT_N; q += 64) st.mt[r * MT_N + q] = useb ? mtb[q] : mt[q];
+        if (lane == 0) st.mt_idx[r] = end;
     }
     if (tid == 0) {
-        st.mt_idx[r] = idx;
         st.a[r] = a;
         st.b[r] = b;
         st.t[r] = t;
@@ -2781,7 +2795,7 @@ extern "C" int64_t mjx_sa_lds_plan(int64_t n, int d, int p, int c, uint32_t flag
     salds::GeoW1 gw1;
     if (!(flags & (MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE | MJX_SA_LDS_PAIR | MJX_SA_LDS_WAVE)) && small_d && T == 1 &&
         salds::geometry_wg1(n, d, 32, &gw1)) {
-        th = 256;                                   // k_sa_lds_wg1: 4 waves x 8 proposals
+        th = 320;                                   // k_sa_lds_wg1: 4 waves x 8 proposals + the parser
         bytes = gw1.bytes;
     } else if (!(flags & (MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE | MJX_SA_LDS_PAIR)) && small_d && T == 1) {
         // k_sa_lds_multi: the one-plane geometry
@@ -2827,8 +2841,8 @@ extern "C" int mjx_sa_lds_steps(const int32_t* adj, int64_t n, int d, int p, int
         const bool trw = st.tr_i || st.tr_acc || st.tr_sum || st.tr_dE;
         auto gow1 = [&](auto kern) -> int {
             MJX_HIP(set_max_lds(kern, gw1.bytes), "sa_lds lds");
-            kern<<<(unsigned)R, 256, (size_t)gw1.bytes, hs>>>(adj, n, R, W, (u64*)s, st, nsteps, par_a, par_b, a_cap,
-                                                              b_cap, t_cap, gw1);
+            kern<<<(unsigned)R, 320, (size_t)gw1.bytes, hs>>>(adj, n, R, W, (u64*)s, st, nsteps, par_a, par_b, a_cap,
+                                                              b_cap, t_cap, gw1);          // 4 waves + the parser
             MJX_LAUNCH_CHECK("k_sa_lds_wg1");
             return MJX_OK;
         };

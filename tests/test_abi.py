@@ -139,7 +139,7 @@ def test_sa_lds_plan_names_the_kernel_that_runs(mjx_mod):
     assert th.value == 64 and one < pair
     assert lib.mjx_sa_lds_plan(10_000, 4, 3, 1, L.MJX_SA_LDS_SINGLE, 0, ctypes.byref(th)) == one and th.value == 64
     wg1 = lib.mjx_sa_lds_plan(10_000, 4, 1, 1, 0, 0, ctypes.byref(th))          # 4 waves x 8 proposals
-    assert th.value == 256 and lib.mjx_sa_lds_bytes(10_000, 4, 1, 1) < wg1 <= 160 * 1024
+    assert th.value == 320 and lib.mjx_sa_lds_bytes(10_000, 4, 1, 1) < wg1 <= 160 * 1024
     assert lib.mjx_sa_lds_plan(10_000, 4, 1, 1, L.MJX_SA_LDS_WAVE, 0, ctypes.byref(th)) == \
         lib.mjx_sa_lds_bytes(10_000, 4, 1, 1) and th.value == 64                    # one wave x 8 proposals
     assert lib.mjx_sa_lds_plan(100_000, 4, 3, 1, 0, 0, ctypes.byref(th)) == -1
