@@ -122,16 +122,20 @@ class ShardedRRG:
     into that many node ranges (NodeRange), each with its own sweep plan; the
     all-gather of piece g runs on RCCL's stream while piece g+1 is swept.
     ``local_sweep(s_in, s_out, counts, g)`` may replace the HIP sweep of piece
-    g (CPU tests over gloo)."""
+    g (CPU tests over gloo).  ``collective=True`` runs the exchange and the
+    count all-reduce through the process group even on one rank (a world-1
+    RCCL group on one GPU executes the same in-place all-gather calls as the
+    8-GPU run; tests/test_rccl_gpu.py)."""
 
     def __init__(self, d, n, seed=0, group=None, adj_rows=None, local_sweep=None, device=None, mode="binned",
-                 pieces=None):
+                 pieces=None, collective=False):
         import torch.distributed as dist
         self.dist = dist if dist.is_available() and dist.is_initialized() else None
         self.group = group
         self.world = self.dist.get_world_size(group) if self.dist else 1
         self.rank = self.dist.get_rank(group) if self.dist else 0
         self.backend = self.dist.get_backend(group) if self.dist else None
+        self.collective = bool(collective) and self.dist is not None
         self.d, self.n, self.seed = int(d), int(n), int(seed)
         if pieces is None:
             pieces = 1 if self.world == 1 else 2
@@ -201,7 +205,7 @@ class ShardedRRG:
         the state is read again.  One code path for every backend: RCCL on the
         GPU runs it on its own stream so piece g+1's sweep overlaps it; gloo (the
         CPU tests) runs the identical in-place call."""
-        if self.world == 1:
+        if self.world == 1 and not self.collective:
             return None
         r = self.range
         whole, mine = buf[r.piece_words(g)], buf[r.own_words(g)]
@@ -244,7 +248,7 @@ class ShardedRRG:
     def total_plus(self):
         """Global +1 count of the last counted sweep (one all-reduce)."""
         tot = self.cnt.clone()
-        if self.world > 1:
+        if self.world > 1 or self.collective:
             self.dist.all_reduce(tot, group=self.group)
         return int(tot.item())
 
