@@ -212,16 +212,18 @@ struct VertCounter {
         }
         ++added;
     }
-    // add the per-bit counts into dst[j*64 + b] (LDS or global)
+    // add the per-bit counts into dst[j*64 + ((b + rot) & 63)] (LDS or global).
+    // rot = the unit's index in the LDS block: lanes of consecutive units then
+    // add into 64 different banks instead of all into bank b
     template <typename DST>
-    __device__ __forceinline__ void flush(DST* dst) {
+    __device__ __forceinline__ void flush(DST* dst, int rot = 0) {
 #pragma unroll
         for (int j = 0; j < VW; ++j) {
             for (int b = 0; b < 64; ++b) {
                 unsigned cnt = 0;
 #pragma unroll
                 for (int p = 0; p < KC; ++p) cnt |= (unsigned)((c[j][p] >> b) & 1ull) << p;
-                if (cnt) atomicAdd(&dst[j * 64 + b], (DST)cnt);
+                if (cnt) atomicAdd(&dst[j * 64 + ((b + rot) & 63)], (DST)cnt);
             }
         }
         reset();
@@ -401,7 +403,7 @@ __device__ __forceinline__ void stv(u64* __restrict__ p, const u64* x) {
 template <int VW, int NK>
 __device__ __forceinline__ void flush_to(VertCounter<VW, NK>& vc, int use_lds, unsigned* lds,
                                          unsigned long long* counts, int64_t unit, int64_t unit0) {
-    if (use_lds) vc.flush(lds + (unit - unit0) * VW * 64);
+    if (use_lds) vc.flush(lds + (unit - unit0) * VW * 64, (int)((unit - unit0) & 63));
     else vc.flush(counts + unit * VW * 64);
 }
 
@@ -420,12 +422,22 @@ __device__ __forceinline__ void count_epilogue(VertCounter<VW, NK>& vc, bool act
                                                unsigned long long* __restrict__ counts) {
     if constexpr (COUNT) {
         if (use_lds) {
-            if (active && vc.added) vc.flush(lds + (unit - unit0) * VW * 64);
+            if (active && vc.added) vc.flush(lds + (unit - unit0) * VW * 64, (int)((unit - unit0) & 63));
             __syncthreads();  // every thread of the block reaches this (no early return)
-            const int64_t r0 = unit0 * VW * 64;
-            for (int64_t r = threadIdx.x; r < Us * VW * 64; r += BS) {
-                unsigned x = lds[r];
-                if (x) atomicAdd(&counts[r0 + r], (unsigned long long)x);
+            // undo the bank rotation; blocks start their walk at different
+            // replicas so that blocks ending together do not queue their global
+            // atomics on the same addresses
+            const int64_t r0 = unit0 * VW * 64, tot = Us * VW * 64;
+            const int64_t start = ((int64_t)blockIdx.x * BS) % tot;
+            for (int64_t i = threadIdx.x; i < tot; i += BS) {
+                int64_t r = start + i;
+                if (r >= tot) r -= tot;
+                const unsigned x = lds[r];
+                if (x) {
+                    const int64_t u = r / (VW * 64), rem = r - u * (VW * 64);
+                    const int64_t b = ((rem & 63) - u) & 63;
+                    atomicAdd(&counts[r0 + u * (VW * 64) + (rem & ~63LL) + b], (unsigned long long)x);
+                }
             }
         } else {
             if (active && vc.added) vc.flush(counts + unit * VW * 64);

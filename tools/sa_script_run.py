@@ -1,11 +1,11 @@
 """SA_RRG.py literally, at the script's own size (code/SA_RRG.py:44-92: n = 1e4,
 d = 4, p = 3, c = 1, N_stat = 5): the replicas back to back on ONE numpy stream
 seeded once, a fresh random 4-regular graph each, every replica run until
-m(s_endstate(s)) = 1 (or the t > 2n^3 cap, or --max-s of wall time) -- what
+m(s_endstate(s)) = 1 (or the t > 2n^3 cap; --max-s bounds this call's wall time) -- what
 mjx.sa_run(..., stream="global") does, stepped here with a progress line every
 --every seconds.  Writes the script's np.savez keys (mag_reached, num_steps,
-conf, graphs) to gpurun_out/MCMC_p3_d4.npz.  A replica stopped by the wall
-cap is checkpointed (SAReplicas.save_checkpoint: its configuration, the
+conf, graphs) to gpurun_out/MCMC_p3_d4.npz.  The replica running when
+the call's wall cap is reached is checkpointed (SAReplicas.save_checkpoint: its configuration, the
 stream, a, b, t) with the results so far to gpurun_out/sa_script_ckpt.npz;
 --resume FILE continues the run from such a file (copied into the tree: the
 GPU box sees only the tree), bit for bit as if it had never stopped.
@@ -27,7 +27,7 @@ ap.add_argument("--n", type=int, default=10_000)
 ap.add_argument("--nstat", type=int, default=5)
 ap.add_argument("--seed", type=int, default=0)
 ap.add_argument("--graph-seed", type=int, default=100)
-ap.add_argument("--max-s", type=float, default=170.0)
+ap.add_argument("--max-s", type=float, default=170.0, help="wall cap of this call (all replicas)")
 ap.add_argument("--every", type=float, default=20.0)
 ap.add_argument("--resume", default=None)
 args = ap.parse_args()
@@ -55,7 +55,7 @@ for k, g in enumerate(graphs):
     torch.cuda.synchronize()
     t0 = last = time.perf_counter()
     chunk = 1 << 16
-    while not sa.all_done() and time.perf_counter() - t0 < args.max_s:
+    while not sa.all_done() and time.perf_counter() - t_all < args.max_s:
         sa.steps(chunk)
         chunk = min(2 * chunk, 1 << 22)
         if time.perf_counter() - last > args.every:
