@@ -53,6 +53,7 @@ for k, g in enumerate(graphs):
     else:
         sa = mjx.SAReplicas(g, p, c, [args.seed], tape=0, mt_state=state, layout="lds")
     torch.cuda.synchronize()
+    steps0 = int(sa.t.item())            # > 0 for a resumed replica
     t0 = last = time.perf_counter()
     chunk = 1 << 16
     while not sa.all_done() and time.perf_counter() - t_all < args.max_s:
@@ -68,7 +69,7 @@ for k, g in enumerate(graphs):
     res["wall_s"][k] += wall
     done = int(out["done"][0])
     print(f"replica {k}: done={done} num_steps={int(out['num_steps'][0])} mag_reached={out['mag_reached'][0]:.4f} "
-          f"wall {wall:.1f} s ({1e6 * wall / max(out['num_steps'][0], 1):.3f} us per proposal)", flush=True)
+          f"wall {wall:.1f} s ({1e6 * wall / max(out['num_steps'][0] - steps0, 1):.3f} us per proposal in this call)", flush=True)
     state = sa.mt_state()
     if done == 0:
         os.makedirs("gpurun_out", exist_ok=True)
