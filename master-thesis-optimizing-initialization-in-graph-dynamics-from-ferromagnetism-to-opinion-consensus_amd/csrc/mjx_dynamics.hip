@@ -575,6 +575,63 @@ __global__ void __launch_bounds__(kBlock) k_sweep_gen_rp(const int32_t* __restri
 // parameter, the runtime bit counter (88 -> fewer VGPRs, more waves in
 // flight for a latency-bound gather).  D = -1: runtime degree `dd` (> 8).
 // ---------------------------------------------------------------------------
+// One node of a degree class: position i of the class (order = the class's
+// node list, cell = its neighbour rows), new bits of this thread's unit into
+// out[] and s_out.
+template <int D, int VW>
+__device__ __forceinline__ void cls_node(const int32_t* __restrict__ order, const int32_t* __restrict__ cell,
+                                         int64_t i, int dd, int64_t W, const u64* __restrict__ s_in,
+                                         u64* __restrict__ s_out, int64_t unit, u64* out) {
+    const int64_t v = order[i];
+    u64 own[VW];
+    if constexpr (D == 0) {
+        // no neighbours: S = 0, a tie, the spin stays (nb:113-117)
+        ldv<VW>(s_in + v * W + unit * VW, out);
+    } else if constexpr (D > 0) {
+        int32_t k[D];
+        load_adj<D>(cell, i, k);
+        u64 x[D][VW];
+#pragma unroll
+        for (int j = 0; j < D; ++j) ldv<VW>(s_in + (int64_t)k[j] * W + unit * VW, x[j]);
+        ldv<VW>(s_in + v * W + unit * VW, own);
+#pragma unroll
+        for (int q = 0; q < VW; ++q) {
+            u64 xs[D];
+#pragma unroll
+            for (int j = 0; j < D; ++j) xs[j] = x[j][q];
+            out[q] = majority_fixed<D>(xs, own[q]);
+        }
+    } else {
+        const int32_t* row = cell + i * dd;
+        BitCounter<8> bc[VW];
+#pragma unroll
+        for (int q = 0; q < VW; ++q) bc[q].reset();
+        int j = 0;
+        for (; j + 4 <= dd; j += 4) {
+            int32_t k[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) k[m] = row[j + m];
+            u64 x[4][VW];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) ldv<VW>(s_in + (int64_t)k[m] * W + unit * VW, x[m]);
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+#pragma unroll
+                for (int q = 0; q < VW; ++q) bc[q].add(x[m][q]);
+        }
+        for (; j < dd; ++j) {
+            u64 x[VW];
+            ldv<VW>(s_in + (int64_t)row[j] * W + unit * VW, x);
+#pragma unroll
+            for (int q = 0; q < VW; ++q) bc[q].add(x[q]);
+        }
+        ldv<VW>(s_in + v * W + unit * VW, own);
+#pragma unroll
+        for (int q = 0; q < VW; ++q) out[q] = bc[q].majority(dd, own[q]);
+    }
+    stv<VW>(s_out + v * W + unit * VW, out);
+}
+
 template <int D, int VW, bool COUNT, int NK = KC>
 __global__ void __launch_bounds__(kBlock) k_sweep_cls_rp(const int32_t* __restrict__ order,
                                                          const int32_t* __restrict__ cell, int64_t cnt, int dd,
@@ -594,54 +651,8 @@ __global__ void __launch_bounds__(kBlock) k_sweep_cls_rp(const int32_t* __restri
     }
     if (active) {
         for (int64_t i = slot; i < cnt; i += slots) {
-            const int64_t v = order[i];
-            u64 own[VW], out[VW];
-            if constexpr (D == 0) {
-                // no neighbours: S = 0, a tie, the spin stays (nb:113-117)
-                ldv<VW>(s_in + v * W + unit * VW, out);
-            } else if constexpr (D > 0) {
-                int32_t k[D];
-                load_adj<D>(cell, i, k);
-                u64 x[D][VW];
-#pragma unroll
-                for (int j = 0; j < D; ++j) ldv<VW>(s_in + (int64_t)k[j] * W + unit * VW, x[j]);
-                ldv<VW>(s_in + v * W + unit * VW, own);
-#pragma unroll
-                for (int q = 0; q < VW; ++q) {
-                    u64 xs[D];
-#pragma unroll
-                    for (int j = 0; j < D; ++j) xs[j] = x[j][q];
-                    out[q] = majority_fixed<D>(xs, own[q]);
-                }
-            } else {
-                const int32_t* row = cell + i * dd;
-                BitCounter<8> bc[VW];
-#pragma unroll
-                for (int q = 0; q < VW; ++q) bc[q].reset();
-                int j = 0;
-                for (; j + 4 <= dd; j += 4) {
-                    int32_t k[4];
-#pragma unroll
-                    for (int m = 0; m < 4; ++m) k[m] = row[j + m];
-                    u64 x[4][VW];
-#pragma unroll
-                    for (int m = 0; m < 4; ++m) ldv<VW>(s_in + (int64_t)k[m] * W + unit * VW, x[m]);
-#pragma unroll
-                    for (int m = 0; m < 4; ++m)
-#pragma unroll
-                        for (int q = 0; q < VW; ++q) bc[q].add(x[m][q]);
-                }
-                for (; j < dd; ++j) {
-                    u64 x[VW];
-                    ldv<VW>(s_in + (int64_t)row[j] * W + unit * VW, x);
-#pragma unroll
-                    for (int q = 0; q < VW; ++q) bc[q].add(x[q]);
-                }
-                ldv<VW>(s_in + v * W + unit * VW, own);
-#pragma unroll
-                for (int q = 0; q < VW; ++q) out[q] = bc[q].majority(dd, own[q]);
-            }
-            stv<VW>(s_out + v * W + unit * VW, out);
+            u64 out[VW];
+            cls_node<D, VW>(order, cell, i, dd, W, s_in, s_out, unit, out);
             if constexpr (COUNT) {
                 vc.add(out);
                 if (vc.added == (1 << NK) - 1) flush_to(vc, use_lds, lds_cnt, counts, unit, unit0);
@@ -649,6 +660,67 @@ __global__ void __launch_bounds__(kBlock) k_sweep_cls_rp(const int32_t* __restri
         }
     }
     count_epilogue<VW, COUNT, kBlock, NK>(vc, active, unit, unit0, Us, lds_cnt, use_lds, counts);
+}
+
+// The counting sweep of a rollout over ALL degree classes in one launch: a
+// thread walks its positions of the class-sorted node order with a forward
+// class cursor and runs the class's node body (D <= 8 specialised).  The
+// per-class launches each paid the count epilogue (Us*VW*64 global atomics
+// per block, 40-100 us per launch at R = 4096, profiles/r04_bench_kernel_stats.csv);
+// here it is paid once per sweep.
+constexpr int kMaxCls = 64;
+struct ClsTable {
+    int nc;
+    int D[kMaxCls];
+    int64_t i0[kMaxCls + 1];   // class c = positions [i0[c], i0[c+1]) of order
+    int64_t base[kMaxCls];     // its cell rows start at cell + base[c]
+};
+
+#ifdef MJX_CLS_ALL_WAVES       // timing variants: a VGPR cap for the one-launch kernel
+#define MJX_CLS_ALL_ATTR __attribute__((amdgpu_waves_per_eu(MJX_CLS_ALL_WAVES, 8)))
+#else
+#define MJX_CLS_ALL_ATTR
+#endif
+template <int VW>
+__global__ void __launch_bounds__(kBlock) MJX_CLS_ALL_ATTR k_sweep_cls_all_rp(const int32_t* __restrict__ order,
+                                                             const int32_t* __restrict__ cell, ClsTable tab,
+                                                             int64_t W, const u64* __restrict__ s_in,
+                                                             u64* __restrict__ s_out,
+                                                             unsigned long long* __restrict__ counts, int use_lds,
+                                                             int64_t Us) {
+    extern __shared__ unsigned lds_cnt[];
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t slots = ((int64_t)gridDim.x * kBlock) / Us;
+    const int64_t unit = t % Us, slot = t / Us;
+    const bool active = slot < slots;
+    VertCounter<VW> vc;
+    vc.reset();
+    lds_count_init<VW>(lds_cnt, Us, use_lds);
+    if (active) {
+        int c = 0;
+        for (int64_t i = tab.i0[0] + slot; i < tab.i0[tab.nc]; i += slots) {
+            while (i >= tab.i0[c + 1]) ++c;
+            const int32_t* o = order + tab.i0[c];
+            const int32_t* cl = cell + tab.base[c];
+            const int64_t r = i - tab.i0[c];
+            u64 out[VW];
+            switch (tab.D[c]) {
+                case 0: cls_node<0, VW>(o, cl, r, 0, W, s_in, s_out, unit, out); break;
+                case 1: cls_node<1, VW>(o, cl, r, 1, W, s_in, s_out, unit, out); break;
+                case 2: cls_node<2, VW>(o, cl, r, 2, W, s_in, s_out, unit, out); break;
+                case 3: cls_node<3, VW>(o, cl, r, 3, W, s_in, s_out, unit, out); break;
+                case 4: cls_node<4, VW>(o, cl, r, 4, W, s_in, s_out, unit, out); break;
+                case 5: cls_node<5, VW>(o, cl, r, 5, W, s_in, s_out, unit, out); break;
+                case 6: cls_node<6, VW>(o, cl, r, 6, W, s_in, s_out, unit, out); break;
+                case 7: cls_node<7, VW>(o, cl, r, 7, W, s_in, s_out, unit, out); break;
+                case 8: cls_node<8, VW>(o, cl, r, 8, W, s_in, s_out, unit, out); break;
+                default: cls_node<-1, VW>(o, cl, r, tab.D[c], W, s_in, s_out, unit, out); break;
+            }
+            vc.add(out);
+            if (vc.added == (1 << KC) - 1) flush_to(vc, use_lds, lds_cnt, counts, unit, 0);
+        }
+    }
+    count_epilogue<VW, true>(vc, active, unit, 0, Us, lds_cnt, use_lds, counts);
 }
 
 // The classes above D = 8 (few nodes each: Poisson tail) in one launch: a
@@ -1295,7 +1367,34 @@ extern "C" int mjx_rollout_class_rp(const int32_t* order, const int32_t* cell, c
     int grid, vw, use_lds; size_t lds;
     rc = rp_geometry(n, words, Us, &grid, &vw, &use_lds, &lds);
     if (rc) return rc;
+    // the counting sweep in one launch when the classes tile `order` in sequence
+    // (-DMJX_CLS_PER_LAUNCH: the per-class counting launches, for timing A/B)
+    ClsTable all{};
+#ifdef MJX_CLS_PER_LAUNCH
+    bool one_launch = false;
+#else
+    bool one_launch = nclasses <= kMaxCls;
+#endif
+    for (int c = 0; c < nclasses && one_launch; ++c) {
+        all.D[c] = (int)classes[4 * c + 2];
+        all.i0[c] = classes[4 * c];
+        all.base[c] = classes[4 * c + 3];
+        one_launch = classes[4 * c] == (c ? classes[4 * (c - 1)] + classes[4 * (c - 1) + 1] : 0) &&
+                     (classes[4 * c + 1] * classes[4 * c + 2] == 0 || cell);
+    }
+    all.nc = nclasses;
+    all.i0[nclasses] = nclasses ? classes[4 * (nclasses - 1)] + classes[4 * (nclasses - 1) + 1] : 0;
     auto sweep = [&](const u64* a, u64* b, unsigned long long* cn) {
+        if (cn && one_launch) {
+            auto go = [&](auto kern) {
+                const int g = resident_grid(kern, kBlock, lds, n * Us);
+                kern<<<g, kBlock, lds, st>>>(order, cell, all, words, a, b, cn, use_lds, Us);
+            };
+            if (vw == 2) go(k_sweep_cls_all_rp<2>);
+            else go(k_sweep_cls_all_rp<1>);
+            MJX_LAUNCH_CHECK("sweep_cls_all_rp");
+            return (int)MJX_OK;
+        }
         // runs of consecutive classes with D > 8 (adjacent in `order`) share one launch
         GenTable tab{};
         int64_t g0 = 0;

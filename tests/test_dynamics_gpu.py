@@ -231,3 +231,33 @@ def test_numpy_neighbour_array_uploaded_once(mjx_mod):
     N2 = mjx_mod.random_regular_graph(4, 1000, seed=4).astype(np.int64)
     assert mjx_mod.as_graph(N2) is not g1
     assert np.array_equal(mjx_mod.s_endstate(N2, s, 2, 1), orc.s_endstate(N2, s, 2, 1))
+
+
+def test_class_sweep_more_classes_than_one_launch_holds(mjx_mod):
+    """More than 64 degree classes: the counting sweep falls back from the
+    one-launch kernel (k_sweep_cls_all_rp, a 64-class table) to a launch per
+    class; rollout and fused counts still equal the CSR sweep and the oracle."""
+    n, R = 3000, 128
+    rng = np.random.default_rng(9)
+    a, b = [], []
+    for hub in range(90):                      # hub h gets h + 1 extra neighbours -> ~90 distinct degrees
+        nb = rng.choice(np.arange(100, n), hub + 1, replace=False)
+        a += [hub] * len(nb)
+        b += nb.tolist()
+    u, v = rng.integers(100, n, 4000), rng.integers(100, n, 4000)
+    a, b = np.r_[a, u], np.r_[b, v]
+    keep = a != b
+    key = np.unique(np.minimum(a, b)[keep] * n + np.maximum(a, b)[keep])
+    rp, col = mjx_mod.csr_from_edges(n, key // n, key % n)
+    g = mjx_mod.Graph.csr(rp, col)
+    _, _, classes = g.class_ell()
+    assert len(classes) > 64
+    W = R // 64
+    S0 = 2 * rng.integers(0, 2, size=(R, n)).astype(np.int64) - 1
+    bits = mjx_mod.pack(S0)
+    for T in (1, 2):
+        cnt = torch.zeros(R, dtype=torch.int64, device="cuda")
+        out = mjx_mod.rollout(g, bits, T, words=W, counts=cnt)
+        want = orc.s_endstate_er(rp, col, S0, T, 1)
+        assert np.array_equal(cnt.cpu().numpy(), (want > 0).sum(axis=1)), T
+        assert torch.equal(out, mjx_mod.pack(want)), T
