@@ -662,13 +662,19 @@ __global__ void __launch_bounds__(kBlock) k_sweep_cls_rp(const int32_t* __restri
     count_epilogue<VW, COUNT, kBlock, NK>(vc, active, unit, unit0, Us, lds_cnt, use_lds, counts);
 }
 
-// The counting sweep of a rollout over ALL degree classes in one launch: a
-// thread walks its positions of the class-sorted node order with a forward
-// class cursor and runs the class's node body (D <= 8 specialised).  The
-// per-class launches each paid the count epilogue (Us*VW*64 global atomics
-// per block, 40-100 us per launch at R = 4096, profiles/r04_bench_kernel_stats.csv);
-// here it is paid once per sweep.
-constexpr int kMaxCls = 64;
+// The counting sweep of a rollout over the degree classes D <= 8 in one
+// launch: a thread walks its positions of the class-sorted node order with a
+// forward class cursor and runs the class's node body.  The per-class launches
+// each paid the count epilogue (Us*VW*64 global atomics per block, 40-100 us
+// per launch at R = 4096, profiles/r04_bench_kernel_stats.csv); here it is
+// paid once for them.  No runtime-degree body (the D > 8 tail keeps its own
+// table launch) and 6 counter planes (a flush every 63 nodes): 90 VGPRs,
+// 5 waves per SIMD (with both: 124, 4 waves).
+constexpr int kMaxCls = 9;
+#ifndef MJX_CLS_ALL_NK
+#define MJX_CLS_ALL_NK 6
+#endif
+constexpr int kClsAllPlanes = MJX_CLS_ALL_NK;
 struct ClsTable {
     int nc;
     int D[kMaxCls];
@@ -676,13 +682,8 @@ struct ClsTable {
     int64_t base[kMaxCls];     // its cell rows start at cell + base[c]
 };
 
-#ifdef MJX_CLS_ALL_WAVES       // timing variants: a VGPR cap for the one-launch kernel
-#define MJX_CLS_ALL_ATTR __attribute__((amdgpu_waves_per_eu(MJX_CLS_ALL_WAVES, 8)))
-#else
-#define MJX_CLS_ALL_ATTR
-#endif
 template <int VW>
-__global__ void __launch_bounds__(kBlock) MJX_CLS_ALL_ATTR k_sweep_cls_all_rp(const int32_t* __restrict__ order,
+__global__ void __launch_bounds__(kBlock) k_sweep_cls_all_rp(const int32_t* __restrict__ order,
                                                              const int32_t* __restrict__ cell, ClsTable tab,
                                                              int64_t W, const u64* __restrict__ s_in,
                                                              u64* __restrict__ s_out,
@@ -693,7 +694,7 @@ __global__ void __launch_bounds__(kBlock) MJX_CLS_ALL_ATTR k_sweep_cls_all_rp(co
     const int64_t slots = ((int64_t)gridDim.x * kBlock) / Us;
     const int64_t unit = t % Us, slot = t / Us;
     const bool active = slot < slots;
-    VertCounter<VW> vc;
+    VertCounter<VW, kClsAllPlanes> vc;
     vc.reset();
     lds_count_init<VW>(lds_cnt, Us, use_lds);
     if (active) {
@@ -714,13 +715,13 @@ __global__ void __launch_bounds__(kBlock) MJX_CLS_ALL_ATTR k_sweep_cls_all_rp(co
                 case 6: cls_node<6, VW>(o, cl, r, 6, W, s_in, s_out, unit, out); break;
                 case 7: cls_node<7, VW>(o, cl, r, 7, W, s_in, s_out, unit, out); break;
                 case 8: cls_node<8, VW>(o, cl, r, 8, W, s_in, s_out, unit, out); break;
-                default: cls_node<-1, VW>(o, cl, r, tab.D[c], W, s_in, s_out, unit, out); break;
+                default: __builtin_unreachable();        // the host passes D <= 8 only
             }
             vc.add(out);
-            if (vc.added == (1 << KC) - 1) flush_to(vc, use_lds, lds_cnt, counts, unit, 0);
+            if (vc.added == (1 << kClsAllPlanes) - 1) flush_to(vc, use_lds, lds_cnt, counts, unit, 0);
         }
     }
-    count_epilogue<VW, true>(vc, active, unit, 0, Us, lds_cnt, use_lds, counts);
+    count_epilogue<VW, true, kBlock, kClsAllPlanes>(vc, active, unit, 0, Us, lds_cnt, use_lds, counts);
 }
 
 // The classes above D = 8 (few nodes each: Poisson tail) in one launch: a
@@ -1367,25 +1368,26 @@ extern "C" int mjx_rollout_class_rp(const int32_t* order, const int32_t* cell, c
     int grid, vw, use_lds; size_t lds;
     rc = rp_geometry(n, words, Us, &grid, &vw, &use_lds, &lds);
     if (rc) return rc;
-    // the counting sweep in one launch when the classes tile `order` in sequence
-    // (-DMJX_CLS_PER_LAUNCH: the per-class counting launches, for timing A/B)
+    // the counting sweep of the leading classes with D <= 8 that tile `order`
+    // from position 0 in one launch (-DMJX_CLS_PER_LAUNCH: the per-class
+    // counting launches, for timing A/B); the rest as below
     ClsTable all{};
-#ifdef MJX_CLS_PER_LAUNCH
-    bool one_launch = false;
-#else
-    bool one_launch = nclasses <= kMaxCls;
-#endif
-    for (int c = 0; c < nclasses && one_launch; ++c) {
-        all.D[c] = (int)classes[4 * c + 2];
-        all.i0[c] = classes[4 * c];
-        all.base[c] = classes[4 * c + 3];
-        one_launch = classes[4 * c] == (c ? classes[4 * (c - 1)] + classes[4 * (c - 1) + 1] : 0) &&
-                     (classes[4 * c + 1] * classes[4 * c + 2] == 0 || cell);
+    int lead = 0;
+#ifndef MJX_CLS_PER_LAUNCH
+    for (int64_t pos = 0; lead < nclasses && lead < kMaxCls; ++lead) {
+        const int64_t* cl = classes + 4 * lead;
+        if (cl[0] != pos || cl[2] > 8 || (cl[1] * cl[2] > 0 && !cell)) break;
+        all.D[lead] = (int)cl[2];
+        all.i0[lead] = cl[0];
+        all.base[lead] = cl[3];
+        pos = cl[0] + cl[1];
     }
-    all.nc = nclasses;
-    all.i0[nclasses] = nclasses ? classes[4 * (nclasses - 1)] + classes[4 * (nclasses - 1) + 1] : 0;
+#endif
+    all.nc = lead;
+    all.i0[lead] = lead ? all.i0[lead - 1] + classes[4 * (lead - 1) + 1] : 0;
     auto sweep = [&](const u64* a, u64* b, unsigned long long* cn) {
-        if (cn && one_launch) {
+        const int c0 = (cn && lead >= 2) ? lead : 0;
+        if (c0) {
             auto go = [&](auto kern) {
                 const int g = resident_grid(kern, kBlock, lds, n * Us);
                 kern<<<g, kBlock, lds, st>>>(order, cell, all, words, a, b, cn, use_lds, Us);
@@ -1393,7 +1395,6 @@ extern "C" int mjx_rollout_class_rp(const int32_t* order, const int32_t* cell, c
             if (vw == 2) go(k_sweep_cls_all_rp<2>);
             else go(k_sweep_cls_all_rp<1>);
             MJX_LAUNCH_CHECK("sweep_cls_all_rp");
-            return (int)MJX_OK;
         }
         // runs of consecutive classes with D > 8 (adjacent in `order`) share one launch
         GenTable tab{};
@@ -1409,7 +1410,7 @@ extern "C" int mjx_rollout_class_rp(const int32_t* order, const int32_t* cell, c
             tab.nc = 0;
             return r;
         };
-        for (int c = 0; c < nclasses; ++c) {
+        for (int c = c0; c < nclasses; ++c) {
             const int64_t i0 = classes[4 * c], cnt = classes[4 * c + 1], base = classes[4 * c + 3];
             const int D = (int)classes[4 * c + 2];
             if (cnt == 0) continue;

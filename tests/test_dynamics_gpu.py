@@ -233,10 +233,11 @@ def test_numpy_neighbour_array_uploaded_once(mjx_mod):
     assert np.array_equal(mjx_mod.s_endstate(N2, s, 2, 1), orc.s_endstate(N2, s, 2, 1))
 
 
-def test_class_sweep_more_classes_than_one_launch_holds(mjx_mod):
-    """More than 64 degree classes: the counting sweep falls back from the
-    one-launch kernel (k_sweep_cls_all_rp, a 64-class table) to a launch per
-    class; rollout and fused counts still equal the CSR sweep and the oracle."""
+def test_class_sweep_long_degree_tail(mjx_mod):
+    """About 90 degree classes: the counting sweep runs the D <= 8 classes in
+    one launch (k_sweep_cls_all_rp) and the long D > 8 tail as several
+    32-class table launches (k_sweep_cls_gen_rp); rollout and fused counts
+    equal the oracle."""
     n, R = 3000, 128
     rng = np.random.default_rng(9)
     a, b = [], []
