@@ -874,7 +874,9 @@ def er_sweep_traffic():
     except (OSError, ValueError):
         return None
     plain = sum(v["bytes_per_launch"] for k, v in d.items() if k.startswith("mjx::k_sweep_cls") and "false" in k)
-    count = sum(v["bytes_per_launch"] for k, v in d.items() if k.startswith("mjx::k_sweep_cls") and "true" in k)
+    # the counting sweep: k_sweep_cls_all_rp (the D <= 8 classes in one launch) + the D > 8 tail
+    count = sum(v["bytes_per_launch"] for k, v in d.items()
+                if k.startswith("mjx::k_sweep_cls") and ("true" in k or k.startswith("mjx::k_sweep_cls_all_rp")))
     return {"plain_sweep_bytes": plain, "counting_sweep_bytes": count} if plain and count else None
 
 
