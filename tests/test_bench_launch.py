@@ -61,3 +61,17 @@ def test_too_few_gpus_fails_loudly():
     assert p.returncode != 0
     assert "visible" in p.stderr
     assert not _json_lines(p.stdout)
+
+
+def test_bench_reads_committed_pmc_traffic():
+    """The bench line's `traffic` fields come from profiles/pmc_traffic.json:
+    the headline sweep's bytes per launch, and the ER step's plain and
+    counting sweeps (the counting one now k_sweep_cls_all_rp + the D > 8
+    tail), each within a few percent of the algorithmic bytes."""
+    sys.path.insert(0, ROOT)
+    import bench
+    t = bench.rocprof_traffic()
+    assert t is not None and abs(t / 3.088e9 - 1) < 0.05        # d=4, N=1e6, R=4096: 3088 B per node
+    er = bench.er_sweep_traffic()
+    assert er is not None
+    assert abs(er["counting_sweep_bytes"] / er["plain_sweep_bytes"] - 1) < 0.05
