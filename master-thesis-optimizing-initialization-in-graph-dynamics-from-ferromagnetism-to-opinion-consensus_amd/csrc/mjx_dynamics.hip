@@ -14,6 +14,8 @@
 #include <string.h>
 #include <stdio.h>
 #include <mutex>
+#include <atomic>
+#include <unordered_map>
 #include <stdlib.h>
 #include <math.h>
 
@@ -25,22 +27,53 @@ void set_hip_error(hipError_t e, const char* where) {
     snprintf(g_hip_err, sizeof(g_hip_err), "%s: %s (%d)", where, hipGetErrorString(e), (int)e);
 }
 
-// A small memo table keyed by (device, pointer, two integers); a value is
-// computed once under the lock, failed computations are not kept.
+// Memo tables keyed by (device, pointer, two integers), in a hash map (no
+// capacity limit: the keys are the library's kernels x the sizes a process
+// uses).  `get`: a value computed once under the lock, failed computations not
+// kept.  `raise_to`: the LARGEST value applied so far per (device, kernel); the
+// setter runs only when a larger one is asked for (the dynamic-LDS opt-in is
+// an upper bound, so a smaller later launch must never lower it: ADVICE r04).
 struct DevMemo {
-    struct Entry { int dev; const void* k; int64_t a, b; int v; };
+    struct Key {
+        int dev; const void* k; int64_t a, b;
+        bool operator==(const Key& o) const { return dev == o.dev && k == o.k && a == o.a && b == o.b; }
+    };
+    struct Hash {
+        size_t operator()(const Key& x) const {
+            uint64_t h = (uint64_t)(uintptr_t)x.k * 0x9E3779B97F4A7C15ull;
+            h ^= ((uint64_t)x.a + 0x632BE59BD9B4E019ull + (h << 6) + (h >> 2));
+            h ^= ((uint64_t)x.b * 0xBF58476D1CE4E5B9ull + (h << 6) + (h >> 2));
+            h ^= (uint64_t)(uint32_t)x.dev * 0x94D049BB133111EBull;
+            return (size_t)h;
+        }
+    };
     std::mutex mu;
-    Entry e[512];
-    int used = 0;
+    std::unordered_map<Key, int, Hash> e;
     template <typename F>
     int get(int dev, const void* k, int64_t a, int64_t b, F&& compute) {
         std::lock_guard<std::mutex> lock(mu);
-        for (int i = 0; i < used; ++i)
-            if (e[i].dev == dev && e[i].k == k && e[i].a == a && e[i].b == b) return e[i].v;
+        const Key key{dev, k, a, b};
+        auto it = e.find(key);
+        if (it != e.end()) return it->second;
         bool ok = true;
         const int v = compute(ok);
-        if (ok && used < 512) e[used++] = Entry{dev, k, a, b, v};
+        if (ok) e.emplace(key, v);
         return v;
+    }
+    // setter(v) -> 0 on success; returns the setter's status (0 when no call was needed)
+    template <typename F>
+    int raise_to(int dev, const void* k, int v, F&& setter) {
+        std::lock_guard<std::mutex> lock(mu);
+        const Key key{dev, k, -1, -1};
+        auto it = e.find(key);
+        if (it != e.end() && it->second >= v) return 0;
+        const int st = setter(v);
+        if (st == 0) e[key] = v;
+        return st;
+    }
+    size_t size() {
+        std::lock_guard<std::mutex> lock(mu);
+        return e.size();
     }
 };
 
@@ -58,25 +91,30 @@ static DevMemo& memo() {
     return m;
 }
 
+// CU count per device: read lock-free on every launch (0 = not yet known)
+constexpr int kMaxDevices = 64;
+static std::atomic<int> g_cus[kMaxDevices];
+
 int device_cus() {
     const int dev = current_device();
-    return memo().get(dev, nullptr, 0, 0, [&](bool& ok) {
-        int cus = 0;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) {
-            (void)hipGetLastError();
-            ok = false;
-            return 256;                 // a whole MI355X (8 XCDs x 32 CUs)
-        }
-        return cus;
-    });
+    const int slot = (dev >= 0 && dev < kMaxDevices) ? dev : -1;
+    if (slot >= 0) {
+        const int v = g_cus[slot].load(std::memory_order_relaxed);
+        if (v > 0) return v;
+    }
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) {
+        (void)hipGetLastError();
+        return 256;                     // a whole MI355X (8 XCDs x 32 CUs); not kept, asked again
+    }
+    if (slot >= 0) g_cus[slot].store(cus, std::memory_order_relaxed);
+    return cus;
 }
 
 hipError_t set_max_lds(const void* kernel, int bytes) {
     const int dev = current_device();
-    return (hipError_t)memo().get(dev, kernel, -1, bytes, [&](bool& ok) {
-        const hipError_t e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-        ok = e == hipSuccess;
-        return (int)e;
+    return (hipError_t)memo().raise_to(dev, kernel, bytes, [&](int v) {
+        return (int)hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, v);
     });
 }
 
@@ -114,6 +152,25 @@ extern "C" int mjx_selftest_devmemo(void) {
     m.get(2, &k1, 0, 0, bad);
     m.get(2, &k1, 0, 0, bad);
     if (tries != 2) return 7;                                          // failures are not kept
+    // the LDS opt-in: n = 1e4, then 1e3, then 1e4 on one kernel
+    int sets = 0, last = 0;
+    auto setter = [&](int v) { ++sets; last = v; return 0; };
+    if (m.raise_to(0, &k2, 138000, setter) != 0 || sets != 1 || last != 138000) return 8;
+    if (m.raise_to(0, &k2, 14000, setter) != 0 || sets != 1) return 9;        // smaller: never lowered
+    if (m.raise_to(0, &k2, 138000, setter) != 0 || sets != 1) return 10;      // still covered
+    if (m.raise_to(0, &k2, 150000, setter) != 0 || sets != 2 || last != 150000) return 11;
+    if (m.raise_to(1, &k2, 14000, setter) != 0 || sets != 3) return 12;       // per device
+    auto fail = [&](int) { return 5; };
+    if (m.raise_to(0, &k1, 9000, fail) != 5) return 13;
+    if (m.raise_to(0, &k1, 9000, setter) != 0 || sets != 4) return 14;        // a failed set is retried
+    // no capacity limit: 2000 distinct keys all kept
+    const size_t before = m.size();
+    for (int i = 0; i < 2000; ++i) m.get(3, &k1, i, 0, f(i));
+    if (m.size() != before + 2000) return 15;
+    const int c0 = calls;
+    for (int i = 0; i < 2000; ++i)
+        if (m.get(3, &k1, i, 0, f(-1)) != i) return 16;
+    if (calls != c0) return 17;
     return 0;
 }
 

@@ -556,15 +556,7 @@ __device__ __forceinline__ void hpr_update_pipe(const float* __restrict__ chi_in
         const float* bb = bias + b * NL * 2;
         float out[X];
         float rs = 0.f;
-#ifdef MJX_HPR_NOCOMPUTE
-        // timing build only (tools/ab_lib.py): the pipeline's memory traffic without the DP
-#pragma unroll
-        for (int x = 0; x < X; ++x) out[x] = rb[lane * PIPE_HRS + x] + bb[0];
-        rs = 1.0f;
-        if (false) {
-#else
         if (active) {
-#endif
             static_for<0, NW>([&](auto ww) {
                 constexpr int wv = decltype(ww)::value;
                 if (wave == wv) {

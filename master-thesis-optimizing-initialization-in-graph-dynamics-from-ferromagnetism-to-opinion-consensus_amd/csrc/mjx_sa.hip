@@ -1517,10 +1517,8 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
         if (!__any(going)) break;
         // empty hash sets (16 KB per wave, 16-B stores); lanes then insert into
         // and read slots other lanes wrote: wave-scope fences at each hand-off
-#ifndef MJX_SPEC_NOHASH   // timing builds only (tools/ab_lib.py): the batches without the hash sets
         for (int q = lane; q < (64 / K) * SPEC_HS / 4; q += 64)
             reinterpret_cast<uint4*>(lc_lists + hoff)[q] = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
-#endif
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
         SA_STAMP(5);
@@ -1668,20 +1666,12 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
         SA_STAMP(2);
         // potential writes of every proposal into the replica's hash set
         constexpr int NTW = 1 + D + D * D;                  // tree positions: i, the a_m, their children
-#ifdef MJX_SPEC_NOHASH
-        if (false) {
-#else
         if (mine && listpath) {
-#endif
             hins(i);
 #pragma unroll
             for (int lv = 1; lv <= T; ++lv)
                 for (int q = 0; q < cnt[lv]; ++q) hins((int32_t)(lists[(L.off[lv] + q) * 64] & 0x7fffffffu));
-#ifdef MJX_SPEC_NOHASH
-        } else if (false) {
-#else
         } else if (mine && ok) {
-#endif
             const uint32_t chg = ch1 | ch2;
             int32_t wv[NTW];
             bool wm[NTW];
@@ -1706,11 +1696,7 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
         // does an earlier proposal of the batch write a node this one read?
         // (k > 0 lanes are tree balls: a list-path ball stands only as k = 0)
         bool stands = mine && (ok || listpath);
-#if defined(MJX_SPEC_NOHASH) || defined(MJX_SPEC_NOLOOKUP)
-        if (false) {
-#else
         if (stands && k > 0) {
-#endif
             int32_t rv[NTW];
             bool rm[NTW];
             rv[0] = i;

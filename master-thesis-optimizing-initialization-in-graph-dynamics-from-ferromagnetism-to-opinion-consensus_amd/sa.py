@@ -288,7 +288,20 @@ class SAReplicas:
         out["schedule"] = np.array([self.par_a, self.par_b, self.a0, self.b0, self.a_cap, self.b_cap],
                                    dtype=np.float64)
         out["t_cap"] = np.array(self.t_cap, dtype=np.int64)
+        out["graphs_sha256"] = np.array(self.graphs_digest())
         return out
+
+    def graphs_digest(self):
+        """SHA-256 of the graphs this run reads: the stacked int32 rows and the
+        replica -> graph map (a resumed run must read the same ones)."""
+        import hashlib
+        h = hashlib.sha256()
+        h.update(np.array([self.n, self.d], dtype=np.int64).tobytes())
+        h.update(np.ascontiguousarray(self.adj.cpu().numpy().astype(np.int32)).tobytes())
+        h.update(b"rep_graph" if self.rep_graph is not None else b"shared")
+        if self.rep_graph is not None:
+            h.update(np.ascontiguousarray(self.rep_graph.cpu().numpy().astype(np.int32)).tobytes())
+        return h.hexdigest()
 
     def save_checkpoint(self, path):
         np.savez(path, **self.checkpoint())
@@ -307,6 +320,12 @@ class SAReplicas:
                  tape=tape, layout=layout, graph_of=graph_of, kernel=kernel)
         if (sa.n, sa.d, sa.R) != (n, d, R):
             raise ValueError(f"checkpoint of n={n}, d={d}, R={R} does not fit these graphs (n={sa.n}, d={sa.d})")
+        if "graphs_sha256" in ckpt and str(ckpt["graphs_sha256"]) != sa.graphs_digest():
+            raise ValueError("checkpoint was taken on other graphs (or another replica -> graph map) than these")
+        a_cap, b_cap = (float(x) for x in ckpt["schedule"][4:6])
+        if (a_cap, b_cap) != (sa.a_cap, sa.b_cap) or int(ckpt["t_cap"]) != int(sa.t_cap):
+            raise ValueError(f"checkpoint caps a={a_cap}, b={b_cap}, t={int(ckpt['t_cap'])} differ from "
+                             f"code/SA_RRG.py's for n={n} (a={sa.a_cap}, b={sa.b_cap}, t={sa.t_cap})")
         sa.t_cap = int(ckpt["t_cap"])
         for k in cls._CKPT_STATE:
             dst = getattr(sa, k)

@@ -143,3 +143,41 @@ def test_sa_lds_plan_names_the_kernel_that_runs(mjx_mod):
     assert lib.mjx_sa_lds_plan(10_000, 4, 1, 1, L.MJX_SA_LDS_WAVE, 0, ctypes.byref(th)) == \
         lib.mjx_sa_lds_bytes(10_000, 4, 1, 1) and th.value == 64                    # one wave x 8 proposals
     assert lib.mjx_sa_lds_plan(100_000, 4, 3, 1, 0, 0, ctypes.byref(th)) == -1
+
+
+def test_variant_builds_are_refused_by_the_product_loader(mjx_mod):
+    """A diagnostic / timing variant (tools/ab_lib.py --build, wrong-result
+    patches from tools/variants/) never carries the source hash as its build
+    id, so open_library(path) with verification refuses it."""
+    _lib, _build = mjx_mod._lib, mjx_mod._lib._build
+    vdir = os.path.join(ROOT, "tools", "variants")
+    patches = sorted(os.path.join(vdir, f) for f in os.listdir(vdir) if f.endswith(".patch"))
+    assert patches
+    ids = {_build.variant_id([], ["mjx_sa.hip"]), _build.variant_id(["-DMJX_SA_PROF"], ["mjx_sa_lds.hip"])}
+    ids |= {_build.variant_id([], ["mjx_sa.hip"], [p]) for p in patches}
+    assert len(ids) == 2 + len(patches)
+    assert _build.source_hash() not in ids
+
+    class Fake:
+        def __init__(self, ident):
+            self.ident = ident
+
+        def mjx_build_id(self):
+            return self.ident.encode()
+
+    for ident in ids:
+        with pytest.raises(mjx_mod.MjxError, match="other sources"):
+            _lib.verify_build_id(Fake(ident))
+
+
+def test_product_sources_hold_no_wrong_result_switches():
+    """Timing builds whose results are wrong (the C2 batches without hash sets,
+    the HPR update without its DP) live only as patches in tools/variants/,
+    not as macros in the product sources."""
+    csrc = os.path.join(ROOT, "master-thesis-optimizing-initialization-in-graph-dynamics-from-ferromagnetism-to-"
+                              "opinion-consensus_amd", "csrc")
+    for name in os.listdir(csrc):
+        if name.endswith((".hip", ".h")):
+            text = open(os.path.join(csrc, name)).read()
+            for macro in ("MJX_SPEC_NOHASH", "MJX_SPEC_NOLOOKUP", "MJX_HPR_NOCOMPUTE"):
+                assert macro not in text, (name, macro)

@@ -221,6 +221,54 @@ def _fp64_min_margin(mjx_mod, plan, p, c, TT, tseed):
     return st.t, margin
 
 
+@pytest.mark.parametrize("key,first_tie", [("n30_d3_p2c1", 61), ("n40_d3_p3c1", 61)])
+def test_hpr_exact_tie_runs_equal_oracle_before_the_tie(mjx_mod, key, first_tie):
+    """The whole-script runs whose marginals tie EXACTLY: the
+    device loop, float64 (reference layout) and float32 (hpr_run's default
+    layout), equals the pinned numpy oracle's loop (which reproduces the
+    reference's whole script, tests/test_hpr_oracle.py) in s after every
+    iteration BEFORE the first exact tie.  The oracle's first tie is at
+    iteration ``first_tie`` (recorded here: a change of fixture or oracle shows
+    up); before it the smallest relative margin is >= 0.22, so no rounding
+    order can flip a decision there."""
+    from oracle import hpr as ohpr
+    full = load_golden("hpr_fullscript.npz")
+    n, d, p, c, TT, tseed = (int(x) for x in full[f"{key}_params"])
+    nbrs = full[f"{key}_graphs"][0].astype(np.int64)
+    edges = full[f"{key}_edges"]
+    inr, src = ohpr.incoming_rows(edges, nbrs)
+    ep = ohpr.edges_pos(edges, nbrs)
+    nc = 4 ** (p + c)
+    # the oracle's loop (code/HPR_pytorch_RRG.py:327-356) on torch's CPU stream
+    g = torch.Generator().manual_seed(tseed)
+    chi = torch.rand((2 * len(edges), nc), dtype=torch.float64, generator=g)
+    chi = (chi / chi.sum(1, keepdim=True)).numpy()
+    b = torch.rand((n, 2), dtype=torch.float64, generator=g)
+    b = (b / b.sum(1, keepdim=True)).numpy()
+    want, t0 = [], None
+    for t in range(first_tie + 1):
+        chi = ohpr.HPr_dp(chi, b, inr, src, n, d, p, c, 1, 25 * n, 0.4)
+        marg = ohpr.marginals_comp(chi, ep, p, c)
+        if t0 is None and np.min(np.abs(marg[:, 1] - marg[:, 0])) == 0:
+            t0 = t
+        u = torch.rand(n, dtype=torch.float64, generator=g).numpy()
+        b, s = ohpr.new_biases_i(b, 0.3, 0.1, marg, t, u)
+        want.append(s.copy())
+    assert t0 == first_tie, t0
+    plan = mjx_mod.HPRPlan(edges, n, d, nbrs)
+    for dtype, layout in ((torch.float64, "ref"), (torch.float32, None)):
+        gen = torch.Generator().manual_seed(tseed)
+        chi0 = torch.rand((2 * plan.E, nc), dtype=torch.float64, generator=gen)
+        chi0 = chi0 / torch.sum(chi0, axis=1, keepdims=True)
+        b0 = torch.rand((n, 2), dtype=torch.float64, generator=gen)
+        b0 = b0 / torch.sum(b0, axis=1, keepdims=True)
+        st = mjx_mod.HPRState(plan, p, c, chi0.to(dtype), b0.to(dtype), dtype=dtype, layout=layout)
+        st.s_from_biases()
+        for t in range(first_tie):
+            st.step(generator=gen)
+            assert np.array_equal(st.s.cpu().numpy(), want[t]), (str(dtype), t)
+
+
 def test_hpr_full_script_float32_loop(mjx_mod):
     """fp32 whole loop (hpr_run's default: the decay-split layout where p+c = 4,
     the reference layout otherwise) against the reference's own whole-script

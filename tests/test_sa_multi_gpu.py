@@ -204,6 +204,9 @@ def test_checkpoint_resume_equals_uninterrupted(mjx_mod, tmp_path, d, n, p, c, m
     path = tmp_path / "sa_ckpt.npz"
     run.save_checkpoint(path)
     del run
+    # other graphs of the same shape (or the stack reordered) are refused
+    with pytest.raises(ValueError, match="other graphs"):
+        mjx_mod.SAReplicas.resume(graphs[1:] + graphs[:1], str(path), mode=mode, layout=layout or "auto")
     res = mjx_mod.SAReplicas.resume(graphs, str(path), mode=mode, layout=layout or "auto")
     res.steps(K2)
     for k in ("t", "a", "b", "sum_end", "done"):
