@@ -26,7 +26,7 @@ def main():
     import mjx
     n, R = 10_000_000, 4096
     W = R // 64
-    g = mjx.erdos_renyi_device(n, 5.0 / (n - 1), seed=31)
+    g = mjx.erdos_renyi_device(n, 5.0 / (n - 1), seed=0 + 31)   # bench.py bench_er: seed (0) + 31 on rank 0
     g.class_ell()                    # the bench's degree-class layout (configs[3])
     gen = torch.Generator(device="cuda").manual_seed(0)
     s0 = torch.randint(-2 ** 62, 2 ** 62, (n * W,), dtype=torch.int64, device="cuda", generator=gen)
