@@ -634,19 +634,23 @@ def hpr_dp_flops(d, p, c):
 
 
 def sq_counters(kernel_prefix):
-    """wait / VALU-active fractions of a kernel from the committed SQ counter
-    pass (profiles/r03_sq_counters.json, tools/pmc_sq_parse.py), or None."""
-    path = os.path.join(ROOT, "profiles", "r03_sq_counters.json")
-    try:
-        with open(path) as f:
-            d = json.load(f)
-    except (OSError, ValueError):
-        return None
-    for k, v in d.items():
-        if k.startswith("_") or kernel_prefix not in k:
+    """wait / VALU-active fractions of a kernel from the newest committed SQ
+    counter pass that holds it (profiles/rNN_sq_counters*.json, written by
+    tools/pmc_sq_parse.py from the `sq` step of tools/gpu_check.sh), or None."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_sq_counters*.json")),
+                   key=lambda p: (os.path.basename(p)[:3], os.path.basename(p)), reverse=True)
+    for path in paths:
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
             continue
-        return {"kernel": k, "wait_frac": v.get("wait_frac"), "valu_active_frac": v.get("valu_active_frac"),
-                "source": "profiles/r03_sq_counters.json (a pass before the round-3 no-SLP build)"}
+        for k, v in d.items():
+            if k.startswith("_") or kernel_prefix not in k:
+                continue
+            return {"kernel": k, "wait_frac": v.get("wait_frac"), "valu_active_frac": v.get("valu_active_frac"),
+                    "source": "profiles/" + os.path.basename(path)}
     return None
 
 
@@ -744,13 +748,13 @@ def bench_hpr(args, rank, world, dist, dev):
         "hpr_dp_ms": upd_q, "marginals_ms": marg_q, "hpr_dp_bytes_per_iter": qbytes,
         "hpr_dp_algorithmic_GBps": qbytes / (upd_q / 1e3) / 1e9,
         "hpr_dp_frac_of_hbm_peak": qbytes / (upd_q / 1e3) / 1e9 / HBM_PEAK_GBS,
-        "hpr_dp_traffic_bytes": rocprof_traffic("k_hpr_update_pipe_q"),
+        "hpr_dp_traffic_bytes": rocprof_traffic("k_hpr_update_q2"),
         "marginals_edge_z_traffic_bytes": rocprof_traffic("k_hpr_edge_z_q")}
     # the compute side of the same launch (the DP is a mixed contraction)
     fl = msgs * hpr_dp_flops(d, p, c)
     res["loop_state_q"]["hpr_dp_compute"] = {
         "flops_per_launch": fl, "achieved_tflops": fl / (upd_q / 1e3) / 1e12, "peak_tflops": FP32_VECTOR_PEAK_TFLOPS,
-        "frac": fl / (upd_q / 1e3) / 1e12 / FP32_VECTOR_PEAK_TFLOPS, "sq": sq_counters("k_hpr_update_pipe_q")}
+        "frac": fl / (upd_q / 1e3) / 1e12 / FP32_VECTOR_PEAK_TFLOPS, "sq": sq_counters("k_hpr_update_q2")}
     # the whole loop iteration of code/HPR_pytorch_RRG.py:344-356 (update,
     # marginals, bias refresh, trial configuration, majority check) in
     # hipGraph-replayed batches of 16 with one host read per batch

@@ -22,11 +22,11 @@ int update_q_f32(const void* ci, void* co, const void* b, const int32_t* nb, con
 
 #ifdef MJX_HPR_PROF
 // profiling build only (-DMJX_HPR_PROF): per-phase cycle sums of k_hpr_update
-extern "C" int mjx_hpr_prof_read(unsigned long long* host8, int reset) {
-    if (hipMemcpyFromSymbol(host8, HIP_SYMBOL(mjx::hpr::mjx_hpr_prof), 8 * sizeof(unsigned long long)) != hipSuccess)
+extern "C" int mjx_hpr_prof_read(unsigned long long* host32, int reset) {
+    if (hipMemcpyFromSymbol(host32, HIP_SYMBOL(mjx::hpr::mjx_hpr_prof), 32 * sizeof(unsigned long long)) != hipSuccess)
         return MJX_EHIP;
     if (reset) {
-        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        unsigned long long z[32] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(mjx::hpr::mjx_hpr_prof), z, sizeof(z)) != hipSuccess) return MJX_EHIP;
     }
     return MJX_OK;

@@ -152,8 +152,10 @@ __device__ __forceinline__ int a_local_of(int lane) { return lane / D; }
 // decay-split layout (qpos below) and the buffer holds their VV and IV
 // quadrants, element (x_k valid ? 0 : H^2) + (x_k >> 1) * H + (x_a >> 1), H =
 // 2^(T-1); the IV entries (x_k invalid) are stored undecayed and scaled by sc.
+// BSOA > 0: the biases as two arrays, b(+1) of slot s at s and b(-1) at BSOA + s
+// (else interleaved at 2s, 2s + 1).
 template <typename S, int T, int P, int D, int XA, int RS = Cfg<S, T, P, D>::STRIDE, bool HALF = false,
-          bool QL = false>
+          bool QL = false, int BSOA = 0>
 __device__ __forceinline__ S xa_messages(const S* __restrict__ rows, const S* __restrict__ bias, int a_local, int m,
                                          S w, S (&out)[1 << T], S sc = S(1)) {
     using C = Cfg<S, T, P, D>;
@@ -165,7 +167,7 @@ __device__ __forceinline__ S xa_messages(const S* __restrict__ rows, const S* __
     // the last one after the cumulative sums (short live ranges: VGPRs)
     auto loadM = [&](int j, S (&Mj)[X]) {
         const int slot = a_local * D + (j < m ? j : j + 1);
-        const S bp = bias[2 * slot], bm = bias[2 * slot + 1];
+        const S bp = BSOA ? bias[slot] : bias[2 * slot], bm = BSOA ? bias[BSOA + slot] : bias[2 * slot + 1];
         if constexpr (QL) {
             constexpr int H = X / 2;
             const S* r = rows + slot * RS + (XA >> 1);
@@ -254,7 +256,9 @@ __device__ __forceinline__ S xa_messages(const S* __restrict__ rows, const S* __
 }
 
 #ifdef MJX_HPR_PROF
-__device__ unsigned long long mjx_hpr_prof[8];
+// [0..3] k_hpr_update phases; [4..9] hpr_update_pipe phases (issue, compute,
+// vmcnt wait, barrier 1, epilogue, barrier 2); [10..17] pipe compute per wave
+__device__ unsigned long long mjx_hpr_prof[32];
 #define MJX_PROF_MARK(k) do { const unsigned long long _c = clock64(); if ((threadIdx.x & 63) == 0) atomicAdd(&mjx_hpr_prof[k], _c - _t0); _t0 = _c; } while (0)
 #else
 #define MJX_PROF_MARK(k) do {} while (0)
@@ -401,8 +405,12 @@ __host__ __device__ constexpr int qpos(int xs, int xr, int T, int pv) {
 //     (i+1)&1 with a 129-float row stride (conflict-free M reads);
 //   * the old rows of tile i (damping), whole (global_load_lds_dwordx4, one
 //     row per wave instruction), at a 260-float stride (conflict-free
-//     16-B epilogue reads).
-// Row indices (wave-uniform, scalar loads) and biases are fetched one tile ahead.
+//     16-B epilogue reads);
+//   * the index rows (in_row, out_row, nbr) of tile i+2 and the sources'
+//     biases of tile i+1, read back from LDS (round 5: scalar index loads
+//     share lgkmcnt with the DP's LDS reads and held up its first one, and a
+//     per-lane out_row load made the loop latch wait for the epilogue's
+//     stores; see hpr_update_q2 below, the decay-split form).
 constexpr int PIPE_HRS = 129;       // half-row stride (floats) of the incoming-row buffers
 constexpr int PIPE_ORS = 260;       // old-row stride (floats): 1040 B, 16-B aligned DMA bases
 
@@ -411,9 +419,9 @@ struct PipeCfg {
     using C = Cfg<float, T, P, D>;
     static constexpr int NW = 8, NL = C::NL, NT = C::NT;
     static constexpr int RPW = (NL + NW - 1) / NW;            // rows per wave per tile
-    static constexpr size_t BUF = (size_t)NL * PIPE_HRS;       // floats per incoming buffer
-    static constexpr size_t OLD = (size_t)NL * PIPE_ORS;       // floats of the old-row buffer
-    static constexpr size_t LDS = (2 * BUF + OLD + 2 * (size_t)NL * 2 + (size_t)NW * 64) * sizeof(float);
+    static constexpr size_t BUF = (size_t)64 * PIPE_HRS;       // floats per incoming buffer
+    static constexpr size_t OLD = (size_t)64 * PIPE_ORS;       // floats of the old-row buffer
+    static constexpr size_t LDS = (2 * BUF + OLD + 2 * 128 + 3 * 192 + (size_t)NW * 64) * sizeof(float);
 };
 
 __device__ __forceinline__ void glds16(const float* gsrc, uint32_t lds_byte_addr) {
@@ -434,26 +442,71 @@ __device__ __forceinline__ void glds4(const float* gsrc, uint32_t lds_byte_addr)
                  : "memory");
 }
 
-template <int T, int P, int D, bool QL>
+// The tile-index plumbing both pipelined updates share: the three index rows
+// of a tile by LDS-DMA (wave 0), this wave's rows read back by LDS broadcast,
+// the sources' biases by LDS-DMA from per-lane addresses (wave 1).  A slot past
+// the tile, or a tile past the end, reads entry 0 (row 0, node 0): the DMA
+// counts stay fixed.
+template <int NT, int D, int RPW>
+struct TileIdx {
+    const int32_t* in_row;
+    const int32_t* out_row;
+    const int32_t* nbr;
+    const float* biases;
+    int32_t* idxb;                  // [3][3][64]: in_row, out_row, nbr per slot
+    uint32_t idx_lds, bias_lds;     // bias: [2][2][64] b(+1) then b(-1) per lane
+    int64_t n, ntiles;
+    int wave, lane;
+    __device__ int tile_nl(int64_t t) const {
+        if (t >= ntiles) return 0;
+        const int64_t a0 = t * NT;
+        return (int)((n - a0) < NT ? (n - a0) : NT) * D;
+    }
+    __device__ void dma_idx(int64_t t, int s3) const {             // wave 0: 3
+        const int nl = tile_nl(t);
+        const int64_t e = lane < nl ? t * NT * D + lane : 0;
+        const uint32_t base = idx_lds + (uint32_t)(s3 * 192 * sizeof(int32_t));
+        glds4(reinterpret_cast<const float*>(in_row + e), base);
+        glds4(reinterpret_cast<const float*>(out_row + e), base + 64 * sizeof(int32_t));
+        glds4(reinterpret_cast<const float*>(nbr + e), base + 128 * sizeof(int32_t));
+    }
+    __device__ void rows_of(int s3, int which, int32_t (&r)[RPW]) const {
+        const int32_t* src = idxb + s3 * 192 + which * 64 + wave * RPW;
+#pragma unroll
+        for (int k = 0; k < RPW; ++k) r[k] = src[k];
+    }
+    __device__ void dma_bias(int s3, int s) const {                // wave 1: 2
+        const int32_t nb = idxb[s3 * 192 + 128 + lane];
+        const float* src = biases + 2 * (int64_t)nb;
+        glds4(src, bias_lds + (uint32_t)((s * 128) * sizeof(float)));
+        glds4(src + 1, bias_lds + (uint32_t)((s * 128 + 64) * sizeof(float)));
+    }
+    __device__ int32_t orow(int s3) const { return idxb[s3 * 192 + 64 + lane]; }
+};
+
+template <int T, int P, int D>
 __device__ __forceinline__ void hpr_update_pipe(const float* __restrict__ chi_in, float* __restrict__ chi_out,
                                                 const float* __restrict__ biases, const int32_t* __restrict__ nbr,
                                                 const int32_t* __restrict__ in_row,
                                                 const int32_t* __restrict__ out_row, int64_t n, int attr_plus,
-                                                float w_plus, float w_minus, float damp, float sc) {
+                                                float w_plus, float w_minus, float damp) {
     using PC = PipeCfg<T, P, D>;
     constexpr int X = 1 << T, NC = X * X, NT = PC::NT, NL = PC::NL, NW = PC::NW, RPW = PC::RPW;
-    static_assert(NC == 256, "pipelined HPR update: 1 KB rows (T = 4, fp32)");
+    static_assert(NC == 256 && RPW == 8 && NL <= 64, "pipelined HPR update: 1 KB rows (T = 4, fp32), 64-lane tiles");
     static_assert(Cfg<float, T, P, D>::NVALID == NW, "one valid x_a per wave");
     extern __shared__ __align__(16) unsigned char smem[];
-    float* rows = reinterpret_cast<float*>(smem);                 // [2][NL][PIPE_HRS] valid halves
-    float* oldb = rows + 2 * PC::BUF;                             // [NL][PIPE_ORS] old rows
-    float* bias = oldb + PC::OLD;                                 // [2][NL][2]
-    float* red = bias + 2 * NL * 2;                               // [NW][64]
+    float* rows = reinterpret_cast<float*>(smem);                 // [2][64][PIPE_HRS] valid halves
+    float* oldb = rows + 2 * PC::BUF;                             // [64][PIPE_ORS] old rows
+    float* bias = oldb + PC::OLD;                                 // [2][2][64]
+    int32_t* idxb = reinterpret_cast<int32_t*>(bias + 2 * 128);   // [3][3][64]
+    float* red = reinterpret_cast<float*>(idxb + 3 * 192);        // [NW][64]
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int64_t ntiles = (n + NT - 1) / NT;
     const uint32_t rows_lds = (uint32_t)(uintptr_t)rows;
     const uint32_t old_lds = (uint32_t)(uintptr_t)oldb;
+    const TileIdx<NT, D, RPW> ti{in_row, out_row, nbr, biases, idxb, (uint32_t)(uintptr_t)idxb,
+                                 (uint32_t)(uintptr_t)bias, n, ntiles, wave, lane};
     const float keep = 1.0f - damp;
     const int q = wave;                                           // valid x_a index
     const int cv = (attr_plus ? 2 * q : 2 * q + 1) * X;           // valid block of every row
@@ -461,99 +514,57 @@ __device__ __forceinline__ void hpr_update_pipe(const float* __restrict__ chi_in
     // column of half-row element h = x_k * 8 + (x_a >> 1)
     const int hcol0 = (lane >> 3) * X + 2 * (lane & 7) + (attr_plus ? 0 : 1);
 
-    auto tile_nl = [&](int64_t t) -> int {
-        const int64_t a0 = t * NT;
-        return (int)((n - a0) < NT ? (n - a0) : NT) * D;
-    };
-    // wave-uniform row indices of this wave's slots wave*RPW + k of tile t (-1: none)
-    auto load_idx = [&](const int32_t* __restrict__ arr, int64_t t, int32_t (&ri)[RPW]) {
-        const int nl = t < ntiles ? tile_nl(t) : 0;
+    auto dma_in = [&](const int32_t (&ri)[RPW], int b) {           // valid halves -> buffer b: 2 * RPW
 #pragma unroll
         for (int k = 0; k < RPW; ++k) {
             const int slot = wave * RPW + k;
-            ri[k] = slot < nl ? __builtin_amdgcn_readfirstlane(arr[t * NT * D + slot]) : -1;
+            const uint32_t dst = rows_lds + (uint32_t)((b * PC::BUF + (size_t)slot * PIPE_HRS) * sizeof(float));
+            const float* src = chi_in + (int64_t)ri[k] * NC + hcol0;
+            glds4(src, dst);                                   // x_k 0..7
+            glds4(src + 8 * X, dst + 64 * sizeof(float));     // x_k 8..15
         }
     };
-    auto dma_in = [&](const int32_t (&ri)[RPW], int b) {           // valid halves -> buffer b
+    auto dma_old = [&](const int32_t (&ro)[RPW]) {                // whole old rows: RPW
 #pragma unroll
         for (int k = 0; k < RPW; ++k) {
-            if (ri[k] >= 0) {
-                const int slot = wave * RPW + k;
-                const uint32_t dst = rows_lds + (uint32_t)((b * PC::BUF + (size_t)slot * PIPE_HRS) * sizeof(float));
-                if (QL) {                                          // VV, IV quadrants: two 256-B runs
-                    const float* src = chi_in + (int64_t)ri[k] * NC + lane;
-                    glds4(src, dst);
-                    glds4(src + NC / 2, dst + 64 * sizeof(float));
-                } else {
-                    const float* src = chi_in + (int64_t)ri[k] * NC + hcol0;
-                    glds4(src, dst);                                   // x_k 0..7
-                    glds4(src + 8 * X, dst + 64 * sizeof(float));     // x_k 8..15
-                }
-            }
+            const int slot = wave * RPW + k;
+            glds16(chi_in + (int64_t)ro[k] * NC + lane * 4,
+                   old_lds + (uint32_t)((size_t)slot * PIPE_ORS * sizeof(float)));
         }
-    };
-    auto dma_old = [&](const int32_t (&ro)[RPW]) {                // whole old rows
-#pragma unroll
-        for (int k = 0; k < RPW; ++k) {
-            if (ro[k] >= 0 && (!QL || lane < 32)) {                // QL: the first half only
-                const int slot = wave * RPW + k;
-                glds16(chi_in + (int64_t)ro[k] * NC + lane * 4,
-                       old_lds + (uint32_t)((size_t)slot * PIPE_ORS * sizeof(float)));
-            }
-        }
-    };
-    // per-lane: source node of slot `lane` (its biases), own out row (the store)
-    auto load_lane = [&](const int32_t* __restrict__ arr, int64_t t) -> int32_t {
-        const int nl = t < ntiles ? tile_nl(t) : 0;
-        return lane < nl ? arr[t * NT * D + lane] : -1;
     };
 
     int64_t t = blockIdx.x;
     if (t >= ntiles) return;
     const int64_t G = gridDim.x;
-    // ---- prologue: tile t's rows and biases staged, the next tile's indices in hand
-    int32_t ri[RPW], ro[RPW];
-    load_idx(in_row, t, ri);
-    dma_in(ri, 0);
-    load_idx(in_row, t + G, ri);
-    load_idx(out_row, t, ro);
-    {
-        const int32_t nb = load_lane(nbr, t);
-        float bp = 0.f, bm = 0.f;
-        if (nb >= 0) {
-            bp = biases[2 * (int64_t)nb];
-            bm = biases[2 * (int64_t)nb + 1];
-        }
-        if (wave == 0 && lane < NL) {
-            bias[2 * lane] = bp;
-            bias[2 * lane + 1] = bm;
-        }
+    int32_t r[RPW];
+    // ---- prologue: the indices of tiles t and t+G, tile t's rows and biases
+    if (wave == 0) {
+        ti.dma_idx(t, 0);
+        ti.dma_idx(t + G, 1);
     }
-    int32_t nb_next = load_lane(nbr, t + G);
-    int32_t orow = load_lane(out_row, t);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    ti.rows_of(0, 0, r);
+    dma_in(r, 0);
+    if (wave == 1) ti.dma_bias(0, 0);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
 
     for (int it = 0; t < ntiles; ++it, t += G) {
-        const int b = it & 1;
-        const int nl = tile_nl(t);
+        const int b = it & 1, s3 = it % 3, s3n = (it + 1) % 3;
+        const int nl = ti.tile_nl(t);
         const bool active = lane < nl;
-        // ---- stage 1 (all DMA): next tile's valid halves, this tile's old rows;
-        // next indices and biases into registers
-        dma_in(ri, 1 - b);
-        dma_old(ro);
-        load_idx(in_row, t + 2 * G, ri);
-        load_idx(out_row, t + G, ro);
-        float nbp = 0.f, nbm = 0.f;
-        if (nb_next >= 0) {
-            nbp = biases[2 * (int64_t)nb_next];
-            nbm = biases[2 * (int64_t)nb_next + 1];
-        }
-        nb_next = load_lane(nbr, t + 2 * G);
-        const int32_t orow_next = load_lane(out_row, t + G);
+        // ---- stage 1 (all DMA): next tile's valid halves, indices and biases,
+        // this tile's old rows
+        ti.rows_of(s3n, 0, r);
+        dma_in(r, 1 - b);
+        if (wave == 0) ti.dma_idx(t + 2 * G, (it + 2) % 3);
+        if (wave == 1) ti.dma_bias(s3n, 1 - b);
+        ti.rows_of(s3, 1, r);
+        dma_old(r);
         // ---- stage 2: compute from buffer b
         const float* rb = rows + b * PC::BUF;
-        const float* bb = bias + b * NL * 2;
+        const float* bb = bias + b * 128;
         float out[X];
         float rs = 0.f;
         if (active) {
@@ -562,15 +573,15 @@ __device__ __forceinline__ void hpr_update_pipe(const float* __restrict__ chi_in
                 if (wave == wv) {
                     constexpr int XP = 2 * wv, XM = 2 * wv + 1;
                     const float wgt0 = (XP < X / 2) ? w_plus : w_minus;
-                    if (attr_plus) rs = xa_messages<float, T, P, D, XP, PIPE_HRS, true, QL>(
-                                         rb, bb, a_local_of<D>(lane), lane % D, wgt0, out, sc);
-                    else rs = xa_messages<float, T, P, D, XM, PIPE_HRS, true, QL>(
-                                   rb, bb, a_local_of<D>(lane), lane % D, wgt0, out, sc);
+                    if (attr_plus) rs = xa_messages<float, T, P, D, XP, PIPE_HRS, true, false, 64>(
+                                         rb, bb, a_local_of<D>(lane), lane % D, wgt0, out);
+                    else rs = xa_messages<float, T, P, D, XM, PIPE_HRS, true, false, 64>(
+                                   rb, bb, a_local_of<D>(lane), lane % D, wgt0, out);
                 }
             });
         }
         red[wave * 64 + lane] = rs;
-        // every DMA of this wave landed (next halves, old rows), LDS writes done
+        // every DMA of this wave landed (next halves, indices, biases, old rows)
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         // ---- stage 3: normalise, damp, store (code/HPR_pytorch_RRG.py:215)
@@ -580,34 +591,7 @@ __device__ __forceinline__ void hpr_update_pipe(const float* __restrict__ chi_in
             for (int w = 0; w < NW; ++w) tot += red[w * 64 + lane];
             const float inv = 1.0f / tot;
             const float* ol = oldb + lane * PIPE_ORS;
-            float* dst = chi_out + (int64_t)orow * NC;
-            if (QL) {
-                // row entries (x_a = this wave's valid sender, x_b): VV at q*8 + (x_b>>1)
-                // for valid x_b, VI at 64 + q*8 + (x_b>>1) for the others
-                constexpr int H = X / 2;
-#pragma unroll
-                for (int half = 0; half < 2; ++half) {
-                    const int base = half * H * H + q * H;
-#pragma unroll
-                    for (int k = 0; k < H / 4; ++k) {
-                        const float4 ov = *reinterpret_cast<const float4*>(ol + base + 4 * k);
-                        float o[4];
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) {
-                            const int j = 4 * k + e;                        // x_b >> 1
-                            // x_b = 2j + (valid ? pv : 1 - pv), pv = attr_plus ? 0 : 1
-                            const bool odd = (half == 0) != (attr_plus != 0);
-                            o[e] = odd ? out[2 * j + 1] : out[2 * j];
-                        }
-                        float4 v;
-                        v.x = damp * (o[0] * inv) + keep * ov.x;
-                        v.y = damp * (o[1] * inv) + keep * ov.y;
-                        v.z = damp * (o[2] * inv) + keep * ov.z;
-                        v.w = damp * (o[3] * inv) + keep * ov.w;
-                        *reinterpret_cast<float4*>(dst + base + 4 * k) = v;
-                    }
-                }
-            } else {
+            float* dst = chi_out + (int64_t)ti.orow(s3) * NC;
 #pragma unroll
             for (int k = 0; k < X / 4; ++k) {
                 const float4 ov = *reinterpret_cast<const float4*>(ol + cv + 4 * k);
@@ -624,14 +608,8 @@ __device__ __forceinline__ void hpr_update_pipe(const float* __restrict__ chi_in
                 *reinterpret_cast<float4*>(dst + cv + 4 * k) = v;
                 *reinterpret_cast<float4*>(dst + ci + 4 * k) = z;
             }
-            }
         }
-        if (wave == 0 && lane < NL) {              // next tile's biases (buffer 1-b)
-            bias[(1 - b) * NL * 2 + 2 * lane] = nbp;
-            bias[(1 - b) * NL * 2 + 2 * lane + 1] = nbm;
-        }
-        orow = orow_next;
-        // old-row buffer and buffer b free, next biases written
+        // old-row buffer and buffer b free
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
     }
@@ -644,22 +622,238 @@ __global__ void __launch_bounds__(512) k_hpr_update_pipe(const float* __restrict
                                                           const int32_t* __restrict__ in_row,
                                                           const int32_t* __restrict__ out_row, int64_t n,
                                                           int attr_plus, float w_plus, float w_minus, float damp) {
-    hpr_update_pipe<T, P, D, false>(chi_in, chi_out, biases, nbr, in_row, out_row, n, attr_plus, w_plus, w_minus,
-                                    damp, 1.0f);
+    hpr_update_pipe<T, P, D>(chi_in, chi_out, biases, nbr, in_row, out_row, n, attr_plus, w_plus, w_minus, damp);
+}
+
+// Which valid x_a each wave of the 8-wave update takes.  A wave's DP costs a
+// fixed convolution plus one FMA per non-empty corner (x, x_b) of its x_a,
+// and the corner counts differ by up to 3x between x_a (d=4, p=c=2, attr +1:
+// 256, 108, 144, 108, 192, 81, 192, 144).  Waves w and w+4 share a SIMD, so
+// x_a is dealt heaviest-with-lightest: wave s the s-th heaviest, wave s+4 the
+// s-th lightest (measured per-wave DP at C3 before: 4.4k/5.5k cycles on SIMD 0
+// against 2.5k/3.0k on SIMD 1).
+template <int T, int P, int D, int XA>
+constexpr int xa_corners() {
+    int c = 0;
+    for (int x = 0; x < (1 << T); ++x)
+        for (int xb = 0; xb < (1 << T); ++xb) c += Tabs<T, P, D, XA>::v.cn[x][xb] >= 0 ? 1 : 0;
+    return c;
+}
+template <int T, int P, int D, int PV>
+struct XaDeal {
+    static constexpr int NW = 8;
+    struct M { int q[NW]; };
+    template <int... Q>
+    static constexpr M make(std::integer_sequence<int, Q...>) {
+        const int cost[NW] = {xa_corners<T, P, D, 2 * Q + PV>()...};
+        int ord[NW] = {0, 1, 2, 3, 4, 5, 6, 7};
+        for (int i = 0; i < NW; ++i)                         // by cost, heaviest first (stable)
+            for (int j = i + 1; j < NW; ++j)
+                if (cost[ord[j]] > cost[ord[i]]) { const int tmp = ord[i]; ord[i] = ord[j]; ord[j] = tmp; }
+        M m{};
+        for (int s = 0; s < NW / 2; ++s) {
+            m.q[s] = ord[s];
+            m.q[s + NW / 2] = ord[NW - 1 - s];
+        }
+        return m;
+    }
+    static constexpr M v = make(std::make_integer_sequence<int, NW>{});
+};
+
+constexpr int PIPE_QORS = 132;      // old half-row stride (floats): 528 B, 16-B aligned DMA bases
+
+template <int T, int P, int D>
+struct PipeQCfg {
+    using C = Cfg<float, T, P, D>;
+    static constexpr int NW = 8, NL = C::NL, NT = C::NT;
+    static constexpr int RPW = (NL + NW - 1) / NW;
+    static constexpr size_t IN = (size_t)64 * PIPE_HRS;         // floats per incoming slot
+    static constexpr size_t OLD = (size_t)64 * PIPE_QORS;       // floats per old-row slot
+    static constexpr size_t LDS = (2 * IN + 2 * OLD + 2 * 128 + 3 * 192 + (size_t)NW * 64) * sizeof(float);
+    static constexpr int N_A = 2 * RPW + RPW;                   // DMA per wave in A (+3 on wave 0, +2 on wave 1)
+};
+
+template <int T, int P, int D>
+__device__ __forceinline__ void hpr_update_q2(const float* __restrict__ chi_in, float* __restrict__ chi_out,
+                                              const float* __restrict__ biases, const int32_t* __restrict__ nbr,
+                                              const int32_t* __restrict__ in_row, const int32_t* __restrict__ out_row,
+                                              int64_t n, int attr_plus, float w_plus, float w_minus, float damp,
+                                              float sc) {
+    using PC = PipeQCfg<T, P, D>;
+    constexpr int X = 1 << T, NC = X * X, H = X / 2, NT = PC::NT, NL = PC::NL, NW = PC::NW, RPW = PC::RPW;
+    static_assert(NC == 256 && RPW == 8 && NL <= 64, "decay-split update: 1 KB rows (T = 4, fp32), 64-lane tiles");
+    static_assert(Cfg<float, T, P, D>::NVALID == NW, "one valid x_a per wave");
+    extern __shared__ __align__(16) unsigned char smem[];
+    float* inb = reinterpret_cast<float*>(smem);                  // [2][64][PIPE_HRS] VV | IV halves
+    float* oldb = inb + 2 * PC::IN;                               // [2][64][PIPE_QORS] first half rows
+    float* biasb = oldb + 2 * PC::OLD;                            // [2][2][64]: b(+1) then b(-1) per lane
+    int32_t* idxb = reinterpret_cast<int32_t*>(biasb + 2 * 128);  // [3][3][64]: in_row, out_row, nbr per slot
+    float* red = reinterpret_cast<float*>(idxb + 3 * 192);        // [NW][64]
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int64_t ntiles = (n + NT - 1) / NT;
+    const uint32_t in_lds = (uint32_t)(uintptr_t)inb, old_lds = (uint32_t)(uintptr_t)oldb;
+    const TileIdx<NT, D, RPW> ti{in_row, out_row, nbr, biases, idxb, (uint32_t)(uintptr_t)idxb,
+                                 (uint32_t)(uintptr_t)biasb, n, ntiles, wave, lane};
+    const float keep = 1.0f - damp;
+    // valid x_a index of this wave (dealt by DP cost, see XaDeal)
+    const int q = attr_plus ? XaDeal<T, P, D, 0>::v.q[wave] : XaDeal<T, P, D, 1>::v.q[wave];
+
+    auto dma_in = [&](const int32_t (&r)[RPW], int s) {           // 2 * RPW
+#pragma unroll
+        for (int k = 0; k < RPW; ++k) {
+            const int slot = wave * RPW + k;
+            const uint32_t dst = in_lds + (uint32_t)((s * PC::IN + (size_t)slot * PIPE_HRS) * sizeof(float));
+            const float* src = chi_in + (int64_t)r[k] * NC + lane;
+            glds4(src, dst);
+            glds4(src + NC / 2, dst + 64 * sizeof(float));
+        }
+    };
+    auto dma_old = [&](const int32_t (&r)[RPW], int s) {          // RPW (lanes 0..31: 512 B)
+#pragma unroll
+        for (int k = 0; k < RPW; ++k) {
+            const int slot = wave * RPW + k;
+            // the M0 base computed outside the lane branch (an SGPR operand)
+            const uint32_t dst = __builtin_amdgcn_readfirstlane(
+                old_lds + (uint32_t)((s * PC::OLD + (size_t)slot * PIPE_QORS) * sizeof(float)));
+            if (lane < 32) glds16(chi_in + (int64_t)r[k] * NC + lane * 4, dst);
+        }
+    };
+
+    int64_t t = blockIdx.x;
+    if (t >= ntiles) return;
+    const int64_t G = gridDim.x;
+    int32_t r[RPW];
+    // ---- prologue: indices of tiles t and t+G; tile t's rows, biases and old rows
+    if (wave == 0) {
+        ti.dma_idx(t, 0);
+        ti.dma_idx(t + G, 1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    ti.rows_of(0, 0, r);
+    dma_in(r, 0);
+    if (wave == 1) ti.dma_bias(0, 0);
+    ti.rows_of(0, 1, r);
+    dma_old(r, 0);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+#ifdef MJX_HPR_PROF
+    unsigned long long _ph[6] = {0, 0, 0, 0, 0, 0}, _tp = __builtin_amdgcn_s_memtime();
+#define PIPE_STAMP(k) do { const unsigned long long _c = __builtin_amdgcn_s_memtime(); _ph[k] += _c - _tp; _tp = _c; } while (0)
+#else
+#define PIPE_STAMP(k) do {} while (0)
+#endif
+
+    for (int it = 0; t < ntiles; ++it, t += G) {
+        const int b = it & 1, s3 = it % 3, s3n = (it + 1) % 3;
+        const int nl = ti.tile_nl(t);
+        const bool active = lane < nl;
+        // ---- A: everything tile t+G reads; the indices of tile t+2G
+        ti.rows_of(s3n, 0, r);
+        dma_in(r, 1 - b);
+        if (wave == 0) ti.dma_idx(t + 2 * G, (it + 2) % 3);
+        if (wave == 1) ti.dma_bias(s3n, 1 - b);
+        ti.rows_of(s3n, 1, r);
+        dma_old(r, 1 - b);
+        PIPE_STAMP(0);
+        // ---- B: DP of tile t
+        const float* rb = inb + b * PC::IN;
+        const float* bb = biasb + b * 128;
+        float out[X];
+        float rs = 0.f;
+        if (active) {
+            static_for<0, NW>([&](auto ww) {
+                constexpr int wv = decltype(ww)::value;
+                if (wave == wv) {
+                    constexpr int XP = 2 * XaDeal<T, P, D, 0>::v.q[wv], XM = 2 * XaDeal<T, P, D, 1>::v.q[wv] + 1;
+                    if (attr_plus) rs = xa_messages<float, T, P, D, XP, PIPE_HRS, true, true, 64>(
+                                         rb, bb, a_local_of<D>(lane), lane % D, (XP < X / 2) ? w_plus : w_minus,
+                                         out, sc);
+                    else rs = xa_messages<float, T, P, D, XM, PIPE_HRS, true, true, 64>(
+                                   rb, bb, a_local_of<D>(lane), lane % D, (XM < X / 2) ? w_plus : w_minus, out, sc);
+                }
+            });
+        }
+        red[wave * 64 + lane] = rs;
+        PIPE_STAMP(1);
+        // ---- C: old rows of tile t retired (all but this iteration's A)
+        if (wave == 0) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(PC::N_A + 3) : "memory");
+        else if (wave == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(PC::N_A + 2) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(PC::N_A) : "memory");
+        PIPE_STAMP(2);
+        __builtin_amdgcn_s_barrier();
+        PIPE_STAMP(3);
+        // ---- E: normalise, damp (code/HPR_pytorch_RRG.py:215), store the first half row
+        float4 v[H / 2];
+        int32_t orow = 0;
+        if (active) {
+            float tot = 0.f;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) tot += red[w * 64 + lane];
+            const float inv = 1.0f / tot;
+            const float* ol = oldb + b * PC::OLD + lane * PIPE_QORS;
+            orow = ti.orow(s3);
+            // entries (x_a = this wave's valid sender, x_b): VV at q*H + (x_b>>1) for
+            // valid x_b, VI at H*H + q*H + (x_b>>1) for the others
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+                const int base = half * H * H + q * H;
+#pragma unroll
+                for (int k = 0; k < H / 4; ++k) {
+                    const float4 ov = *reinterpret_cast<const float4*>(ol + base + 4 * k);
+                    float o[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int j = 4 * k + e;                        // x_b >> 1
+                        const bool odd = (half == 0) != (attr_plus != 0);
+                        o[e] = odd ? out[2 * j + 1] : out[2 * j];
+                    }
+                    float4 rr;
+                    rr.x = damp * (o[0] * inv) + keep * ov.x;
+                    rr.y = damp * (o[1] * inv) + keep * ov.y;
+                    rr.z = damp * (o[2] * inv) + keep * ov.z;
+                    rr.w = damp * (o[3] * inv) + keep * ov.w;
+                    v[half * (H / 4) + k] = rr;
+                }
+            }
+        }
+        // tile t+G's incoming rows, biases and tile t+2G's indices retired
+        // (tile t+G's old rows may fly on)
+        asm volatile("s_waitcnt vmcnt(%0)" :: "n"(RPW) : "memory");
+        if (active) {
+            float* dst = chi_out + (int64_t)orow * NC;
+#pragma unroll
+            for (int half = 0; half < 2; ++half)
+#pragma unroll
+                for (int k = 0; k < H / 4; ++k)
+                    *reinterpret_cast<float4*>(dst + half * H * H + q * H + 4 * k) = v[half * (H / 4) + k];
+        }
+        PIPE_STAMP(4);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        PIPE_STAMP(5);
+    }
+#ifdef MJX_HPR_PROF
+    if (lane == 0) {
+        for (int k = 0; k < 6; ++k) atomicAdd(&mjx_hpr_prof[4 + k], _ph[k]);
+        atomicAdd(&mjx_hpr_prof[10 + wave], _ph[1]);
+    }
+#endif
+#undef PIPE_STAMP
 }
 
 // the decay-split layout; scale_in = decay of chi_in's IV quadrants
 template <int T, int P, int D>
-__global__ void __launch_bounds__(512) k_hpr_update_pipe_q(const float* __restrict__ chi_in,
-                                                            float* __restrict__ chi_out,
-                                                            const float* __restrict__ biases,
-                                                            const int32_t* __restrict__ nbr,
-                                                            const int32_t* __restrict__ in_row,
-                                                            const int32_t* __restrict__ out_row, int64_t n,
-                                                            int attr_plus, float w_plus, float w_minus, float damp,
-                                                            const float* __restrict__ scale_in) {
-    hpr_update_pipe<T, P, D, true>(chi_in, chi_out, biases, nbr, in_row, out_row, n, attr_plus, w_plus, w_minus,
-                                   damp, *scale_in);
+__global__ void __launch_bounds__(512) k_hpr_update_q2(const float* __restrict__ chi_in, float* __restrict__ chi_out,
+                                                        const float* __restrict__ biases,
+                                                        const int32_t* __restrict__ nbr,
+                                                        const int32_t* __restrict__ in_row,
+                                                        const int32_t* __restrict__ out_row, int64_t n, int attr_plus,
+                                                        float w_plus, float w_minus, float damp,
+                                                        const float* __restrict__ scale_in) {
+    hpr_update_q2<T, P, D>(chi_in, chi_out, biases, nbr, in_row, out_row, n, attr_plus, w_plus, w_minus, damp,
+                           *scale_in);
 }
 
 // ---- marginals (code/HPR_pytorch_RRG.py:147-167) ---------------------------
@@ -1002,15 +1196,17 @@ static int launch_update_q(const void* chi_in, void* chi_out, const void* biases
     } else {
         const int64_t tiles = (n + C::NT - 1) / C::NT;
         if (tiles > INT32_MAX) return MJX_ERANGE;
-        auto pk = k_hpr_update_pipe_q<T, P, D>;
-        MJX_HIP(set_max_lds(pk, (int)PC::LDS), "hpr pipe q set lds");
-        const int per = resident_blocks_per_cu((const void*)pk, 512, PC::LDS);
+        using PQ = PipeQCfg<T, P, D>;
+        static_assert(PQ::LDS <= 160 * 1024, "decay-split update LDS");
+        auto pk = k_hpr_update_q2<T, P, D>;
+        MJX_HIP(set_max_lds(pk, (int)PQ::LDS), "hpr update q set lds");
+        const int per = resident_blocks_per_cu((const void*)pk, 512, PQ::LDS);
         int64_t grid = (int64_t)device_cus() * (per > 0 ? per : 1);
         if (grid > tiles) grid = tiles;
-        pk<<<(unsigned)grid, 512, PC::LDS, st>>>((const float*)chi_in, (float*)chi_out, (const float*)biases, nbr,
+        pk<<<(unsigned)grid, 512, PQ::LDS, st>>>((const float*)chi_in, (float*)chi_out, (const float*)biases, nbr,
                                                  in_row, out_row, n, attr_plus, (float)w_plus, (float)w_minus,
                                                  (float)damp, scale_in);
-        MJX_LAUNCH_CHECK("k_hpr_update_pipe<q>");
+        MJX_LAUNCH_CHECK("k_hpr_update_q2");
         return MJX_OK;
     }
 }

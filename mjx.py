@@ -14,3 +14,9 @@ _spec = _ilu.spec_from_file_location("mjx", _os.path.join(PKG_DIR, "__init__.py"
 _mod = _ilu.module_from_spec(_spec)
 _sys.modules["mjx"] = _mod
 _spec.loader.exec_module(_mod)
+
+if __name__ == "__main__":
+    # python -m mjx sa|hpr|bdcm ...: the reference's experiments with its
+    # constants as flags (package module cli.py)
+    import importlib as _il
+    _il.import_module("mjx.cli").main(_sys.argv[1:])

@@ -17,7 +17,7 @@ chi /= chi.sum(1, keepdim=True)
 b = torch.rand((n, 2), dtype=torch.float32, device="cuda")
 b /= b.sum(1, keepdim=True)
 out = torch.empty_like(chi)
-buf = (ctypes.c_ulonglong * 8)()
+buf = (ctypes.c_ulonglong * 32)()
 for _ in range(3):
     mjx.HPr_dp(chi, b, plan, p, c, 1, 25 * n, 0.4, out=out)
 torch.cuda.synchronize()
