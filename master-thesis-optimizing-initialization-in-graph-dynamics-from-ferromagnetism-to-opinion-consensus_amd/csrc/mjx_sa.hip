@@ -1512,6 +1512,22 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
 #ifdef MJX_SA_PROF
     unsigned long long _acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, _t0 = __builtin_amdgcn_s_memtime();
 #endif
+    // The proposal tape and the adjacency do not depend on accept decisions, so
+    // the next batch's proposals (pos + K + k: every proposal of this batch
+    // consumed, the usual case) and the rows of their balls are fetched while
+    // this batch evaluates and resolves: the tape entry at its start, the row of
+    // i after the evaluation, the rows of i's neighbours after the hash phase.
+    // A batch that consumed fewer than K (a conflict, a non-tree ball, a stop)
+    // fetches its own afresh.  Three dependent round trips per batch fewer.
+    int64_t pf_pos = -1;
+    int32_t pf_i = 0, pf_A0[D], pf_A1[D][D];
+    double pf_u = 0.0;
+#pragma unroll
+    for (int m = 0; m < D; ++m) {
+        pf_A0[m] = 0;
+#pragma unroll
+        for (int x = 0; x < D; ++x) pf_A1[m][x] = 0;
+    }
     for (;;) {
         const bool going = live && done == 0 && pos < nsteps;
         if (!__any(going)) break;
@@ -1524,15 +1540,33 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
         SA_STAMP(5);
         const int64_t kk = pos + k;
         const bool mine = going && kk < nsteps;
+        const bool fresh = pf_pos != pos;                     // (the whole lane group alike)
         int32_t i = 0;
         double u = 0.0;
-        if (mine) { i = tape_i[kk * R + r]; u = tape_u[kk * R + r]; }
-        // rows of i and of its neighbours (two round trips per batch); the rows
-        // of the children only where level 2 needs them (below)
         int32_t A0[D], A1[D][D], C[D][D][D];
-        row(i, A0);
+        if (fresh) {
+            // rows of i and of its neighbours (two round trips); the rows of the
+            // children only where level 2 needs them (below)
+            if (mine) { i = tape_i[kk * R + r]; u = tape_u[kk * R + r]; }
+            row(i, A0);
 #pragma unroll
-        for (int m = 0; m < D; ++m) row(A0[m], A1[m]);
+            for (int m = 0; m < D; ++m) row(A0[m], A1[m]);
+        } else {
+            i = mine ? pf_i : 0;
+            u = pf_u;
+#pragma unroll
+            for (int m = 0; m < D; ++m) {
+                A0[m] = pf_A0[m];
+#pragma unroll
+                for (int x = 0; x < D; ++x) A1[m][x] = pf_A1[m][x];
+            }
+        }
+        // the next batch's tape entry (proposal pos + K + k)
+        const int64_t nk = pos + K + k;
+        const bool pf = going && nk < nsteps;
+        int32_t n_i = 0;
+        double n_u = 0.0;
+        if (pf) { n_i = tape_i[nk * R + r]; n_u = tape_u[nk * R + r]; }
         // tree shape (lc_tree2)
         bool ok = true, simple = true;
 #pragma unroll
@@ -1664,6 +1698,9 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
             else ds = lc_delta_mlp<D, false>(adj, NS, colo, bit, T, L, lists, i, cnt, &old_i, A0, A1);
         }
         SA_STAMP(2);
+        // the next batch: the row of its i
+        int32_t n_A0[D], n_A1[D][D];
+        row(n_i, n_A0);
         // potential writes of every proposal into the replica's hash set
         constexpr int NTW = 1 + D + D * D;                  // tree positions: i, the a_m, their children
         if (mine && listpath) {
@@ -1732,6 +1769,9 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
             stands = !hit;
         }
         SA_STAMP(3);
+        // the next batch: the rows of its i's neighbours (land during the resolution)
+#pragma unroll
+        for (int m = 0; m < D; ++m) row(n_A0[m], n_A1[m]);
         // resolution: J0 = first proposal that does not stand
         const int gs = g * K;
         const uint32_t nst = (uint32_t)((__ballot(!stands) >> gs) & GM);
@@ -1802,9 +1842,19 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
             }
             t += J;
             pos += J;
+            // the prefetched batch is the next one only if all K were consumed
+            pf_pos = (J == K) ? pos : -1;
         } else {
             (void)__shfl(sum_after, lane, 64);                // keep the shuffles wave-uniform
             (void)__shfl(dn, lane, 64);
+        }
+        pf_i = n_i;
+        pf_u = n_u;
+#pragma unroll
+        for (int m = 0; m < D; ++m) {
+            pf_A0[m] = n_A0[m];
+#pragma unroll
+            for (int x = 0; x < D; ++x) pf_A1[m][x] = n_A1[m][x];
         }
         // flips land before the next batch reads; the hash reads end before the next clear
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
