@@ -38,6 +38,7 @@
 // sum_end, done back to the state arrays.  Same proposals, accepts and outputs
 // as every other SA mode.
 #include "mjx_common.h"
+#include <type_traits>
 #include "mjx_mt.h"
 #include <math.h>
 
@@ -1720,17 +1721,18 @@ struct GeoW {
     int nw;        // uint32 bit words per level (even)
     int lc;        // change-list capacity per level
     int off_lev;   // (T+1) * nw level words
-    int off_mk;    // T * nw * 32 mark bytes (levels 1..T)
+    int off_mk;    // T * nw * 32 marks (levels 1..T): a byte each, 16 bits above 8 waves
     int off_lev0;  // nw words: level 0 at launch start
     int off_mt;
-    int off_list;  // NW * (T+1) * lc list words (one set per wave)
+    int off_list;  // NW * T * lc list words (one set per wave, levels 1..T)
     int off_q;     // proposal queue: i[64], end[64], u[64]
-    int off_res;   // per proposal: packed word, schedule a, b after its step; control words
+    int off_res;   // per proposal: conflict word, packed word, schedule a, b after its step; control words
     int bytes;
 };
 
 static bool geometry_wg(int64_t n, int d, int T, int NW, GeoW* g) {
-    if (n < 2 || n > 65535 || d < 1 || d > 4 || T < 1 || T > kMaxT || NW < 2 || NW > 8) return false;
+    if (n < 2 || n > 65535 || d < 1 || d > 4 || T < 1 || T > kMaxT || NW < 2 || NW > 16) return false;
+    const int mkb = NW > 8 ? 2 : 1;                 // bytes per mark
     g->nw = (int)(((n + 63) / 64) * 2);
     int64_t lc = ball(d, T);
     if (lc > n) lc = n;
@@ -1739,15 +1741,23 @@ static bool geometry_wg(int64_t n, int d, int T, int NW, GeoW* g) {
     g->lc = (int)lc;
     int64_t off = ((int64_t)n * 4 * 2 + 15) / 16 * 16;
     g->off_lev = (int)off;   off += (int64_t)(T + 1) * g->nw * 4;
-    g->off_mk = (int)off;    off += (int64_t)T * g->nw * 32;
+    g->off_mk = (int)off;    off += (int64_t)T * g->nw * 32 * mkb;
     g->off_lev0 = (int)off;  off += (int64_t)g->nw * 4;
     g->off_mt = (int)off;    off += MT_N * 4;
-    g->off_list = (int)off;  off += (int64_t)NW * (T + 1) * g->lc * 4;
+    g->off_list = (int)off;  off += (int64_t)NW * T * g->lc * 4;
     off = (off + 15) / 16 * 16;
     g->off_q = (int)off;     off += 64 * 4 + 64 * 4 + 64 * 8;
-    g->off_res = (int)off;   off += 8 * 4 + 8 * 8 + 8 * 8 + 4 * 4;
+    g->off_res = (int)off;   off += (int64_t)NW * (4 + 4 + 8 + 8) + 4 * 4;
     g->bytes = (int)off;
     return (size_t)off <= kLdsMax;
+}
+
+// waves of the whole-CU kernel: 16 where its LDS fits (d = 4, T = 3: n <= ~1e4,
+// SA_RRG.py's own size), else 8; kernel option split = 4 or 8 forces that many
+static int wg_waves(int64_t n, int d, int T, int split) {
+    if (split == 4 || split == 8) return split;
+    GeoW g;
+    return geometry_wg(n, d, T, 16, &g) ? 16 : 8;
 }
 
 template <int D, int T, int NW, bool TRACE>
@@ -1755,7 +1765,12 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
                                                       int64_t W, u64* __restrict__ s, mjx_sa_state st, int64_t nsteps,
                                                       double par_a, double par_b, double a_cap, double b_cap,
                                                       int64_t t_cap, GeoW geo) {
-    static_assert(D >= 1 && D <= 4 && T >= 2 && T <= 4 && NW >= 2 && NW <= 8, "whole-CU LDS SA: d <= 4, 2 <= T <= 4");
+    static_assert(D >= 1 && D <= 4 && T >= 2 && T <= 4 && NW >= 2 && NW <= 16, "whole-CU LDS SA: d <= 4, 2 <= T <= 4");
+    // a mark per (level >= 1, node): bit q = proposal q of the round; bytes up to
+    // 8 waves, 16-bit words for 16 (n = 1e4, T = 3 then fits in 159 KB)
+    using MK = typename std::conditional<(NW > 8), uint16_t, uint8_t>::type;
+    constexpr int MKB = 8 * (int)sizeof(MK);       // bits per mark
+    constexpr int MPW = 4 / (int)sizeof(MK);       // marks per 32-bit word
     constexpr int DP1 = D + 1;
     constexpr int MAXM = 64 / DP1;                 // members of C_{t-1} one wave can expand
     constexpr int NT = 64 * NW;
@@ -1769,17 +1784,19 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
     const int mkl = nw * 32;                       // mark bytes per level
     uint16_t* rows = reinterpret_cast<uint16_t*>(smem);
     uint32_t* lev = reinterpret_cast<uint32_t*>(smem + geo.off_lev);
-    unsigned char* mk = smem + geo.off_mk;
+    MK* mk = reinterpret_cast<MK*>(smem + geo.off_mk);
     uint32_t* lev0s = reinterpret_cast<uint32_t*>(smem + geo.off_lev0);
     uint32_t* mt = reinterpret_cast<uint32_t*>(smem + geo.off_mt);
-    uint32_t* lst = reinterpret_cast<uint32_t*>(smem + geo.off_list) + w * (T + 1) * lc;   // this wave's lists
+    // this wave's lists of levels 1..T (level l at (l-1)*lc)
+    uint32_t* lst = reinterpret_cast<uint32_t*>(smem + geo.off_list) + w * T * lc - lc;
     int* q_i = reinterpret_cast<int*>(smem + geo.off_q);
     int* q_end = q_i + 64;
     double* q_u = reinterpret_cast<double*>(q_end + 64);
-    uint32_t* res = reinterpret_cast<uint32_t*>(smem + geo.off_res);      // packed result per proposal
-    double* res_a = reinterpret_cast<double*>(res + 8);
-    double* res_b = res_a + 8;
-    int* ctl = reinterpret_cast<int*>(res_b + 8);
+    uint32_t* res_cf = reinterpret_cast<uint32_t*>(smem + geo.off_res);   // per proposal: conflict bits
+    uint32_t* res = res_cf + NW;                                           // packed result per proposal
+    double* res_a = reinterpret_cast<double*>(res + NW);
+    double* res_b = res_a + NW;
+    int* ctl = reinterpret_cast<int*>(res_b + NW);
     const uint32_t obit = 1u << w;                 // this proposal's mark bit
     const uint32_t early = obit - 1u;              // the earlier proposals' mark bits
 
@@ -1792,8 +1809,9 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
         return ((lw >> (v & 31)) ^ (mb >> w)) & 1u;
     };
     auto mark_word = [&](int t, int v) -> uint32_t* {
-        return reinterpret_cast<uint32_t*>(mk + (t - 1) * mkl + (v & ~3));
+        return reinterpret_cast<uint32_t*>(mk + (t - 1) * mkl + (v & ~(MPW - 1)));
     };
+    auto mark_bit = [&](int v) -> uint32_t { return obit << (MKB * (v & (MPW - 1))); };
     auto nbrs = [&](int v, int (&o)[D]) {
         const uint2 x = *reinterpret_cast<const uint2*>(rows + v * 4);
         o[0] = (int)(x.x & 0xffffu);
@@ -1813,7 +1831,7 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
             rows[v * 4 + (q - v * D)] = (uint16_t)g[q];
         }
         for (int q = tid; q < (T + 1) * nw; q += NT) lev[q] = 0u;
-        for (int q = tid; q < T * nw * 8; q += NT) reinterpret_cast<uint32_t*>(mk)[q] = 0u;
+        for (int q = tid; q < T * nw * 8 * (int)sizeof(MK); q += NT) reinterpret_cast<uint32_t*>(mk)[q] = 0u;
         for (int q = tid; q < MT_N; q += NT) mt[q] = st.mt[r * MT_N + q];
         const int64_t col = r >> 6;
         const u64 rbit = 1ull << (r & 63);
@@ -1986,9 +2004,6 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
         const bool act = w < nq;
         const int iv = __builtin_amdgcn_readfirstlane(q_i[pks + (act ? w : 0)]);
         const double u = q_u[pks + (act ? w : 0)];
-        int ip[NW - 1];                                    // the earlier proposals' i (level-0 conflicts)
-#pragma unroll
-        for (int j = 0; j < NW - 1; ++j) ip[j] = (act && j < w) ? q_i[pks + j] : -1;
         const uint32_t old_i = bit_of(0, iv);
         uint32_t cf = 0;                                   // bit j: read something proposal j changed
         int cand, nv[D];
@@ -2012,9 +2027,11 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
             for (int e = 0; e < D; ++e) ones += (int)(bit_of(0, nv[e]) ^ (nv[e] == iv));
 #pragma unroll
             for (int j = 0; j < NW - 1; ++j) {
-                bool hit = cand == ip[j];
+                // the earlier proposals' i (level-0 conflicts), LDS broadcast reads
+                const int ipj = (act && j < w) ? q_i[pks + j] : -1;
+                bool hit = cand == ipj;
 #pragma unroll
-                for (int e = 0; e < D; ++e) hit |= nv[e] == ip[j];
+                for (int e = 0; e < D; ++e) hit |= nv[e] == ipj;
                 if (live && hit) cf |= 1u << j;
             }
             const uint32_t own = bit_of(0, cand) ^ (cand == iv);
@@ -2023,7 +2040,7 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
             const bool chg = live && nb != cur;
             const u64 m = __ballot(chg);
             if (chg) {
-                atomicOr(mark_word(1, cand), obit << (8 * (cand & 3)));
+                atomicOr(mark_word(1, cand), mark_bit(cand));
                 lst[lc + __popcll(m & ltmask)] = (uint32_t)cand;
             }
             lc_c[1] = cand;
@@ -2091,7 +2108,7 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
                 const uint32_t nb = maj(ones, own);
                 const uint32_t cur = bit_of(l, c2);
                 const bool chg = act2 && nb != cur;
-                const uint32_t mb = obit << (8 * (c2 & 3));
+                const uint32_t mb = mark_bit(c2);
                 bool add = chg;
                 if (l == T) {
                     // the last level counts distinct nodes: the first mark wins
@@ -2137,7 +2154,7 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
                         for (int e = 0; e < D; ++e) ones += (int)look(l - 1, nv2[e], cfm);
                         const uint32_t own = look(l - 1, cd, cfm);
                         const uint32_t nb = maj(ones, own);
-                        const uint32_t mb = obit << (8 * (cd & 3));
+                        const uint32_t mb = mark_bit(cd);
                         cur = bit_of(l, cd);
                         if (nb != cur) add = (atomicOr(mark_word(l, cd), mb) & mb) == 0u;
                     }
@@ -2204,7 +2221,8 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
         for (int j = 0; j < NW - 1; ++j)
             if (__ballot((cf >> j) & 1u)) cfw |= 1u << j;
         if (lane == 0) {
-            res[w] = cfw | (acc ? 0x100u : 0u) | (tie ? 0x200u : 0u) | ((uint32_t)(ds & 0xffff) << 16);
+            res_cf[w] = cfw;
+            res[w] = (acc ? 1u : 0u) | (tie ? 2u : 0u) | ((uint32_t)(ds & 0xffff) << 16);
             res_a[w] = anx;
             res_b[w] = bnx;
         }
@@ -2215,21 +2233,22 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
         // up to a stop
         // lane-parallel over the NW proposals: lane q holds proposal q's result
         const bool lq = lane < nq;
-        const uint32_t pq = lq ? res[lane & 7] : 0u;
-        const bool aq = (pq >> 8) & 1u;
+        const uint32_t pq = lq ? res[lane & (NW - 1)] : 0u;
+        const uint32_t pcf = lq ? res_cf[lane & (NW - 1)] : 0u;
+        const bool aq = pq & 1u;
         const uint32_t accm = (uint32_t)__ballot(lq && aq);
-        const u64 clm = __ballot(lq && (pq & accm & 0xffu) != 0u);     // read a taken... accepted earlier one
+        const u64 clm = __ballot(lq && (pcf & accm) != 0u);             // read an accepted earlier one's change
         int qstop = nq;
         if (clm) {
             const int qc = __ffsll((unsigned long long)clm) - 1;
             if (qc < qstop) qstop = qc;
         }
-        // sum(s_end) after each proposal: prefix over the accepted ones (8 lanes)
+        // sum(s_end) after each proposal: prefix over the accepted ones (NW lanes)
         int pre = (lq && aq) ? (int)(int16_t)(pq >> 16) : 0;
 #pragma unroll
-        for (int o = 1; o < 8; o <<= 1) {
-            const int v = __shfl_up(pre, o, 8);
-            if ((lane & 7) >= o) pre += v;
+        for (int o = 1; o < NW; o <<= 1) {
+            const int v = __shfl_up(pre, o, NW);
+            if ((lane & (NW - 1)) >= o) pre += v;
         }
         const int64_t sum_after = sum_end + (int64_t)pre;
         const int dnq = (t + lane + 1 > t_cap) ? 2 : ((sum_after == n) ? 1 : 0);
@@ -2239,7 +2258,7 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
             const int qs = __ffsll((unsigned long long)stq) - 1;
             if (qs + 1 < taken) taken = qs + 1;
         }
-        ties += __popcll(__ballot(lane < taken && ((pq >> 9) & 1u)));
+        ties += __popcll(__ballot(lane < taken && ((pq >> 1) & 1u)));
         if constexpr (TRACE) {
             const int64_t my_sum = __shfl(sum_after, w, 64);        // sum(s_end) after this wave's step
             if (w < taken && lane == 0) {
@@ -2250,7 +2269,7 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
                 if (st.tr_dE) st.tr_dE[kk * R + r] = dE;
             }
         }
-        const double ra = res_a[lane & 7], rb = res_b[lane & 7];
+        const double ra = res_a[lane & (NW - 1)], rb = res_b[lane & (NW - 1)];
         sum_end = __shfl(sum_after, taken - 1, 64);
         done = __shfl(dnq, taken - 1, 64);
         t += taken;                                                 // (code/SA_RRG.py:77,82)
@@ -2791,7 +2810,7 @@ extern "C" int64_t mjx_sa_lds_plan(int64_t n, int d, int p, int c, uint32_t flag
     const bool small_d = d == 3 || d == 4;
     salds::GeoW gw;
     salds::Geo g2;
-    const int nwv = (split == 4) ? 4 : 8;
+    const int nwv = salds::wg_waves(n, d, T, split);
     salds::GeoW1 gw1;
     if (!(flags & (MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE | MJX_SA_LDS_PAIR | MJX_SA_LDS_WAVE)) && small_d && T == 1 &&
         salds::geometry_wg1(n, d, 32, &gw1)) {
@@ -2863,7 +2882,7 @@ extern "C" int mjx_sa_lds_steps(const int32_t* adj, int64_t n, int d, int p, int
         return trm ? gom(salds::k_sa_lds_multi<4, 8, true>) : gom(salds::k_sa_lds_multi<4, 8, false>);
     }
     salds::GeoW gw;
-    const int nwv = (st.opt_split == 4) ? 4 : 8;
+    const int nwv = salds::wg_waves(n, d, T, st.opt_split);
     if (!(st.opt_flags & (MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE | MJX_SA_LDS_WAVE)) && (d == 3 || d == 4) && T >= 2 &&
         T <= 4 && salds::geometry_wg(n, d, T, nwv, &gw)) {
         const bool trw = st.tr_i || st.tr_acc || st.tr_sum || st.tr_dE;
@@ -2876,6 +2895,7 @@ extern "C" int mjx_sa_lds_steps(const int32_t* adj, int64_t n, int d, int p, int
         };
 #define MJX_LDS_WG3(DD, TT)                                                                                       \
         if (nwv == 4) return trw ? gow(salds::k_sa_lds_wg<DD, TT, 4, true>) : gow(salds::k_sa_lds_wg<DD, TT, 4, false>); \
+        if (nwv == 16) return trw ? gow(salds::k_sa_lds_wg<DD, TT, 16, true>) : gow(salds::k_sa_lds_wg<DD, TT, 16, false>); \
         return trw ? gow(salds::k_sa_lds_wg<DD, TT, 8, true>) : gow(salds::k_sa_lds_wg<DD, TT, 8, false>);
 #define MJX_LDS_WG(DD)                       \
         switch (T) {                         \

@@ -33,17 +33,18 @@ def _plan(mjx_mod, n, p, c, sa):
     return int(nbytes), int(threads.value)
 
 
-@pytest.mark.parametrize("p,c,K1,K2,threads_want", [
-    (3, 1, 1900, 1133, 512),     # SA_RRG.py's p=3, c=1: k_sa_lds_wg<4,3,8,false>, 8 waves
-    (1, 1, 2900, 1733, 320),     # configs[0]'s p=c=1: k_sa_lds_wg1<4,4,8,false>, 4 waves + the parser
+@pytest.mark.parametrize("p,c,K1,K2,threads_want,kernel", [
+    (3, 1, 1900, 1133, 1024, None),          # SA_RRG.py's p=3, c=1: k_sa_lds_wg<4,3,16,false>, 16 waves
+    (3, 1, 1900, 1133, 512, {"split": 8}),   # the 8-wave form (byte marks)
+    (1, 1, 2900, 1733, 320, None),           # configs[0]'s p=c=1: k_sa_lds_wg1<4,4,8,false>, 4 waves + the parser
 ])
-def test_script_size_no_trace_matches_oracle(mjx_mod, p, c, K1, K2, threads_want):
+def test_script_size_no_trace_matches_oracle(mjx_mod, p, c, K1, K2, threads_want, kernel):
     """The kernels run() and the bench use (TRACE = false) at n = 1e4, 64
     replicas on 64 graphs, two ragged calls: conf, t and MT19937 stream of
     replicas 0, 1, 31 and 63 equal the oracle's."""
     graphs = _graphs(mjx_mod, R_SCRIPT, 7000 + 100 * p)
     seeds = list(range(3000, 3000 + R_SCRIPT))
-    sa = mjx_mod.SAReplicas(graphs, p, c, seeds, layout="lds")
+    sa = mjx_mod.SAReplicas(graphs, p, c, seeds, layout="lds", kernel=kernel)
     assert sa.layout == "lds" and sa.rep_graph is not None
     nbytes, threads = _plan(mjx_mod, N_SCRIPT, p, c, sa)
     assert threads == threads_want, threads        # the whole-CU kernel
