@@ -18,7 +18,7 @@ names = ["B0 (wave 0 parses)", "level 1", "level 2", "level 3", "dE+accept", "ba
          "resolve+apply"]
 n, d, R = 10_000, 4, 64
 graphs = [mjx.random_regular_graph(d, n, seed=7000 + k) for k in range(R)]
-for (p, c, kern, nw) in ((3, 1, None, 8), (3, 1, {"split": 4}, 4), (2, 1, None, 8)):
+for (p, c, kern, nw) in ((3, 1, None, 16), (3, 1, {"split": 8}, 8), (2, 1, None, 16)):
     sa = mjx.SAReplicas(graphs, p, c, list(range(R)), layout="lds", kernel=kern)
     K = 20000
     sa.steps(K)
@@ -32,7 +32,7 @@ for (p, c, kern, nw) in ((3, 1, None, 8), (3, 1, {"split": 4}, 4), (2, 1, None, 
     lib.mjx_sa_lds_prof_read(buf, 1)
     wave_rounds = buf[7]                       # rounds x waves, over all replicas
     rounds = wave_rounds / nw / R              # rounds per replica
-    print(f"p={p} c={c} {kern or 'wg8'}: {1e6 * el / K:.3f} us/step, {K / rounds:.2f} proposals per round, "
+    print(f"p={p} c={c} {kern or 'wg16'}: {1e6 * el / K:.3f} us/step, {K / rounds:.2f} proposals per round, "
           f"{1e6 * el / rounds:.3f} us per round; cycles per round per wave: "
           + ", ".join(f"{nm} {buf[q] / wave_rounds:.0f}" for q, nm in enumerate(names))
           + f"; total {sum(buf[:7]) / wave_rounds:.0f}", flush=True)
