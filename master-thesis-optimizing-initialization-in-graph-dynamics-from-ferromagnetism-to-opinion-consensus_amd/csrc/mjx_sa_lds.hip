@@ -104,6 +104,12 @@ __device__ __forceinline__ int64_t wave_sum(int64_t x) {
     return x;
 }
 
+// lane l's 64-bit value (l wave-uniform): two readlanes, no LDS round trip
+__device__ __forceinline__ int64_t rl64(int64_t x, int l) {
+    return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)((uint64_t)x >> 32), l) << 32) |
+                     (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l));
+}
+
 // Diagnostic build only (-DMJX_SA_PROF, tools/sa_lds_prof.py): per-phase
 // s_memtime cycles of k_sa_lds_fast summed over waves; every stamp drains the
 // wave's counters first, so a phase's exposed latency is charged to it.
@@ -2002,8 +2008,10 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
         if (nq > NW) nq = NW;
         if ((int64_t)nq > nsteps - k) nq = (int)(nsteps - k);
         const bool act = w < nq;
-        const int iv = __builtin_amdgcn_readfirstlane(q_i[pks + (act ? w : 0)]);
+        // the round's proposals' i, lane j = proposal j (one read; readlanes below)
+        const int ipv = q_i[(pks + lane < 64) ? pks + lane : 63];
         const double u = q_u[pks + (act ? w : 0)];
+        const int iv = __builtin_amdgcn_readlane(ipv, act ? w : 0);
         const uint32_t old_i = bit_of(0, iv);
         uint32_t cf = 0;                                   // bit j: read something proposal j changed
         int cand, nv[D];
@@ -2027,8 +2035,8 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
             for (int e = 0; e < D; ++e) ones += (int)(bit_of(0, nv[e]) ^ (nv[e] == iv));
 #pragma unroll
             for (int j = 0; j < NW - 1; ++j) {
-                // the earlier proposals' i (level-0 conflicts), LDS broadcast reads
-                const int ipj = (act && j < w) ? q_i[pks + j] : -1;
+                // the earlier proposals' i (level-0 conflicts)
+                const int ipj = (act && j < w) ? __builtin_amdgcn_readlane(ipv, j) : -1;
                 bool hit = cand == ipj;
 #pragma unroll
                 for (int e = 0; e < D; ++e) hit |= nv[e] == ipj;
@@ -2244,12 +2252,12 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
             if (qc < qstop) qstop = qc;
         }
         // sum(s_end) after each proposal: prefix over the accepted ones (NW lanes)
+        // (DPP row shifts: lanes 0..15 are one row and hold every proposal)
         int pre = (lq && aq) ? (int)(int16_t)(pq >> 16) : 0;
-#pragma unroll
-        for (int o = 1; o < NW; o <<= 1) {
-            const int v = __shfl_up(pre, o, NW);
-            if ((lane & (NW - 1)) >= o) pre += v;
-        }
+        pre += __builtin_amdgcn_update_dpp(0, pre, 0x111, 0xf, 0xf, false);     // row_shr:1
+        pre += __builtin_amdgcn_update_dpp(0, pre, 0x112, 0xf, 0xf, false);     // row_shr:2
+        pre += __builtin_amdgcn_update_dpp(0, pre, 0x114, 0xf, 0xf, false);     // row_shr:4
+        if constexpr (NW > 8) pre += __builtin_amdgcn_update_dpp(0, pre, 0x118, 0xf, 0xf, false);   // row_shr:8
         const int64_t sum_after = sum_end + (int64_t)pre;
         const int dnq = (t + lane + 1 > t_cap) ? 2 : ((sum_after == n) ? 1 : 0);
         const u64 stq = __ballot(lane < qstop && dnq != 0);            // (code/SA_RRG.py:84), m == 1
@@ -2260,7 +2268,7 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
         }
         ties += __popcll(__ballot(lane < taken && ((pq >> 1) & 1u)));
         if constexpr (TRACE) {
-            const int64_t my_sum = __shfl(sum_after, w, 64);        // sum(s_end) after this wave's step
+            const int64_t my_sum = rl64(sum_after, w);              // sum(s_end) after this wave's step
             if (w < taken && lane == 0) {
                 const int64_t kk = k + w;
                 if (st.tr_i) st.tr_i[kk * R + r] = iv;
@@ -2269,12 +2277,11 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
                 if (st.tr_dE) st.tr_dE[kk * R + r] = dE;
             }
         }
-        const double ra = res_a[lane & (NW - 1)], rb = res_b[lane & (NW - 1)];
-        sum_end = __shfl(sum_after, taken - 1, 64);
-        done = __shfl(dnq, taken - 1, 64);
+        sum_end = rl64(sum_after, taken - 1);
+        done = __builtin_amdgcn_readlane(dnq, taken - 1);
         t += taken;                                                 // (code/SA_RRG.py:77,82)
-        a = __shfl(ra, taken - 1, 64);                              // (:80-81) after the taken steps
-        b = __shfl(rb, taken - 1, 64);
+        a = res_a[taken - 1];                                       // (:80-81) after the taken steps
+        b = res_b[taken - 1];
         // ---- the taken accepted proposals' changes; every proposal clears its marks
         const bool mine = w < taken && ((accm >> w) & 1u);
         if (mine && lane == 0) atomicXor(&lev[iv >> 5], 1u << (iv & 31));
