@@ -1703,8 +1703,8 @@ __global__ void __launch_bounds__(64) k_sa_lds_multi(const int32_t* __restrict__
 // The whole CU for one replica (k_sa_lds_wg<D, T, NW>, d <= 4, 1 < T <= 4).
 // The one-wave kernels above leave 3 of a CU's 4 SIMDs idle: a replica's step
 // is a chain of dependent LDS round trips on one wave.  Here NW waves share the
-// replica's LDS image and evaluate NW consecutive proposals k, k+1, ..., k+NW-1
-// at once, each against the levels as they stand at the start of the round,
+// replica's LDS image; NW-1 of them evaluate as many consecutive proposals k,
+// k+1, ... at once, each against the levels as they stand at the start of the round,
 // wave q exactly as k_sa_lds_fast evaluates one proposal.  The change marks
 // are one BYTE per (level, node): bit q = proposal q's C_t, so "level t as
 // proposal q sees it" is the level bit XOR mark bit q, and the bits below q in
@@ -1720,9 +1720,11 @@ __global__ void __launch_bounds__(64) k_sa_lds_multi(const int32_t* __restrict__
 // taken accepted one, or up to the first stop (consensus, t cap).  Taken
 // accepted change sets are disjoint (a shared node would be a conflict), so
 // they are applied concurrently.  Workgroup barriers: one after the proposals
-// are published, one per level (marks of C_{l-1} before they are read), one
-// before the resolution.  Wave 0 parses the proposal windows (as
-// k_sa_lds_multi) into an LDS queue.  Same draws, accepts and state as k_sa_lds.
+// are published, one after every proposal's marks (the conflict checks read
+// them), one before the resolution.  The last wave parses the numpy stream's
+// windows (as k_sa_lds_multi) into an LDS ring of proposals while the others
+// evaluate, off the round's critical path.  Same draws, accepts and state as
+// k_sa_lds.
 struct GeoW {
     int nw;        // uint32 bit words per level (even)
     int lc;        // change-list capacity per level
@@ -1730,7 +1732,7 @@ struct GeoW {
     int off_mk;    // T * nw * 32 marks (levels 1..T): a byte each, 16 bits above 8 waves
     int off_lev0;  // nw words: level 0 at launch start
     int off_mt;
-    int off_list;  // NW * T * lc list words (one set per wave, levels 1..T)
+    int off_list;  // (NW - 1) * T * lc list words (one set per evaluating wave, levels 1..T)
     int off_q;     // proposal queue: i[64], end[64], u[64]
     int off_res;   // per proposal: conflict word, packed word, schedule a, b after its step; control words
     int bytes;
@@ -1750,7 +1752,7 @@ static bool geometry_wg(int64_t n, int d, int T, int NW, GeoW* g) {
     g->off_mk = (int)off;    off += (int64_t)T * g->nw * 32 * mkb;
     g->off_lev0 = (int)off;  off += (int64_t)g->nw * 4;
     g->off_mt = (int)off;    off += MT_N * 4;
-    g->off_list = (int)off;  off += (int64_t)NW * T * g->lc * 4;
+    g->off_list = (int)off;  off += (int64_t)(NW - 1) * T * g->lc * 4;
     off = (off + 15) / 16 * 16;
     g->off_q = (int)off;     off += 64 * 4 + 64 * 4 + 64 * 8;
     g->off_res = (int)off;   off += (int64_t)NW * (4 + 4 + 8 + 8) + 4 * 4;
@@ -1780,6 +1782,7 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
     constexpr int DP1 = D + 1;
     constexpr int MAXM = 64 / DP1;                 // members of C_{t-1} one wave can expand
     constexpr int NT = 64 * NW;
+    constexpr int NE = NW - 1;                     // waves evaluating proposals; wave NE parses
     extern __shared__ __align__(16) unsigned char smem[];
     const int tid = threadIdx.x;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // this wave's proposal slot in a round
@@ -1883,139 +1886,135 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
     double inv_n = 1.0 / (double)n;
     asm volatile("" : "+v"(a), "+v"(b), "+v"(par_a), "+v"(par_b), "+v"(a_cap), "+v"(b_cap), "+v"(inv_n));
 
-    // ---- proposal windows (wave 0): lane j holds proposal j, mirrored in the LDS queue
-    int pb_i = 0, pb_end = 0;
-    uint32_t pb_w1 = 0, pb_w2 = 0;
-    double pb_u = 0.0;
-    int npend = 0, pk = 0;
-    auto parse = [&](bool one) {
-        for (;;) {
-            if (idx >= MT_N) {
-                if (one) break;
-                lds_twist(mt, lane);
-                idx = 0;
-            }
-            const int lim = (MT_N - idx < 64) ? MT_N - idx : 64;
-            uint32_t tw = 0, y = 0;
-            bool ok = false;
-            if (lane < lim) {
-                tw = mt_temper(mt[idx + lane]);
-                y = tw & mask;
-                ok = y <= rng;
-            }
-            const u64 okm = __ballot(ok);
-            // proposal starts by a scalar walk over the ballot (each: the first
-            // acceptable word at or after the previous end, then rand()'s two
-            // words); the start lanes push their lane ids to their target lanes,
-            // which pull i, w1, w2 (lane-parallel: no readlane per proposal)
-            u64 stm = 0;
-            int pos = 0, got = 0;
-            while (pos < 64 && npend + got < 63) {
-                const u64 m = okm >> pos;
-                if (!m) break;
-                const int f = pos + __ffsll((unsigned long long)m) - 1;
-                if (f + 2 >= lim) break;
-                stm |= 1ull << f;
-                ++got;
-                pos = f + 3;
-            }
-            if (got > 0) {
-                const bool isst = (stm >> lane) & 1ull;
-                const int tgt = isst ? npend + __popcll(stm & ((1ull << lane) - 1ull)) : 63;
-                const int src = __builtin_amdgcn_ds_permute(tgt * 4, lane) & 63;
-                const int yi = __builtin_amdgcn_ds_bpermute(src * 4, (int)y);
-                const int x1 = __builtin_amdgcn_ds_bpermute((src + 1) * 4, (int)tw);
-                const int x2 = __builtin_amdgcn_ds_bpermute((src + 2) * 4, (int)tw);
-                if (lane >= npend && lane < npend + got) {
-                    pb_i = yi;
-                    pb_w1 = (uint32_t)x1;
-                    pb_w2 = (uint32_t)x2;
-                    pb_end = idx + src + 3;
-                }
-                npend += got;
-                idx += pos;
-                break;
-            }
-            if (one) break;
-            if (!okm) { idx += lim; continue; }
-            const int f = __ffsll((unsigned long long)okm) - 1;
-            if (f > 0) { idx += f; continue; }
-            // i is the window's first word and rand()'s two words cross the end of
-            // the state: the serial draw twists between them, as numpy does
-            const int iv = __builtin_amdgcn_readlane((int)y, 0);
-            idx += 1;
-            if (idx >= MT_N) { lds_twist(mt, lane); idx = 0; }
-            const uint32_t w1 = mt_temper(mt[idx]);
-            idx += 1;
-            if (idx >= MT_N) { lds_twist(mt, lane); idx = 0; }
-            const uint32_t w2 = mt_temper(mt[idx]);
-            idx += 1;
-            if (lane == npend) { pb_i = iv; pb_w1 = w1; pb_w2 = w2; pb_end = idx; }
-            ++npend;
-            break;
-        }
-        pb_u = mt_double(pb_w1, pb_w2);
+    // ---- the proposal ring (wave P = NE parses, the NE others evaluate): slot
+    // q & 63 holds proposal q of the launch (i, u, end: the MT index after its
+    // draws, bit 10 its state generation's parity).  npend proposals parsed, pk
+    // taken (running counts, every wave tracks pk); the parse wave appends while
+    // the round evaluates, into slots the round does not read, and keeps slot
+    // pk-1 (the last taken proposal's end) for the launch's MT position.  A twist
+    // under unconsumed proposals first saves the old state to st.mt: the launch
+    // ends on either generation (the buffer the last taken proposal drew from).
+    uint32_t npend = 0, pk = 0;
+    int gen = 0;
+    const int idx0 = idx;
+    auto twist = [&]() {
+        for (int q = lane; q < MT_N; q += 64) st.mt[r * MT_N + q] = mt[q];
+        lds_twist(mt, lane);
+        idx = 0;
+        gen ^= 1;
     };
+    // one window of up to 64 words at idx: at most `room` proposals appended
+    auto parse_window = [&](uint32_t room) {
+        if (idx >= MT_N) twist();
+        const int lim = (MT_N - idx < 64) ? MT_N - idx : 64;
+        uint32_t tw = 0, y = 0;
+        bool ok = false;
+        if (lane < lim) {
+            tw = mt_temper(mt[idx + lane]);
+            y = tw & mask;
+            ok = y <= rng;
+        }
+        const u64 okm = __ballot(ok);
+        // proposal starts by a scalar walk over the ballot (each: the first
+        // acceptable word at or after the previous end, then rand()'s two words)
+        u64 stm = 0;
+        int pos = 0;
+        uint32_t got = 0;
+        while (pos < 64 && got < room) {
+            const u64 m = okm >> pos;
+            if (!m) break;
+            const int f = pos + __ffsll((unsigned long long)m) - 1;
+            if (f + 2 >= lim) break;
+            stm |= 1ull << f;
+            ++got;
+            pos = f + 3;
+        }
+        if (got > 0) {
+            const uint32_t x1 = (uint32_t)__builtin_amdgcn_ds_bpermute(((lane + 1) & 63) * 4, (int)tw);
+            const uint32_t x2 = (uint32_t)__builtin_amdgcn_ds_bpermute(((lane + 2) & 63) * 4, (int)tw);
+            if ((stm >> lane) & 1ull) {
+                const int q = (int)((npend + (uint32_t)__popcll(stm & ltmask)) & 63u);
+                q_i[q] = (int)y;
+                q_u[q] = mt_double(x1, x2);
+                q_end[q] = (idx + lane + 3) | (gen << 10);
+            }
+            npend += got;
+            idx += pos;
+            return;
+        }
+        if (room == 0) return;
+        if (!okm) { idx += lim; return; }
+        const int f = __ffsll((unsigned long long)okm) - 1;
+        if (f > 0) { idx += f; return; }
+        // i is the window's first word and rand()'s two words cross the end of
+        // the state: the serial draw twists between them, as numpy does
+        const int iv = __builtin_amdgcn_readlane((int)y, 0);
+        idx += 1;
+        if (idx >= MT_N) twist();
+        const uint32_t w1 = mt_temper(mt[idx]);
+        idx += 1;
+        if (idx >= MT_N) twist();
+        const uint32_t w2 = mt_temper(mt[idx]);
+        idx += 1;
+        if (lane == 0) {
+            const int q = (int)(npend & 63u);
+            q_i[q] = iv;
+            q_u[q] = mt_double(w1, w2);
+            q_end[q] = idx | (gen << 10);
+        }
+        npend += 1;
+    };
+    auto room = [&]() -> uint32_t { return 63u - (npend - pk); };     // slot pk-1 kept
 
     int lc_c[T + 1];
     uint32_t lc_v[T + 1];
     bool lc_in[T + 1];
     int lc_n[T + 1];
     bool lc_fast[T + 1];
-    bool drew = false;
     int64_t k = 0;
 #ifdef MJX_SA_PROF
     unsigned long long _acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, _t0 = __builtin_amdgcn_s_memtime();
 #endif
     while (k < nsteps && done == 0) {
-        if (w == 0) {
-            const int avail = npend - pk;
-            bool re = false;
-            if (avail < NW && idx + 64 <= MT_N) {
-                // carry the unconsumed proposals to lanes 0.. and append one window
-                // (no twist can fall under a carried proposal)
-                const int src = (lane + pk < 64) ? lane + pk : 63;
-                pb_i = __shfl(pb_i, src, 64);
-                pb_end = __shfl(pb_end, src, 64);
-                pb_w1 = (uint32_t)__shfl((int)pb_w1, src, 64);
-                pb_w2 = (uint32_t)__shfl((int)pb_w2, src, 64);
-                npend = avail;
-                pk = 0;
-                parse(true);
-                if (npend == 0) parse(false);
-                re = true;
-            } else if (avail == 0) {
-                npend = 0;
-                pk = 0;
-                parse(false);
-                re = true;
-            }
-            if (re) {
-                q_i[lane] = pb_i;
-                q_u[lane] = pb_u;
-            }
-            if (lane == 0) {
-                ctl[0] = npend;
-                ctl[1] = pk;
-            }
+        if (w == NE) {
+            // a full round's proposals before it starts (the ring is normally
+            // that far ahead: this parses only at launch start or after a dry spell)
+            while (npend - pk < (uint32_t)NE) parse_window(room());
+            if (lane == 0) ctl[0] = (int)npend;
         }
         __syncthreads();                                   // the round's proposals are published
         LDS_STAMP(0);
-        drew = true;
-        const int npd = __builtin_amdgcn_readfirstlane(ctl[0]);
-        const int pks = __builtin_amdgcn_readfirstlane(ctl[1]);
-        int nq = npd - pks;
-        if (nq > NW) nq = NW;
+        const uint32_t npd = (uint32_t)__builtin_amdgcn_readfirstlane(ctl[0]);
+        int nq = (int)(npd - pk);
+        if (nq > NE) nq = NE;
         if ((int64_t)nq > nsteps - k) nq = (int)(nsteps - k);
         const bool act = w < nq;
+        int iv = 0;
+        uint32_t old_i = 0, cf = 0;                        // cf bit j: read something proposal j changed
+        int last = 0;
+        int64_t ds = 0;
+        // the nodes this wave read at each level l >= 2 (a candidate and its
+        // neighbours per lane): checked against the earlier proposals' marks of
+        // level l-1 once every wave is through its levels (no barrier per level)
+        int rd_c[T + 1], rd_n[T + 1][D];
+        bool rd_on[T + 1];
+        bool rd_all = false;                               // a list level: conflicts with every earlier one
+#pragma unroll
+        for (int l = 0; l <= T; ++l) {
+            rd_on[l] = false;
+            lc_fast[l] = true;
+            lc_in[l] = false;
+            lc_n[l] = 0;
+        }
+        bool acc = false, tie = false;
+        double dE = 0.0, anx = a, bnx = b;
+        if (w < NE) {
         // the round's proposals' i, lane j = proposal j (one read; readlanes below)
-        const int ipv = q_i[(pks + lane < 64) ? pks + lane : 63];
-        const double u = q_u[pks + (act ? w : 0)];
-        const int iv = __builtin_amdgcn_readlane(ipv, act ? w : 0);
-        const uint32_t old_i = bit_of(0, iv);
-        uint32_t cf = 0;                                   // bit j: read something proposal j changed
+        const int ipv = q_i[(pk + (uint32_t)(lane < NE ? lane : 0)) & 63u];
+        const double u = q_u[(pk + (uint32_t)(act ? w : 0)) & 63u];
+        iv = __builtin_amdgcn_readlane(ipv, act ? w : 0);
+        old_i = bit_of(0, iv);
         int cand, nv[D];
-        int last;
         // ---- level 1: i and its neighbours, level 0 with i flipped
         {
             int ri[D];
@@ -2034,7 +2033,7 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
 #pragma unroll
             for (int e = 0; e < D; ++e) ones += (int)(bit_of(0, nv[e]) ^ (nv[e] == iv));
 #pragma unroll
-            for (int j = 0; j < NW - 1; ++j) {
+            for (int j = 0; j < NE - 1; ++j) {
                 // the earlier proposals' i (level-0 conflicts)
                 const int ipj = (act && j < w) ? __builtin_amdgcn_readlane(ipv, j) : -1;
                 bool hit = cand == ipj;
@@ -2059,19 +2058,8 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
             last = lc_n[1] ? 1 : 0;
         }
         LDS_STAMP(1);
-        int64_t ds = 0;
-        // the nodes this wave read at each level l >= 2 (a candidate and its
-        // neighbours per lane): checked against the earlier proposals' marks of
-        // level l-1 once every wave is through its levels (no barrier per level)
-        int rd_c[T + 1], rd_n[T + 1][D];
-        bool rd_on[T + 1];
-        bool rd_all = false;                               // a list level: conflicts with every earlier one
 #pragma unroll
         for (int l = 2; l <= T; ++l) {
-            lc_in[l] = false;
-            lc_fast[l] = true;
-            lc_n[l] = 0;
-            rd_on[l] = false;
             rd_c[l] = 0;
 #pragma unroll
             for (int e = 0; e < D; ++e) rd_n[l][e] = 0;
@@ -2188,8 +2176,8 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
                 if (bh < b_cap) bh = par_b * bh;
             }
         }
-        const double anx = (ah < a_cap) ? par_a * ah : ah;          // the schedule after this step
-        const double bnx = (bh < b_cap) ? par_b * bh : bh;
+        anx = (ah < a_cap) ? par_a * ah : ah;                       // the schedule after this step
+        bnx = (bh < b_cap) ? par_b * bh : bh;
         const double si = old_i ? 1.0 : -1.0;
         const double t1 = (-2.0 * ah) * si;
         const double t2 = bh * (double)(-ds);
@@ -2199,8 +2187,6 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
         const float xf = (float)(-num * inv_n);
         const float ef = __expf(xf);
         const float mg = ef * (1e-6f * (1.0f + fabsf(xf))) + 1e-37f;
-        bool acc, tie = false;
-        double dE = 0.0;
         if (fabs(u - (double)ef) > (double)mg) {
             acc = u < (double)ef;
             if (TRACE && st.tr_dE) dE = num / (double)n;
@@ -2212,6 +2198,10 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
             tie = e < 1.0 && fabs(u - e) <= 4.0 * (nextafter(e, 2.0) - e);
         }
         LDS_STAMP(4);
+        } else {
+            // the parse wave: windows into the ring's free slots while the round evaluates
+            for (int it = 0; it < 2 && room() >= 8u; ++it) parse_window(room());
+        }
         __syncthreads();                                   // every proposal's marks of every level
         // what this proposal read at level l-1 that an earlier one changed
 #pragma unroll
@@ -2226,9 +2216,9 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
         if (rd_all) cf |= early;
         uint32_t cfw = 0;
 #pragma unroll
-        for (int j = 0; j < NW - 1; ++j)
+        for (int j = 0; j < NE - 1; ++j)
             if (__ballot((cf >> j) & 1u)) cfw |= 1u << j;
-        if (lane == 0) {
+        if (lane == 0 && w < NE) {
             res_cf[w] = cfw;
             res[w] = (acc ? 1u : 0u) | (tie ? 2u : 0u) | ((uint32_t)(ds & 0xffff) << 16);
             res_a[w] = anx;
@@ -2241,8 +2231,8 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
         // up to a stop
         // lane-parallel over the NW proposals: lane q holds proposal q's result
         const bool lq = lane < nq;
-        const uint32_t pq = lq ? res[lane & (NW - 1)] : 0u;
-        const uint32_t pcf = lq ? res_cf[lane & (NW - 1)] : 0u;
+        const uint32_t pq = lq ? res[lane] : 0u;
+        const uint32_t pcf = lq ? res_cf[lane] : 0u;
         const bool aq = pq & 1u;
         const uint32_t accm = (uint32_t)__ballot(lq && aq);
         const u64 clm = __ballot(lq && (pcf & accm) != 0u);             // read an accepted earlier one's change
@@ -2257,7 +2247,7 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
         pre += __builtin_amdgcn_update_dpp(0, pre, 0x111, 0xf, 0xf, false);     // row_shr:1
         pre += __builtin_amdgcn_update_dpp(0, pre, 0x112, 0xf, 0xf, false);     // row_shr:2
         pre += __builtin_amdgcn_update_dpp(0, pre, 0x114, 0xf, 0xf, false);     // row_shr:4
-        if constexpr (NW > 8) pre += __builtin_amdgcn_update_dpp(0, pre, 0x118, 0xf, 0xf, false);   // row_shr:8
+        if constexpr (NE > 8) pre += __builtin_amdgcn_update_dpp(0, pre, 0x118, 0xf, 0xf, false);   // row_shr:8
         const int64_t sum_after = sum_end + (int64_t)pre;
         const int dnq = (t + lane + 1 > t_cap) ? 2 : ((sum_after == n) ? 1 : 0);
         const u64 stq = __ballot(lane < qstop && dnq != 0);            // (code/SA_RRG.py:84), m == 1
@@ -2309,7 +2299,7 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
             }
         }
         k += taken;
-        pk += taken;
+        pk += (uint32_t)taken;
         LDS_STAMP(6);
 #ifdef MJX_SA_PROF
         _acc[7] += 1;                                      // rounds (every wave counts)
@@ -2319,7 +2309,6 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
     if (lane == 0)
         for (int q = 0; q < 8; ++q) atomicAdd(&mjx_sa_lds_prof[q], _acc[q]);
 #endif
-    if (w == 0 && drew) idx = __builtin_amdgcn_readlane(pb_end, pk - 1);
     if (TRACE && tid == 0) {
         for (; k < nsteps; ++k) {
             if (st.tr_i) st.tr_i[k * R + r] = -1;
@@ -2335,10 +2324,16 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
             if (((lev[v >> 5] ^ lev0s[v >> 5]) >> (v & 31)) & 1u)
                 atomicXor((unsigned long long*)&s[v * W + col], 1ull << (r & 63));
         }
-        for (int q = tid; q < MT_N; q += NT) st.mt[r * MT_N + q] = mt[q];
+    }
+    if (w == NE) {
+        // the launch's MT position: after the last taken proposal's draws, in the
+        // generation it drew from (st.mt holds the old one when the ring ran past a twist)
+        const int e = (pk > 0) ? q_end[(pk - 1u) & 63u] : idx0;
+        if (((e >> 10) & 1) == gen)
+            for (int q = lane; q < MT_N; q += 64) st.mt[r * MT_N + q] = mt[q];
+        if (lane == 0) st.mt_idx[r] = e & 1023;
     }
     if (tid == 0) {
-        st.mt_idx[r] = idx;
         st.a[r] = a;
         st.b[r] = b;
         st.t[r] = t;
