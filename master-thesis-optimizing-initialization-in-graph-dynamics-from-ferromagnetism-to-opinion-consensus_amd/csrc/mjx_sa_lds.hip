@@ -1728,8 +1728,9 @@ __global__ void __launch_bounds__(64) k_sa_lds_multi(const int32_t* __restrict__
 struct GeoW {
     int nw;        // uint32 bit words per level (even)
     int lc;        // change-list capacity per level
-    int off_lev;   // (T+1) * nw level words
-    int off_mk;    // T * nw * 32 marks (levels 1..T): a byte each, 16 bits above 8 waves
+    int off_lev;   // nw level-0 words
+    int off_mk;    // T * nw * 32 marks (levels 1..T): a byte each, 16 bits above 8 waves;
+                   // the top bit holds the level's value
     int off_lev0;  // nw words: level 0 at launch start
     int off_mt;
     int off_list;  // (NW - 1) * T * lc list words (one set per evaluating wave, levels 1..T)
@@ -1748,7 +1749,7 @@ static bool geometry_wg(int64_t n, int d, int T, int NW, GeoW* g) {
     if (lc > 4096) return false;
     g->lc = (int)lc;
     int64_t off = ((int64_t)n * 4 * 2 + 15) / 16 * 16;
-    g->off_lev = (int)off;   off += (int64_t)(T + 1) * g->nw * 4;
+    g->off_lev = (int)off;   off += (int64_t)g->nw * 4;
     g->off_mk = (int)off;    off += (int64_t)T * g->nw * 32 * mkb;
     g->off_lev0 = (int)off;  off += (int64_t)g->nw * 4;
     g->off_mt = (int)off;    off += MT_N * 4;
@@ -1806,16 +1807,19 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
     double* res_a = reinterpret_cast<double*>(res + NW);
     double* res_b = res_a + NW;
     int* ctl = reinterpret_cast<int*>(res_b + NW);
+    constexpr int LVB = MKB - 1;                   // the level value's bit in a mark (above NE proposals)
+    static_assert(NE <= LVB, "a mark holds NE proposal bits and the level bit");
     const uint32_t obit = 1u << w;                 // this proposal's mark bit
     const uint32_t early = obit - 1u;              // the earlier proposals' mark bits
 
-    auto bit_of = [&](int t, int v) -> uint32_t { return (lev[t * nw + (v >> 5)] >> (v & 31)) & 1u; };
-    // node v at level t >= 1 as this proposal sees it; earlier proposals' marks into cfm
+    auto bit_of = [&](int v) -> uint32_t { return (lev[v >> 5] >> (v & 31)) & 1u; };     // level 0
+    auto lvl = [&](int t, int v) -> uint32_t { return ((uint32_t)mk[(t - 1) * mkl + v] >> LVB) & 1u; };   // t >= 1
+    // node v at level t >= 1 as this proposal sees it (one read: the level bit
+    // and the marks); earlier proposals' marks into cfm
     auto look = [&](int t, int v, uint32_t& cfm) -> uint32_t {
-        const uint32_t lw = lev[t * nw + (v >> 5)];
         const uint32_t mb = mk[(t - 1) * mkl + v];
         cfm |= mb & early;
-        return ((lw >> (v & 31)) ^ (mb >> w)) & 1u;
+        return ((mb >> LVB) ^ (mb >> w)) & 1u;
     };
     auto mark_word = [&](int t, int v) -> uint32_t* {
         return reinterpret_cast<uint32_t*>(mk + (t - 1) * mkl + (v & ~(MPW - 1)));
@@ -1839,7 +1843,7 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
             const int64_t v = q / D;
             rows[v * 4 + (q - v * D)] = (uint16_t)g[q];
         }
-        for (int q = tid; q < (T + 1) * nw; q += NT) lev[q] = 0u;
+        for (int q = tid; q < nw; q += NT) lev[q] = 0u;
         for (int q = tid; q < T * nw * 8 * (int)sizeof(MK); q += NT) reinterpret_cast<uint32_t*>(mk)[q] = 0u;
         for (int q = tid; q < MT_N; q += NT) mt[q] = st.mt[r * MT_N + q];
         const int64_t col = r >> 6;
@@ -1857,19 +1861,14 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
         }
         __syncthreads();
         for (int t = 1; t <= T; ++t) {
-            for (int64_t v0 = (int64_t)w * 64; v0 < (int64_t)nw * 32; v0 += NT) {
-                const int v = (int)(v0 + lane);
-                uint32_t nb = 0;
-                if (v < n) {
-                    int nv[D];
-                    nbrs(v, nv);
-                    int ones = 0;
+            for (int v = tid; v < n; v += NT) {
+                int nv[D];
+                nbrs(v, nv);
+                int ones = 0;
 #pragma unroll
-                    for (int q = 0; q < D; ++q) ones += (int)bit_of(t - 1, nv[q]);
-                    nb = maj(ones, bit_of(t - 1, v));
-                }
-                const u64 m = __ballot(nb != 0);
-                if (lane < 2) lev[t * nw + (int)(v0 >> 5) + lane] = (uint32_t)(m >> (32 * lane));
+                for (int q = 0; q < D; ++q) ones += (int)(t == 1 ? bit_of(nv[q]) : lvl(t - 1, nv[q]));
+                const uint32_t nb = maj(ones, t == 1 ? bit_of(v) : lvl(t - 1, v));
+                mk[(t - 1) * mkl + v] = (MK)(nb << LVB);
             }
             __syncthreads();
         }
@@ -2013,7 +2012,7 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
         const int ipv = q_i[(pk + (uint32_t)(lane < NE ? lane : 0)) & 63u];
         const double u = q_u[(pk + (uint32_t)(act ? w : 0)) & 63u];
         iv = __builtin_amdgcn_readlane(ipv, act ? w : 0);
-        old_i = bit_of(0, iv);
+        old_i = bit_of(iv);
         int cand, nv[D];
         // ---- level 1: i and its neighbours, level 0 with i flipped
         {
@@ -2031,7 +2030,7 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
             const bool live = act && lane <= D && !dup;
             int ones = 0;
 #pragma unroll
-            for (int e = 0; e < D; ++e) ones += (int)(bit_of(0, nv[e]) ^ (nv[e] == iv));
+            for (int e = 0; e < D; ++e) ones += (int)(bit_of(nv[e]) ^ (nv[e] == iv));
 #pragma unroll
             for (int j = 0; j < NE - 1; ++j) {
                 // the earlier proposals' i (level-0 conflicts)
@@ -2041,9 +2040,9 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
                 for (int e = 0; e < D; ++e) hit |= nv[e] == ipj;
                 if (live && hit) cf |= 1u << j;
             }
-            const uint32_t own = bit_of(0, cand) ^ (cand == iv);
+            const uint32_t own = bit_of(cand) ^ (cand == iv);
             const uint32_t nb = maj(ones, own);
-            const uint32_t cur = bit_of(1, cand);
+            const uint32_t cur = lvl(1, cand);
             const bool chg = live && nb != cur;
             const u64 m = __ballot(chg);
             if (chg) {
@@ -2102,7 +2101,7 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
 #pragma unroll
                 for (int e = 0; e < D; ++e) rd_n[l][e] = nv2[e];
                 const uint32_t nb = maj(ones, own);
-                const uint32_t cur = bit_of(l, c2);
+                const uint32_t cur = lvl(l, c2);
                 const bool chg = act2 && nb != cur;
                 const uint32_t mb = mark_bit(c2);
                 bool add = chg;
@@ -2151,7 +2150,7 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
                         const uint32_t own = look(l - 1, cd, cfm);
                         const uint32_t nb = maj(ones, own);
                         const uint32_t mb = mark_bit(cd);
-                        cur = bit_of(l, cd);
+                        cur = lvl(l, cd);
                         if (nb != cur) add = (atomicOr(mark_word(l, cd), mb) & mb) == 0u;
                     }
                     const u64 bal = __ballot(add);
@@ -2272,7 +2271,9 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
         t += taken;                                                 // (code/SA_RRG.py:77,82)
         a = res_a[taken - 1];                                       // (:80-81) after the taken steps
         b = res_b[taken - 1];
-        // ---- the taken accepted proposals' changes; every proposal clears its marks
+        // ---- the taken accepted proposals' changes (the level bit of the mark set,
+        // its proposal bits cleared: the other proposals that marked the node clear
+        // only their own bits, atomically); every proposal clears its marks
         const bool mine = w < taken && ((accm >> w) & 1u);
         if (mine && lane == 0) atomicXor(&lev[iv >> 5], 1u << (iv & 31));
 #pragma unroll
@@ -2281,19 +2282,15 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
                 if (lc_fast[l]) {
                     if (lc_in[l]) {
                         const int v = lc_c[l];
-                        const uint32_t bt = 1u << (v & 31);
-                        if (mine) {
-                            if (lc_v[l]) atomicAnd(&lev[l * nw + (v >> 5)], ~bt);
-                            else atomicOr(&lev[l * nw + (v >> 5)], bt);
-                        }
-                        mk[(l - 1) * mkl + v] = 0;                  // every mark of the byte is this round's
+                        if (mine) mk[(l - 1) * mkl + v] = (MK)((lc_v[l] ^ 1u) << LVB);   // (repeats store alike)
+                        else atomicAnd(mark_word(l, v), ~mark_bit(v));
                     }
                 } else {
                     const uint32_t* cl = lst + l * lc;
                     for (int q = lane; q < lc_n[l]; q += 64) {
-                        const int v = (int)cl[q];
-                        if (mine) atomicXor(&lev[l * nw + (v >> 5)], 1u << (v & 31));
-                        mk[(l - 1) * mkl + v] = 0;
+                        const int v = (int)cl[q];      // (distinct: the list path dedups every level)
+                        if (mine) atomicXor(mark_word(l, v), mark_bit(v) | ((1u << LVB) << (MKB * (v & (MPW - 1)))));
+                        else atomicAnd(mark_word(l, v), ~mark_bit(v));
                     }
                 }
             }
