@@ -1810,6 +1810,8 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
     constexpr int LVB = MKB - 1;                   // the level value's bit in a mark (above NE proposals)
     static_assert(NE <= LVB, "a mark holds NE proposal bits and the level bit");
     const uint32_t obit = 1u << w;                 // this proposal's mark bit
+    const int b2s = lane / (D + 1), b2e = lane - b2s * (D + 1);   // level-0 ball lane: candidate, entry
+    const bool b2in = lane < (D + 1) * (D + 1);
     const uint32_t early = obit - 1u;              // the earlier proposals' mark bits
 
     auto bit_of = [&](int v) -> uint32_t { return (lev[v >> 5] >> (v & 31)) & 1u; };     // level 0
@@ -1990,6 +1992,8 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
         const bool act = w < nq;
         int iv = 0;
         uint32_t old_i = 0, cf = 0;                        // cf bit j: read something proposal j changed
+        uint32_t cf0 = 0;                                  // (level 0, wave-uniform)
+        int b2x = -1;                                      // this lane's node of the radius-2 ball
         int last = 0;
         int64_t ds = 0;
         // the nodes this wave read at each level l >= 2 (a candidate and its
@@ -2031,14 +2035,16 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
             int ones = 0;
 #pragma unroll
             for (int e = 0; e < D; ++e) ones += (int)(bit_of(nv[e]) ^ (nv[e] == iv));
+            // level-0 conflicts: the level-0 values read here are those of the
+            // ball of radius 2 around i, one node a lane (lane = (D+1) s + e: e-th
+            // entry of candidate s's closed neighbourhood; compared after the
+            // Metropolis test, off the level chain)
+            {
+                int cs = iv;
 #pragma unroll
-            for (int j = 0; j < NE - 1; ++j) {
-                // the earlier proposals' i (level-0 conflicts)
-                const int ipj = (act && j < w) ? __builtin_amdgcn_readlane(ipv, j) : -1;
-                bool hit = cand == ipj;
-#pragma unroll
-                for (int e = 0; e < D; ++e) hit |= nv[e] == ipj;
-                if (live && hit) cf |= 1u << j;
+                for (int q = 0; q < D; ++q)
+                    if (b2s == q + 1) cs = ri[q];
+                b2x = (b2e > 0) ? (int)rows[cs * 4 + b2e - 1] : cs;
             }
             const uint32_t own = bit_of(cand) ^ (cand == iv);
             const uint32_t nb = maj(ones, own);
@@ -2196,6 +2202,11 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
             acc = u < prob;
             tie = e < 1.0 && fabs(u - e) <= 4.0 * (nextafter(e, 2.0) - e);
         }
+        // an earlier proposal j conflicts at level 0 when i_j is in the ball (a
+        // ballot per j: a wave-uniform mask)
+        if (act)
+            for (int j = 0; j < w; ++j)
+                if (__ballot(b2in && b2x == __builtin_amdgcn_readlane(ipv, j))) cf0 |= 1u << j;
         LDS_STAMP(4);
         } else {
             // the parse wave: windows into the ring's free slots while the round evaluates
@@ -2213,10 +2224,15 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
             }
         }
         if (rd_all) cf |= early;
-        uint32_t cfw = 0;
-#pragma unroll
-        for (int j = 0; j < NE - 1; ++j)
-            if (__ballot((cf >> j) & 1u)) cfw |= 1u << j;
+        // the lanes' conflicts OR-ed: DPP row prefixes, the four row ends
+        cf |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)cf, 0x111, 0xf, 0xf, false);   // row_shr:1
+        cf |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)cf, 0x112, 0xf, 0xf, false);   // row_shr:2
+        cf |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)cf, 0x114, 0xf, 0xf, false);   // row_shr:4
+        cf |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)cf, 0x118, 0xf, 0xf, false);   // row_shr:8
+        const uint32_t cfw = cf0 | (uint32_t)__builtin_amdgcn_readlane((int)cf, 15) |
+                             (uint32_t)__builtin_amdgcn_readlane((int)cf, 31) |
+                             (uint32_t)__builtin_amdgcn_readlane((int)cf, 47) |
+                             (uint32_t)__builtin_amdgcn_readlane((int)cf, 63);
         if (lane == 0 && w < NE) {
             res_cf[w] = cfw;
             res[w] = (acc ? 1u : 0u) | (tie ? 2u : 0u) | ((uint32_t)(ds & 0xffff) << 16);
