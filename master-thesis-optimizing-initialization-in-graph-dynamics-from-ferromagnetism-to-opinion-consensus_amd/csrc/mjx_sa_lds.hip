@@ -114,7 +114,7 @@ __device__ __forceinline__ int64_t rl64(int64_t x, int l) {
 // s_memtime cycles of k_sa_lds_fast summed over waves; every stamp drains the
 // wave's counters first, so a phase's exposed latency is charged to it.
 #ifdef MJX_SA_PROF
-__device__ unsigned long long mjx_sa_lds_prof[8];
+__device__ unsigned long long mjx_sa_lds_prof[32];
 #define LDS_STAMP(k) do { __builtin_amdgcn_sched_barrier(0); asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); const unsigned long long _c = __builtin_amdgcn_s_memtime(); _acc[k] += _c - _t0; _t0 = _c; __builtin_amdgcn_sched_barrier(0); } while (0)
 #else
 #define LDS_STAMP(k) do {} while (0)
@@ -1810,8 +1810,7 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
     constexpr int LVB = MKB - 1;                   // the level value's bit in a mark (above NE proposals)
     static_assert(NE <= LVB, "a mark holds NE proposal bits and the level bit");
     const uint32_t obit = 1u << w;                 // this proposal's mark bit
-    const int b2s = lane / (D + 1), b2e = lane - b2s * (D + 1);   // level-0 ball lane: candidate, entry
-    const bool b2in = lane < (D + 1) * (D + 1);
+    const int l1 = (lane >= 1 && lane <= D) ? lane - 1 : 0;      // (clamped row entry)
     const uint32_t early = obit - 1u;              // the earlier proposals' mark bits
 
     auto bit_of = [&](int v) -> uint32_t { return (lev[v >> 5] >> (v & 31)) & 1u; };     // level 0
@@ -1974,7 +1973,10 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
     bool lc_fast[T + 1];
     int64_t k = 0;
 #ifdef MJX_SA_PROF
-    unsigned long long _acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, _t0 = __builtin_amdgcn_s_memtime();
+    // (32-bit sums: a launch's rounds fit; slot 8 this wave's levels + test, 9 the
+    // parse wave's parsing, 10 the barrier-1 wait; per-wave sums of slot 8 at 16 + w)
+    unsigned int _acc[11] = {};
+    unsigned long long _t0 = __builtin_amdgcn_s_memtime();
 #endif
     while (k < nsteps && done == 0) {
         if (w == NE) {
@@ -1993,7 +1995,7 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
         int iv = 0;
         uint32_t old_i = 0, cf = 0;                        // cf bit j: read something proposal j changed
         uint32_t cf0 = 0;                                  // (level 0, wave-uniform)
-        int b2x = -1;                                      // this lane's node of the radius-2 ball
+        int riq[D];                                        // i's neighbours
         int last = 0;
         int64_t ds = 0;
         // the nodes this wave read at each level l >= 2 (a candidate and its
@@ -2016,36 +2018,30 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
         const int ipv = q_i[(pk + (uint32_t)(lane < NE ? lane : 0)) & 63u];
         const double u = q_u[(pk + (uint32_t)(act ? w : 0)) & 63u];
         iv = __builtin_amdgcn_readlane(ipv, act ? w : 0);
+        int rj[D];                                         // lane j: proposal j's neighbours
+        nbrs(ipv, rj);
         old_i = bit_of(iv);
         int cand, nv[D];
         // ---- level 1: i and its neighbours, level 0 with i flipped
         {
             int ri[D];
             nbrs(iv, ri);
-            cand = iv;
+            // lane l in 1..D: i's l-th neighbour, by its own read (no per-lane selects)
+            const int c1 = (int)rows[iv * 4 + l1];
+            cand = (lane >= 1 && lane <= D) ? c1 : iv;
+            // a repeat of i or of an earlier lane's neighbour (multi-edges) is not live
+            int first = D;
 #pragma unroll
-            for (int q = 0; q < D; ++q)
-                if (lane == q + 1) cand = ri[q];
-            bool dup = lane > 0 && cand == iv;
-#pragma unroll
-            for (int q = 0; q < D; ++q)
-                if (q + 1 < lane) dup |= ri[q] == cand;
+            for (int q = D - 1; q >= 0; --q)
+                if (ri[q] == cand) first = q;
+            const bool dup = lane > 0 && (cand == iv || first + 1 < lane);
             nbrs(cand, nv);
             const bool live = act && lane <= D && !dup;
             int ones = 0;
 #pragma unroll
             for (int e = 0; e < D; ++e) ones += (int)(bit_of(nv[e]) ^ (nv[e] == iv));
-            // level-0 conflicts: the level-0 values read here are those of the
-            // ball of radius 2 around i, one node a lane (lane = (D+1) s + e: e-th
-            // entry of candidate s's closed neighbourhood; compared after the
-            // Metropolis test, off the level chain)
-            {
-                int cs = iv;
 #pragma unroll
-                for (int q = 0; q < D; ++q)
-                    if (b2s == q + 1) cs = ri[q];
-                b2x = (b2e > 0) ? (int)rows[cs * 4 + b2e - 1] : cs;
-            }
+            for (int q = 0; q < D; ++q) riq[q] = ri[q];
             const uint32_t own = bit_of(cand) ^ (cand == iv);
             const uint32_t nb = maj(ones, own);
             const uint32_t cur = lvl(1, cand);
@@ -2202,17 +2198,30 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
             acc = u < prob;
             tie = e < 1.0 && fabs(u - e) <= 4.0 * (nextafter(e, 2.0) - e);
         }
-        // an earlier proposal j conflicts at level 0 when i_j is in the ball (a
-        // ballot per j: a wave-uniform mask)
-        if (act)
-            for (int j = 0; j < w; ++j)
-                if (__ballot(b2in && b2x == __builtin_amdgcn_readlane(ipv, j))) cf0 |= 1u << j;
+        // level-0 conflicts: the level-0 values read here are those of the ball of
+        // radius 2 around i, and i_j is in it iff the closed neighbourhoods of i
+        // and i_j meet (lane j compares the two, off the level chain)
+        if (act) {
+            bool meet = ipv == iv;
+#pragma unroll
+            for (int e = 0; e < D; ++e) meet |= (rj[e] == iv) | (ipv == riq[e]);
+#pragma unroll
+            for (int e = 0; e < D; ++e)
+#pragma unroll
+                for (int f = 0; f < D; ++f) meet |= rj[e] == riq[f];
+            cf0 = (uint32_t)__ballot(meet) & early;
+        }
         LDS_STAMP(4);
+#ifdef MJX_SA_PROF
+        _acc[8] = _acc[1] + _acc[2] + _acc[3] + _acc[4];
+#endif
         } else {
             // the parse wave: windows into the ring's free slots while the round evaluates
             for (int it = 0; it < 2 && room() >= 8u; ++it) parse_window(room());
+            LDS_STAMP(9);
         }
         __syncthreads();                                   // every proposal's marks of every level
+        LDS_STAMP(10);
         // what this proposal read at level l-1 that an earlier one changed
 #pragma unroll
         for (int l = 2; l <= T; ++l) {
@@ -2319,8 +2328,10 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
 #endif
     }
 #ifdef MJX_SA_PROF
-    if (lane == 0)
-        for (int q = 0; q < 8; ++q) atomicAdd(&mjx_sa_lds_prof[q], _acc[q]);
+    if (lane == 0) {
+        for (int q = 0; q < 11; ++q) atomicAdd(&mjx_sa_lds_prof[q], (unsigned long long)_acc[q]);
+        atomicAdd(&mjx_sa_lds_prof[16 + w], (unsigned long long)_acc[8]);
+    }
 #endif
     if (TRACE && tid == 0) {
         for (; k < nsteps; ++k) {
@@ -2796,10 +2807,10 @@ using namespace mjx;
 
 #ifdef MJX_SA_PROF
 extern "C" int mjx_sa_lds_prof_read(unsigned long long* out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(salds::mjx_sa_lds_prof), 8 * sizeof(unsigned long long)) != hipSuccess)
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(salds::mjx_sa_lds_prof), 32 * sizeof(unsigned long long)) != hipSuccess)
         return MJX_EHIP;
     if (reset) {
-        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        unsigned long long z[32] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(salds::mjx_sa_lds_prof), z, sizeof(z)) != hipSuccess) return MJX_EHIP;
     }
     return MJX_OK;

@@ -22,7 +22,7 @@ for (p, c, kern) in ((1, 1, None), (1, 1, {"lds_pair": True}), (3, 1, None), (3,
     K = 20000
     sa.steps(K)
     torch.cuda.synchronize()
-    buf = (ctypes.c_ulonglong * 8)()
+    buf = (ctypes.c_ulonglong * 32)()
     raw.mjx_sa_lds_prof_read(buf, 1)
     t0 = time.perf_counter()
     sa.steps(K)

@@ -22,7 +22,7 @@ sa = mjx.SAReplicas(graphs, 1, 1, list(range(R)), layout="lds")
 K = 40000
 sa.steps(K)
 torch.cuda.synchronize()
-buf = (ctypes.c_ulonglong * 8)()
+buf = (ctypes.c_ulonglong * 32)()
 lib.mjx_sa_lds_prof_read(buf, 1)
 t0 = time.perf_counter()
 sa.steps(K)

@@ -14,7 +14,7 @@ import torch  # noqa: E402
 import mjx  # noqa: E402
 
 lib = mjx._lib.load()
-names = ["B0 (wave 0 parses)", "level 1", "level 2", "level 3", "dE+accept", "barrier+mark check+result+barrier",
+names = ["B0 (publish barrier)", "level 1", "level 2", "level 3", "dE+accept", "mark check+result+barrier",
          "resolve+apply"]
 n, d, R = 10_000, 4, 64
 graphs = [mjx.random_regular_graph(d, n, seed=7000 + k) for k in range(R)]
@@ -23,7 +23,7 @@ for (p, c, kern, nw) in ((3, 1, None, 16), (3, 1, {"split": 8}, 8), (2, 1, None,
     K = 20000
     sa.steps(K)
     torch.cuda.synchronize()
-    buf = (ctypes.c_ulonglong * 8)()
+    buf = (ctypes.c_ulonglong * 32)()
     lib.mjx_sa_lds_prof_read(buf, 1)
     t0 = time.perf_counter()
     sa.steps(K)
@@ -35,5 +35,8 @@ for (p, c, kern, nw) in ((3, 1, None, 16), (3, 1, {"split": 8}, 8), (2, 1, None,
     print(f"p={p} c={c} {kern or 'wg16'}: {1e6 * el / K:.3f} us/step, {K / rounds:.2f} proposals per round, "
           f"{1e6 * el / rounds:.3f} us per round; cycles per round per wave: "
           + ", ".join(f"{nm} {buf[q] / wave_rounds:.0f}" for q, nm in enumerate(names))
-          + f"; total {sum(buf[:7]) / wave_rounds:.0f}", flush=True)
+          + f"; total {sum(buf[:7]) / wave_rounds:.0f}; barrier-1 wait {buf[10] / wave_rounds:.0f}; "
+          f"parse wave parsing {buf[9] / (wave_rounds / nw):.0f}", flush=True)
+    print("  levels + test by wave: " + " ".join(f"{buf[16 + q] / (wave_rounds / nw):.0f}" for q in range(nw - 1)),
+          flush=True)
     del sa
