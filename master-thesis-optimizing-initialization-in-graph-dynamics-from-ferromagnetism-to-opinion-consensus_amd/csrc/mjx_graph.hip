@@ -357,6 +357,8 @@ struct Shape {
 };
 
 inline int64_t align256(int64_t x) { return (x + 255) & ~255ll; }
+constexpr int kChunk = 512;                     // phase-1 slots per wave load: 8 a lane; block starts aligned to it
+__host__ __device__ inline int64_t align_chunk(int64_t x) { return (x + kChunk - 1) & ~(int64_t)(kChunk - 1); }
 
 inline Shape shape(int64_t n, int d, int64_t rows) {
     Shape s;
@@ -364,7 +366,7 @@ inline Shape shape(int64_t n, int d, int64_t rows) {
     s.T = (rows + kTile - 1) >> kTileShift;
     s.S = s.K * s.T;
     s.slots = rows * d;
-    s.src_len = align256(s.slots + 7 * s.S) + 256 * s.K;     // segments padded to 8 slots, blocks to 256
+    s.src_len = align_chunk(s.slots + 7 * s.S) + kChunk * s.K;   // segments padded to 8 slots, blocks to kChunk
     s.off_len = s.slots + 8 * s.S + 8;
     s.index_len = (s.K + 1) + s.S + (s.S + 1);
     s.msg_words = s.src_len / 64 + 2;
@@ -428,7 +430,7 @@ __global__ void __launch_bounds__(256) k_bin_blockscan(const uint32_t* __restric
         carry += sh[255];
         __syncthreads();
     }
-    if (threadIdx.x == 0) blk[b] = (carry + 255) & ~255ll;
+    if (threadIdx.x == 0) blk[b] = align_chunk(carry);
 }
 
 // absolute phase-1 starts (b-major, for the fill) and their t-major copy
@@ -481,44 +483,49 @@ __global__ void k_bin_pack(const int32_t* __restrict__ src32, int64_t chunks, ui
 
 // ---- the sweep ----------------------------------------------------------------
 
-// UC chunks of a wave's phase-1 stream: lane l holds slots 4l..4l+3 of each
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+
+// UC chunks of a wave's phase-1 stream: lane l holds slots 8l..8l+7 of each
+// (one 16-B load of 16-bit word indices, one 4-B load of eight 4-bit bit
+// positions; streamed once, so non-temporal)
 template <int UC>
 struct MsgGroup {
     static constexpr int NW = kMsgThreads / 64;
-    uint2 l[UC];       // four 16-bit state-word indices
-    unsigned h[UC];    // four 4-bit bit positions
+    v4u l[UC];         // eight 16-bit state-word indices
+    unsigned h[UC];    // eight 4-bit bit positions
     // chunks c, c + NW, ... (clamped to the wave's last chunk: always a valid
     // load); c and last are wave-uniform, so every address is a scalar base
     // plus the lane's constant offset
-    __device__ __forceinline__ void fetch(const uint2* __restrict__ lo2, const uint16_t* __restrict__ src_hi,
+    __device__ __forceinline__ void fetch(const v4u* __restrict__ lo4, const unsigned* __restrict__ hi4,
                                           int64_t c, int64_t last, int lane) {
 #pragma unroll
         for (int u = 0; u < UC; ++u) {
             const int64_t cc = (c + u * NW <= last) ? c + u * NW : last;
-            const uint2* pl = lo2 + cc * 64;
-            const uint16_t* ph = src_hi + cc * 64;
-            l[u] = pl[lane];
-            h[u] = ph[lane];
+            l[u] = __builtin_nontemporal_load(lo4 + cc * 64 + lane);
+            h[u] = __builtin_nontemporal_load(hi4 + cc * 64 + lane);
         }
     }
-    // message bits of chunks c, c + NW, ... below a1: lane l's four bits are
-    // bits 4l..4l+3 of its chunk, so three DPP row shifts assemble 32-bit
-    // words in lanes 0, 8, .., 56 (no ballots, no lane selects)
+    // message bits of chunks c, c + NW, ... below a1: lane l's byte is bits
+    // 8l..8l+7 of its chunk, so two DPP row shifts assemble 32-bit words in
+    // lanes 0, 4, .., 60 (no ballots, no lane selects)
     __device__ __forceinline__ void emit(const uint16_t* sb16, int64_t c, int64_t a1, int lane,
                                          uint32_t* __restrict__ msg32) const {
 #pragma unroll
         for (int u = 0; u < UC; ++u) {
-            const unsigned x = l[u].x, y = l[u].y, hh = h[u];
-            const unsigned v0 = sb16[x & 0xffffu], v1 = sb16[x >> 16];
-            const unsigned v2 = sb16[y & 0xffffu], v3 = sb16[y >> 16];
-            unsigned m = __builtin_amdgcn_ubfe(v0, hh & 15u, 1) | (__builtin_amdgcn_ubfe(v1, (hh >> 4) & 15u, 1) << 1) |
-                         (__builtin_amdgcn_ubfe(v2, (hh >> 8) & 15u, 1) << 2) | (__builtin_amdgcn_ubfe(v3, hh >> 12, 1) << 3);
+            const unsigned hh = h[u];
+            unsigned m = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const unsigned x = l[u][q];
+                const unsigned v0 = sb16[x & 0xffffu], v1 = sb16[x >> 16];
+                m |= (__builtin_amdgcn_ubfe(v0, (hh >> (8 * q)) & 15u, 1) << (2 * q)) |
+                     (__builtin_amdgcn_ubfe(v1, (hh >> (8 * q + 4)) & 15u, 1) << (2 * q + 1));
+            }
             // row_shl:k (dpp_ctrl 0x100 + k): lane i reads lane i + k of its 16-lane row
-            m |= (unsigned)__builtin_amdgcn_mov_dpp((int)m, 0x101, 0xf, 0xf, true) << 4;
-            m |= (unsigned)__builtin_amdgcn_mov_dpp((int)m, 0x102, 0xf, 0xf, true) << 8;
-            m |= (unsigned)__builtin_amdgcn_mov_dpp((int)m, 0x104, 0xf, 0xf, true) << 16;
+            m |= (unsigned)__builtin_amdgcn_mov_dpp((int)m, 0x101, 0xf, 0xf, true) << 8;
+            m |= (unsigned)__builtin_amdgcn_mov_dpp((int)m, 0x102, 0xf, 0xf, true) << 16;
             const int64_t cc = c + u * NW;
-            if ((lane & 7) == 0 && cc < a1) msg32[cc * 8 + (lane >> 3)] = m;
+            if ((lane & 3) == 0 && cc < a1) msg32[cc * 16 + (lane >> 2)] = m;
         }
     }
 };
@@ -527,7 +534,7 @@ struct MsgGroup {
 // workgroups share a block (each stages the block's 128 KB of state bits).
 // UC chunks per wave step, loaded unconditionally (a step's last chunks are
 // clamped to the wave's last one and not stored) so that every load of a step
-// is in flight before the first ballot.
+// is in flight before the first lookup.
 template <int UC>
 __global__ void __launch_bounds__(kMsgThreads) k_bin_msg(const uint16_t* __restrict__ src_lo,
                                                          const uint16_t* __restrict__ src_hi,
@@ -557,29 +564,27 @@ __global__ void __launch_bounds__(kMsgThreads) k_bin_msg(const uint16_t* __restr
         for (int k = 0; k < V; ++k) reinterpret_cast<uint4*>(sb)[threadIdx.x + k * kMsgThreads] = x[k];
     }
     __syncthreads();
-    const int64_t c0 = blk[b] >> 8, c1 = blk[b + 1] >> 8;   // 256-slot chunks of this block
+    const int64_t c0 = blk[b] / kChunk, c1 = blk[b + 1] / kChunk;   // this block's chunks
     const int64_t per = (c1 - c0 + split - 1) / split;
     const int64_t a0 = c0 + part * per;
     const int64_t a1 = (a0 + per < c1) ? a0 + per : c1;
     constexpr int NW = kMsgThreads / 64;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const uint2* lo2 = reinterpret_cast<const uint2*>(src_lo);
+    const v4u* lo4 = reinterpret_cast<const v4u*>(src_lo);
+    const unsigned* hi4 = reinterpret_cast<const unsigned*>(src_hi);
     // this wave's chunks: a0 + wave + NW*i
     const int64_t last = (a1 - 1 - a0 - wave >= 0) ? a0 + wave + ((a1 - 1 - a0 - wave) / NW) * NW : -1;
     const uint16_t* sb16 = reinterpret_cast<const uint16_t*>(sb);
     uint32_t* msg32 = reinterpret_cast<uint32_t*>(msg);
     // two groups in flight: the loads of group i+1 are issued before the
-    // lookups of group i (unrolled by two, so no register copies wait on them);
-    // 3.40 -> 3.35 ms per sweep at N=1e9, d=6 (UC 2: 3.53, UC 8: 3.37).  With
-    // the LDS lookups removed (timing build) the kernel takes the same time:
-    // it is bound by the stream, not by the lookups or the VALU work.
+    // lookups of group i (unrolled by two, so no register copies wait on them)
     if (last < 0) return;
     MsgGroup<UC> ga, gb;
-    ga.fetch(lo2, src_hi, a0 + wave, last, lane);
+    ga.fetch(lo4, hi4, a0 + wave, last, lane);
     for (int64_t c = a0 + wave; c < a1; c += 2 * UC * NW) {
-        gb.fetch(lo2, src_hi, c + UC * NW, last, lane);
+        gb.fetch(lo4, hi4, c + UC * NW, last, lane);
         ga.emit(sb16, c, a1, lane, msg32);
-        ga.fetch(lo2, src_hi, c + 2 * UC * NW, last, lane);
+        ga.fetch(lo4, hi4, c + 2 * UC * NW, last, lane);
         gb.emit(sb16, c + UC * NW, a1, lane, msg32);
     }
 }
