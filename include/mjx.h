@@ -454,9 +454,10 @@ int mjx_sweep_ell_np_range(const int32_t* adj, int64_t n, int d, int64_t row_lo,
  * static plan bins the (row_hi-row_lo)*d (destination, source) slots by source
  * block (1M nodes, staged in LDS) and destination tile (64K nodes, LDS byte
  * counters); a sweep is two streaming kernels (messages, then counts + rule).
- * mjx_binned_plan_shape fills sizes[6] = {src_lo_len, src_hi_len, off_len
- * (uint16 elements each), index_len (int64 elements), msg_words (uint64
- * per-sweep message bits), work_bytes (device scratch for mjx_binned_build)}.
+ * mjx_binned_plan_shape fills sizes[6] = {src_lo_len (the phase-1 stream),
+ * src_hi_len (0: src_hi is unused and may be NULL), off_len (uint16 elements
+ * each), index_len (int64 elements), msg_words (uint64 per-sweep message
+ * bits), work_bytes (device scratch for mjx_binned_build)}.
  * Limits: n <= 2^31-1, d <= 16; row_lo a multiple of 64, row_hi too unless
  * row_hi == n.  adj holds the rows' ELL entries (global node ids).  */
 int mjx_binned_plan_shape(int64_t n, int d, int64_t row_lo, int64_t row_hi, int64_t* sizes);

@@ -325,12 +325,15 @@ extern "C" int mjx_graph_check_ell(const int32_t* adj, int64_t n, int d, unsigne
 // instead of one random line per slot.
 //
 // Plan (sizes from mjx_binned_plan_shape):
-//   src_lo uint16[src_len]   phase-1 order; segment starts padded to 8 slots,
-//                            block starts to 256 slots: slot j's source offset
-//                            (20 bits within its block) >> 4, i.e. the index of
-//                            the 16-bit state word that holds its bit;
-//   src_hi uint16[src_len/4] the bit within that word (offset & 15) of slots
-//                            4i..4i+3 in entry i (nibble k = slot 4i+k);
+//   src_lo uint16[src_len/512*640]  the phase-1 stream, in 512-slot chunks
+//                            (segment starts padded to 8 slots, block starts to
+//                            512): per chunk 512 entries = each slot's source
+//                            offset (20 bits within its block) >> 4, i.e. the
+//                            index of the 16-bit state word that holds its bit,
+//                            then 128 entries = the bit within that word
+//                            (offset & 15) of slots 4i..4i+3 in entry i (nibble
+//                            k = slot 4i+k): one contiguous 1280-B piece;
+//   src_hi                   unused (size 0; may be NULL);
 //   off   uint16[off_len] phase-2 order; segment starts padded to 8 slots;
 //   index int64           blk[K+1]  phase-1 padded block starts |
 //                         p1T[S]    phase-1 start of segment (b,t), at t*K+b |
@@ -466,18 +469,22 @@ __global__ void __launch_bounds__(256) k_bin_fill(const int32_t* __restrict__ ad
     }
 }
 
-// int32 source offsets (20 bits) -> 16-bit state-word indices + 4-bit bit positions
-__global__ void k_bin_pack(const int32_t* __restrict__ src32, int64_t chunks, uint16_t* __restrict__ lo,
-                           uint16_t* __restrict__ hi) {
-    const int64_t quads = chunks * 64;
+// int32 source offsets (20 bits) -> the phase-1 stream: per 512-slot chunk
+// 1024 B of 16-bit state-word indices then 256 B of 4-bit bit positions (one
+// contiguous 1280-B piece per chunk, kChunkU16 entries)
+constexpr int kChunkU16 = kChunk + kChunk / 4;
+__global__ void k_bin_pack(const int32_t* __restrict__ src32, int64_t chunks, uint16_t* __restrict__ stream) {
+    const int64_t quads = chunks * (kChunk / 4);
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < quads; i += (int64_t)gridDim.x * blockDim.x) {
         const int4 x = reinterpret_cast<const int4*>(src32)[i];
+        const int64_t c = i / (kChunk / 4), q = i - c * (kChunk / 4);
+        uint16_t* ch = stream + c * kChunkU16;
         uint2 l;
         l.x = ((unsigned)x.x >> 4) | (((unsigned)x.y >> 4) << 16);
         l.y = ((unsigned)x.z >> 4) | (((unsigned)x.w >> 4) << 16);
-        reinterpret_cast<uint2*>(lo)[i] = l;
-        hi[i] = (uint16_t)(((unsigned)x.x & 15u) | (((unsigned)x.y & 15u) << 4) | (((unsigned)x.z & 15u) << 8) |
-                           (((unsigned)x.w & 15u) << 12));
+        reinterpret_cast<uint2*>(ch)[q] = l;
+        ch[kChunk + q] = (uint16_t)(((unsigned)x.x & 15u) | (((unsigned)x.y & 15u) << 4) |
+                                    (((unsigned)x.z & 15u) << 8) | (((unsigned)x.w & 15u) << 12));
     }
 }
 
@@ -496,13 +503,13 @@ struct MsgGroup {
     // chunks c, c + NW, ... (clamped to the wave's last chunk: always a valid
     // load); c and last are wave-uniform, so every address is a scalar base
     // plus the lane's constant offset
-    __device__ __forceinline__ void fetch(const v4u* __restrict__ lo4, const unsigned* __restrict__ hi4,
-                                          int64_t c, int64_t last, int lane) {
+    __device__ __forceinline__ void fetch(const uint16_t* __restrict__ stream, int64_t c, int64_t last, int lane) {
 #pragma unroll
         for (int u = 0; u < UC; ++u) {
             const int64_t cc = (c + u * NW <= last) ? c + u * NW : last;
-            l[u] = __builtin_nontemporal_load(lo4 + cc * 64 + lane);
-            h[u] = __builtin_nontemporal_load(hi4 + cc * 64 + lane);
+            const uint16_t* ch = stream + cc * kChunkU16;
+            l[u] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(ch) + lane);
+            h[u] = __builtin_nontemporal_load(reinterpret_cast<const unsigned*>(ch + kChunk) + lane);
         }
     }
     // message bits of chunks c, c + NW, ... below a1: lane l's byte is bits
@@ -570,8 +577,6 @@ __global__ void __launch_bounds__(kMsgThreads) k_bin_msg(const uint16_t* __restr
     const int64_t a1 = (a0 + per < c1) ? a0 + per : c1;
     constexpr int NW = kMsgThreads / 64;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const v4u* lo4 = reinterpret_cast<const v4u*>(src_lo);
-    const unsigned* hi4 = reinterpret_cast<const unsigned*>(src_hi);
     // this wave's chunks: a0 + wave + NW*i
     const int64_t last = (a1 - 1 - a0 - wave >= 0) ? a0 + wave + ((a1 - 1 - a0 - wave) / NW) * NW : -1;
     const uint16_t* sb16 = reinterpret_cast<const uint16_t*>(sb);
@@ -580,11 +585,11 @@ __global__ void __launch_bounds__(kMsgThreads) k_bin_msg(const uint16_t* __restr
     // lookups of group i (unrolled by two, so no register copies wait on them)
     if (last < 0) return;
     MsgGroup<UC> ga, gb;
-    ga.fetch(lo4, hi4, a0 + wave, last, lane);
+    ga.fetch(src_lo, a0 + wave, last, lane);
     for (int64_t c = a0 + wave; c < a1; c += 2 * UC * NW) {
-        gb.fetch(lo4, hi4, c + UC * NW, last, lane);
+        gb.fetch(src_lo, c + UC * NW, last, lane);
         ga.emit(sb16, c, a1, lane, msg32);
-        ga.fetch(lo4, hi4, c + 2 * UC * NW, last, lane);
+        ga.fetch(src_lo, c + 2 * UC * NW, last, lane);
         gb.emit(sb16, c + UC * NW, a1, lane, msg32);
     }
 }
@@ -897,8 +902,8 @@ extern "C" int mjx_binned_plan_shape(int64_t n, int d, int64_t row_lo, int64_t r
     const int rc = check_range(n, d, row_lo, row_hi);
     if (rc) return rc;
     const Shape s = shape(n, d, row_hi - row_lo);
-    sizes[0] = s.src_len;
-    sizes[1] = s.src_len / 4;
+    sizes[0] = s.src_len / kChunk * kChunkU16;       // the phase-1 stream (src_lo; src_hi unused)
+    sizes[1] = 0;
     sizes[2] = s.off_len;
     sizes[3] = s.index_len;
     sizes[4] = s.msg_words;
@@ -914,7 +919,7 @@ extern "C" int mjx_binned_build(const int32_t* adj, int64_t n, int d, int64_t ro
     if (rc) return rc;
     const int64_t rows = row_hi - row_lo;
     if (rows == 0) return MJX_OK;
-    if (!adj || !src_lo || !src_hi || !off || !index || !work) return MJX_EINVAL;
+    if (!adj || !src_lo || !off || !index || !work) return MJX_EINVAL;
     const Shape s = shape(n, d, rows);
     if (work_bytes < s.work_bytes) return MJX_ERANGE;
     const int64_t K = s.K, T = s.T, S = s.S;
@@ -946,7 +951,7 @@ extern "C" int mjx_binned_build(const int32_t* adj, int64_t n, int d, int64_t ro
     MJX_LAUNCH_CHECK("k_bin_finish");
     k_bin_fill<<<(unsigned)T, 256, K * sizeof(unsigned), st>>>(adj, rows, d, n, K, T, p1, p2, src, off);
     MJX_LAUNCH_CHECK("k_bin_fill");
-    k_bin_pack<<<mjx::grid_for(s.src_len / 4), 256, 0, st>>>(src, s.src_len / 256, src_lo, src_hi);
+    k_bin_pack<<<mjx::grid_for(s.src_len / 4), 256, 0, st>>>(src, s.src_len / kChunk, src_lo);
     MJX_LAUNCH_CHECK("k_bin_pack");
     return MJX_OK;
 }
@@ -960,7 +965,7 @@ extern "C" int mjx_sweep_binned(const uint16_t* src_lo, const uint16_t* src_hi, 
     if (rc) return rc;
     if (apply_form < 0 || apply_form > 2) return MJX_EINVAL;
     if (row_hi == row_lo) return MJX_OK;
-    if (!src_lo || !src_hi || !off || !index || !s_in || !msg || !s_out || s_in == s_out) return MJX_EINVAL;
+    if (!src_lo || !off || !index || !s_in || !msg || !s_out || s_in == s_out) return MJX_EINVAL;
     const Shape s = shape(n, d, row_hi - row_lo);
     const long long* blk = index;
     const long long* p1T = index + (s.K + 1);
