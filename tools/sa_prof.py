@@ -11,8 +11,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import mjx  # noqa: E402
 
-lib = mjx.load_library()
-raw = ctypes.CDLL(mjx.lib_path())
+raw = mjx._lib.load()                      # (the variant under tools/ab_lib.py)
 names = ["tape+rows(i,A0)+tree", "rows(C)+sectors+lvl1", "gc words+lvl2", "hash lookups", "resolve+flips+drain",
          "hash clear", "hash inserts", "fence"]
 n, d, p, c = 1_000_000, 3, 2, 1
