@@ -180,6 +180,16 @@ typedef struct mjx_sa_state {
     int32_t   opt_split;   /* waves per 64-replica word column: 1, 2, 4, ..., 64 */
     int32_t   opt_spec_k;  /* speculative batch width: 8 or 16 */
     uint32_t  opt_flags;   /* MJX_SA_NO_SPEC | MJX_SA_NO_CONE2 | MJX_SA_LDS_* */
+    /* nullable: the NON-parity proposal stream.  When set,
+     * the tape of mjx_sa_lightcone_steps / _cone_steps / _rec_steps (tape_cap
+     * > 0, required) is drawn by Philox-4x32-10 instead of the MT19937 replay:
+     * the proposal of step t of replica r is philox4x32_10(counter (t_lo,
+     * t_hi, 0, 0), key (k_lo, k_hi)) with k = philox_key[r]: i = the high 64
+     * bits of (x0 | x1 << 32) * n, u = (x2 >> 5, x3 >> 6) as numpy's rand().
+     * A pure function of (key, t): any chunking, any kernel, same run.  The
+     * steps that draw inside the kernel (mjx_sa_steps, mjx_sa_lds_steps)
+     * refuse it (MJX_EINVAL). */
+    const uint64_t* philox_key;   /* [R] */
 } mjx_sa_state;
 
 #define MJX_SA_NO_SPEC   1u   /* no speculative batches (k_sa_spec) */

@@ -125,7 +125,7 @@ class MjxSaState(ctypes.Structure):
         ("tr_i", c_vp), ("tr_acc", c_vp), ("tr_sum", c_vp), ("tr_dE", c_vp), ("tr_tie", c_vp),
         ("tape_i", c_vp), ("tape_u", c_vp), ("tape_cap", c_i64),
         ("rep_graph", c_vp), ("opt_split", ctypes.c_int32), ("opt_spec_k", ctypes.c_int32),
-        ("opt_flags", ctypes.c_uint32),
+        ("opt_flags", ctypes.c_uint32), ("philox_key", c_vp),
     ]
 
 

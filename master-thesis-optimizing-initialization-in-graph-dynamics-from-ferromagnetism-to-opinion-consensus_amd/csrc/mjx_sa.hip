@@ -792,15 +792,21 @@ __device__ bool lc_tree2(const int32_t* __restrict__ adj, int64_t W, int64_t col
 }
 
 // (i_t, u_t) tape of K proposals per running replica (code/SA_RRG.py:73,76):
-// wave per replica, its MT19937 state twisted in LDS; the draws are consumed
-// serially (uniform across the wave) exactly as k_sa_lightcone would.  The
-// stream does not depend on accept decisions, so the tape can run ahead of the
-// steps; a replica that finishes inside the tape leaves its tail unused.
+// wave per replica, its MT19937 state twisted in LDS.  The stream does not
+// depend on accept decisions, so the tape can run ahead of the steps; a replica
+// that finishes inside the tape leaves its tail unused.  The draws are parsed
+// a 64-word window at a time, lane-parallel (as the whole-CU LDS kernels parse
+// them): every lane tempers one word and tests randint's masked rejection; a
+// scalar walk over the ballot finds the proposal starts (the first acceptable
+// word at or after the previous proposal's end, then rand()'s two words); the
+// start lanes write their proposals' tape entries.  A proposal whose words
+// cross the end of the state is drawn serially across the twist, as numpy does.
 __global__ void __launch_bounds__(64) k_sa_tape(int64_t n, int64_t R, int64_t K, mjx_sa_state st,
                                                 int32_t* __restrict__ tape_i, double* __restrict__ tape_u) {
     __shared__ uint32_t buf[MT_N];
     const int64_t r = blockIdx.x;
     const int lane = threadIdx.x;
+    const u64 ltmask = (1ull << lane) - 1ull;
     if (st.done[r]) return;
     uint32_t* g = st.mt + r * MT_N;
     for (int k = lane; k < MT_N; k += 64) buf[k] = ld_nc(g + k);
@@ -810,30 +816,119 @@ __global__ void __launch_bounds__(64) k_sa_tape(int64_t n, int64_t R, int64_t K,
     const uint64_t rng = (uint64_t)(n - 1);
     uint32_t mask = (uint32_t)rng;
     mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
-    auto next = [&]() -> uint32_t {
+    auto twist_if_end = [&]() {
         if (idx >= MT_N) {
             lds_twist(buf, lane);
             idx = 0;
         }
-        return mt_temper(buf[idx++]);
     };
-    for (int64_t k = 0; k < K; ++k) {
-        uint32_t i = 0;
-        if (rng > 0) {
-            for (;;) {
-                const uint32_t v = next() & mask;
-                if (v <= (uint32_t)rng) { i = v; break; }
+    int64_t k = 0;
+    if (rng == 0) {
+        // n = 1: randint(0, 1) draws nothing; rand() two words a proposal
+        for (; k < K; ++k) {
+            twist_if_end();
+            const uint32_t w1 = mt_temper(buf[idx++]);
+            twist_if_end();
+            const uint32_t w2 = mt_temper(buf[idx++]);
+            if (lane == 0) {
+                tape_i[k * R + r] = 0;
+                tape_u[k * R + r] = mt_double(w1, w2);
             }
         }
-        const uint32_t w1 = next();
-        const uint32_t w2 = next();
+    }
+    while (k < K) {
+        twist_if_end();
+        const int lim = (MT_N - idx < 64) ? MT_N - idx : 64;
+        uint32_t tw = 0, y = 0;
+        bool ok = false;
+        if (lane < lim) {
+            tw = mt_temper(buf[idx + lane]);
+            y = tw & mask;
+            ok = y <= (uint32_t)rng;
+        }
+        const u64 okm = __ballot(ok);
+        u64 stm = 0;
+        int pos = 0;
+        int64_t got = 0;
+        while (pos < 64 && k + got < K) {
+            const u64 m = okm >> pos;
+            if (!m) break;
+            const int f = pos + __ffsll((unsigned long long)m) - 1;
+            if (f + 2 >= lim) break;
+            stm |= 1ull << f;
+            ++got;
+            pos = f + 3;
+        }
+        if (got > 0) {
+            const uint32_t x1 = (uint32_t)__builtin_amdgcn_ds_bpermute(((lane + 1) & 63) * 4, (int)tw);
+            const uint32_t x2 = (uint32_t)__builtin_amdgcn_ds_bpermute(((lane + 2) & 63) * 4, (int)tw);
+            if ((stm >> lane) & 1ull) {
+                const int64_t j = k + __popcll(stm & ltmask);
+                tape_i[j * R + r] = (int32_t)y;
+                tape_u[j * R + r] = mt_double(x1, x2);
+            }
+            k += got;
+            idx += pos;
+            continue;
+        }
+        if (!okm) { idx += lim; continue; }
+        const int f = __ffsll((unsigned long long)okm) - 1;
+        if (f > 0) { idx += f; continue; }
+        // i is the window's first word and rand()'s two words cross the end of
+        // the state: the serial draw twists between them
+        const int32_t iv = __builtin_amdgcn_readlane((int)y, 0);
+        idx += 1;
+        twist_if_end();
+        const uint32_t w1 = mt_temper(buf[idx++]);
+        twist_if_end();
+        const uint32_t w2 = mt_temper(buf[idx++]);
         if (lane == 0) {
-            tape_i[k * R + r] = (int32_t)i;
+            tape_i[k * R + r] = iv;
             tape_u[k * R + r] = mt_double(w1, w2);
         }
+        ++k;
     }
-    for (int k = lane; k < MT_N; k += 64) g[k] = buf[k];
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    for (int q = lane; q < MT_N; q += 64) g[q] = buf[q];
     if (lane == 0) st.mt_idx[r] = idx;
+}
+
+// Philox-4x32-10 (Salmon et al., SC'11; Random123's philox4x32_10): the
+// NON-parity proposal stream (mjx_sa_state.philox_key).  Ten
+// rounds of two 32x32->64 multiplies, the key bumped by the Weyl constants
+// between rounds; oracle/orc_majority.c's orc_philox4x32_10 is the checker.
+__device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
+                                              uint32_t k1, uint32_t (&x)[4]) {
+#pragma unroll
+    for (int q = 0; q < 10; ++q) {
+        if (q > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+        const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+        const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    }
+    x[0] = c0; x[1] = c1; x[2] = c2; x[3] = c3;
+}
+
+// the Philox tape: entry (k, r) = the proposal of step t_r + k of replica r
+// (counter (t lo, t hi, 0, 0), key = philox_key[r]): i = the high 64 bits of
+// (x0 | x1 << 32) * n, u = numpy rand()'s 53-bit double of (x2, x3).  One
+// thread an entry, row k of the tape = k * R + r: coalesced, no state to
+// carry (the step count is the counter).
+__global__ void __launch_bounds__(256) k_sa_tape_philox(int64_t n, int64_t R, int64_t K, mjx_sa_state st,
+                                                        int32_t* __restrict__ tape_i, double* __restrict__ tape_u) {
+    const int64_t total = K * R;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t k = e / R, r = e - k * R;
+        if (st.done[r]) continue;
+        const uint64_t t = (uint64_t)(st.t[r] + k), key = st.philox_key[r];
+        uint32_t x[4];
+        philox4x32_10((uint32_t)t, (uint32_t)(t >> 32), 0u, 0u, (uint32_t)key, (uint32_t)(key >> 32), x);
+        const uint64_t w = (uint64_t)x[0] | ((uint64_t)x[1] << 32);
+        tape_i[e] = (int32_t)__umul64hi(w, (uint64_t)n);
+        tape_u[e] = mt_double(x[2], x[3]);
+    }
 }
 
 template <int D, bool TAPE>
@@ -1516,7 +1611,8 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
     // the next batch's proposals (pos + K + k: every proposal of this batch
     // consumed, the usual case) and the rows of their balls are fetched while
     // this batch evaluates and resolves: the tape entry at its start, the row of
-    // i after the evaluation, the rows of i's neighbours after the hash phase.
+    // i behind this batch's first loads, the rows of i's neighbours after the
+    // evaluation (each lands under a later phase of this batch).
     // A batch that consumed fewer than K (a conflict, a non-tree ball, a stop)
     // fetches its own afresh.  Three dependent round trips per batch fewer.
     int64_t pf_pos = -1;
@@ -1599,7 +1695,9 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
         uint32_t ch1 = 0, nv1 = 0, ch2 = 0;      // positions: 0 = i, 1+m = a_m, 1+D+m*D+x = child
         bool listpath = false;
         int cnt[LC_MAXT + 1] = {0, 0, 0, 0, 0, 0, 0};
-        if (mine && ok) {
+        u64 wi[3], wa[D][3], wc[D][D][3], wg[D][D][D];
+        const bool tree = mine && ok;
+        if (tree) {
             // rows of the children (T = 2) and the level sectors of i, the a_m and
             // the children in one batch
             if constexpr (TT == 2) {
@@ -1609,7 +1707,6 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
                     for (int x = 0; x < D; ++x)
                         if (A1[m][x] != i) row(A1[m][x], C[m][x]);
             }
-            u64 wi[3], wa[D][3], wc[D][D][3], wg[D][D][D];
             sector(i, wi);
 #pragma unroll
             for (int m = 0; m < D; ++m) {
@@ -1620,6 +1717,14 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
                     if (A1[m][x] != i) sector(A1[m][x], wc[m][x]);
                 }
             }
+        }
+        // the next batch: the row of its i (its tape entry landed with this
+        // batch's first loads), in flight while this batch evaluates
+        int32_t n_A0[D], n_A1[D][D];
+        __builtin_amdgcn_sched_barrier(0);
+        row(n_i, n_A0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (tree) {
             const uint32_t f = bv(wi[0]) ^ 1u;
             old_i = (int)bv(wi[0]);
             {
@@ -1698,9 +1803,10 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
             else ds = lc_delta_mlp<D, false>(adj, NS, colo, bit, T, L, lists, i, cnt, &old_i, A0, A1);
         }
         SA_STAMP(2);
-        // the next batch: the row of its i
-        int32_t n_A0[D], n_A1[D][D];
-        row(n_i, n_A0);
+        // the next batch: the rows of its i's neighbours (land during the hash
+        // phase and the resolution)
+#pragma unroll
+        for (int m = 0; m < D; ++m) row(n_A0[m], n_A1[m]);
         // potential writes of every proposal into the replica's hash set
         constexpr int NTW = 1 + D + D * D;                  // tree positions: i, the a_m, their children
         if (mine && listpath) {
@@ -1769,9 +1875,6 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
             stands = !hit;
         }
         SA_STAMP(3);
-        // the next batch: the rows of its i's neighbours (land during the resolution)
-#pragma unroll
-        for (int m = 0; m < D; ++m) row(n_A0[m], n_A1[m]);
         // resolution: J0 = first proposal that does not stand
         const int gs = g * K;
         const uint32_t nst = (uint32_t)((__ballot(!stands) >> gs) & GM);
@@ -2001,6 +2104,7 @@ extern "C" int mjx_sa_steps(const int32_t* adj, int64_t n, int d, int p, int c, 
                             double par_b, double a_cap, double b_cap, int64_t t_cap, void* stream) {
     if (!stp || n < 2 || R < 1 || d < 1 || p < 0 || c < 0 || p + c < 1 || !adj || !s || !tmp1 || nsteps < 0)
         return MJX_EINVAL;
+    if (stp->philox_key) return MJX_EINVAL;             // draws the MT19937 replay inside the step
     if (n > (int64_t)INT32_MAX) return MJX_ERANGE;
     mjx_sa_state st = *stp;
     const int64_t W = (R + 63) / 64;
@@ -2074,6 +2178,7 @@ static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d
     hipStream_t hs = as_stream(stream);
     const mjx_sa_state st = *stp;
     const bool tape = st.tape_i && st.tape_u && st.tape_cap > 0;
+    if (st.philox_key && !tape) return MJX_EINVAL;       // the Philox stream is drawn into the tape
     const int split = st.opt_split ? st.opt_split : lc_split(W, lds);
     if (split < 1 || split > 64 || (64 % split)) return MJX_EINVAL;
     if (st.opt_spec_k != 0 && st.opt_spec_k != 8 && st.opt_spec_k != 16) return MJX_EINVAL;
@@ -2135,8 +2240,15 @@ static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d
         if (!tape) return launch(kern_plain, st, nsteps);
         for (int64_t k0 = 0; k0 < nsteps; k0 += st.tape_cap) {
             const int64_t k = (nsteps - k0 < st.tape_cap) ? nsteps - k0 : st.tape_cap;
-            k_sa_tape<<<(unsigned)R, 64, 0, hs>>>(n, R, k, st, st.tape_i, st.tape_u);
-            MJX_LAUNCH_CHECK("k_sa_tape");
+            if (st.philox_key) {
+                const int64_t blocks = (k * R + 255) / 256;
+                k_sa_tape_philox<<<(unsigned)(blocks < 65536 ? blocks : 65536), 256, 0, hs>>>(n, R, k, st, st.tape_i,
+                                                                                              st.tape_u);
+                MJX_LAUNCH_CHECK("k_sa_tape_philox");
+            } else {
+                k_sa_tape<<<(unsigned)R, 64, 0, hs>>>(n, R, k, st, st.tape_i, st.tape_u);
+                MJX_LAUNCH_CHECK("k_sa_tape");
+            }
             mjx_sa_state s2 = st;     // trace rows of this chunk
             if (s2.tr_i) s2.tr_i += k0 * R;
             if (s2.tr_acc) s2.tr_acc += k0 * R;

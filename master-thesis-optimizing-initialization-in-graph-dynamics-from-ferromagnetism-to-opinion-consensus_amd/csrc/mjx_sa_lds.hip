@@ -2860,6 +2860,7 @@ extern "C" int mjx_sa_lds_steps(const int32_t* adj, int64_t n, int d, int p, int
                                 mjx_sa_state* stp, int64_t nsteps, double par_a, double par_b, double a_cap,
                                 double b_cap, int64_t t_cap, void* stream) {
     if (!stp || !adj || !s || R < 1 || nsteps < 0 || p < 0 || c < 0) return MJX_EINVAL;
+    if (stp->philox_key) return MJX_EINVAL;             // the LDS kernels replay MT19937 inside the step
     const int T = p + c - 1;
     salds::Geo g;
     if (!salds::geometry(n, d, T, &g)) return MJX_ERANGE;

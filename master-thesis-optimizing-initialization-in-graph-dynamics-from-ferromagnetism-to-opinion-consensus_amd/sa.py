@@ -97,7 +97,7 @@ class SAReplicas:
     replica (device resident)."""
 
     def __init__(self, N, p, c, seeds, par_a=PAR_A, par_b=PAR_B, a0=None, b0=None, mode="auto", tape=1024,
-                 mt_state=None, layout="auto", graph_of=None, kernel=None):
+                 mt_state=None, layout="auto", graph_of=None, kernel=None, rng="mt19937"):
         """``N``: one (n, d) neighbour array (or Graph) for every replica, or a
         sequence of them (or a (G, n, d) array): replica r runs on graph r, or
         on graph ``graph_of[r]``.  ``mt_state`` = (mt uint32 (R, 624), idx
@@ -116,7 +116,12 @@ class SAReplicas:
         column), ``spec_k`` (8 or 16), ``no_spec``, ``no_cone2``, ``lds_serial``, ``lds_single``, ``lds_pair``,
         ``lds_wave`` (one wave per replica instead of the whole-CU kernel at
         p+c-1 >= 2; ``split`` = 4 or 8 waves for the latter); the results
-        never depend on it."""
+        never depend on it.  ``rng``: ``"mt19937"`` replays numpy's seeded
+        stream (the reference's proposals, bit for bit); ``"philox"`` is the
+        NON-parity throughput mode: the proposal of step t of
+        replica r comes from Philox-4x32-10 keyed by its seed (a pure function
+        of (seed, t), drawn into the tape: light-cone mode, a non-LDS layout,
+        tape > 0; the initial configuration still from the seeded MT19937)."""
         seeds = np.asarray(seeds, dtype=np.int64).reshape(-1)
         if seeds.size == 0 or seeds.min() < 0 or seeds.max() > 0xFFFFFFFF:
             raise ValueError("seeds must be in [0, 2**32)")  # np.random.seed's range
@@ -126,6 +131,9 @@ class SAReplicas:
         dev = _device.require_gpu()
         self.p, self.c = int(p), int(c)
         self.n = n
+        if rng not in ("mt19937", "philox"):
+            raise ValueError(f"unknown rng {rng!r}")
+        self.rng = rng
         if n < 2:
             raise ValueError("n must be >= 2")
         self.W = W = _device.words_for(R)
@@ -167,6 +175,10 @@ class SAReplicas:
         if kernel:
             raise ValueError(f"unknown kernel options {sorted(kernel)}")
         self._state.opt_flags = flags
+        self.philox_key = None
+        if rng == "philox":
+            self.philox_key = torch.from_numpy(seeds.astype(np.int64)).to(dev)
+            self._state.philox_key = self.philox_key.data_ptr()
         T = self.p + self.c - 1
         if mt_state is None:
             _lib.call("mjx_sa_init", _device.ptr(self.adj), n, self.d, self.p, self.c, R,
@@ -189,6 +201,8 @@ class SAReplicas:
         fits = T >= 1 and 0 < lds <= 150 * 1024
         if mode == "auto":
             mode = "lightcone" if fits else "rollout"
+        if rng == "philox" and mode != "lightcone":
+            raise ValueError("the Philox stream is drawn into the light-cone tape: mode='lightcone'")
         if mode == "lightcone" and not fits:
             raise ValueError(f"light-cone SA unsupported for d={self.d}, p+c-1={T}")
         if mode not in ("lightcone", "rollout"):
@@ -211,8 +225,12 @@ class SAReplicas:
         spec = (self.d == 3 and T <= 2) or (self.d == 4 and T == 1)
         per_cu = max(1, min((160 * 1024) // max(lds_bytes, 1), 32 // max(1, lds_threads.value // 64)))
         one_round = lds_fits and R <= _device.cu_count() * per_cu
+        if rng == "philox" and layout == "lds":
+            raise ValueError("the LDS kernels replay MT19937 in the step: rng='philox' needs another layout")
+        if rng == "philox" and not tape:
+            raise ValueError("rng='philox' draws into the proposal tape: tape > 0")
         if layout == "auto":
-            if lds_fits and (one_round or not spec):
+            if lds_fits and (one_round or not spec) and rng != "philox":
                 layout = "lds"
             elif spec and self.rep_graph is None:
                 layout = "rec"
@@ -280,7 +298,7 @@ class SAReplicas:
         (replica-packed bits), every replica's MT19937 stream (numpy's state,
         exactly), a, b, t, sum(s_end), the done flags (code/SA_RRG.py:65-85's
         loop state) and the parameters.  ``resume`` continues it bit for bit."""
-        if self.mode == "lightcone" and getattr(self, "tape_cap", 0):
+        if self.mode == "lightcone" and getattr(self, "tape_cap", 0) and self.rng != "philox":
             raise ValueError("the proposal tape draws ahead: checkpoint needs tape=0 (or the lds / rollout modes)")
         torch.cuda.current_stream().synchronize()
         out = {k: getattr(self, k).cpu().numpy().copy() for k in self._CKPT_STATE}
@@ -289,6 +307,9 @@ class SAReplicas:
                                    dtype=np.float64)
         out["t_cap"] = np.array(self.t_cap, dtype=np.int64)
         out["graphs_sha256"] = np.array(self.graphs_digest())
+        out["rng"] = np.array(self.rng)
+        if self.philox_key is not None:          # (the Philox stream's state: the key and t)
+            out["philox_key"] = self.philox_key.cpu().numpy().copy()
         return out
 
     def graphs_digest(self):
@@ -316,8 +337,11 @@ class SAReplicas:
                 ckpt = {k: z[k] for k in z.files}
         n, d, p, c, R = (int(x) for x in ckpt["params"])
         par_a, par_b, a0, b0 = (float(x) for x in ckpt["schedule"][:4])
+        rng = str(ckpt["rng"]) if "rng" in ckpt else "mt19937"
+        if rng == "philox":
+            mode, tape = "lightcone", (tape or 1024)
         sa = cls(N, p, c, np.zeros(R, dtype=np.int64), par_a=par_a, par_b=par_b, a0=a0, b0=b0, mode=mode,
-                 tape=tape, layout=layout, graph_of=graph_of, kernel=kernel)
+                 tape=tape, layout=layout, graph_of=graph_of, kernel=kernel, rng=rng)
         if (sa.n, sa.d, sa.R) != (n, d, R):
             raise ValueError(f"checkpoint of n={n}, d={d}, R={R} does not fit these graphs (n={sa.n}, d={sa.d})")
         if "graphs_sha256" in ckpt and str(ckpt["graphs_sha256"]) != sa.graphs_digest():
@@ -334,6 +358,8 @@ class SAReplicas:
                 raise ValueError(f"checkpoint field {k}: {tuple(src.shape)} {src.dtype}, expected "
                                  f"{tuple(dst.shape)} {dst.dtype}")
             dst.copy_(src)
+        if rng == "philox":
+            sa.philox_key.copy_(torch.from_numpy(np.ascontiguousarray(ckpt["philox_key"], dtype=np.int64)))
         if sa.mode == "lightcone" and sa.layout != "lds":
             sa._build_levels()
         torch.cuda.current_stream().synchronize()

@@ -14,7 +14,7 @@ def build(force=False, verbose=True):
     if not force and os.path.exists(LIB) and os.path.getmtime(LIB) > os.path.getmtime(SRC):
         return LIB
     # -ffp-contract=off: delta_H rounds every operation like numpy (code/SA_RRG.py:37)
-    cmd = ["gcc", "-O2", "-std=c99", "-ffp-contract=off", "-fPIC", "-shared", "-o", LIB + ".tmp", SRC, "-lm"]
+    cmd = ["gcc", "-O2", "-std=gnu99", "-ffp-contract=off", "-fPIC", "-shared", "-o", LIB + ".tmp", SRC, "-lm"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

@@ -12,6 +12,10 @@
  *                       numpy's legacy global MT19937 stream (np.random.seed,
  *                       binomial(1,.5), randint(0,n), rand) restated as in
  *                       oracle/mt19937.py.
+ *   orc_sa_loop_philox  the same loop with the library's NON-parity proposal
+ *                       stream: proposal t of a replica from
+ *                       Philox-4x32-10 keyed by its seed (orc_philox4x32_10);
+ *                       the initial configuration still from the seeded MT.
  * It does exactly what the reference does per proposal (three full rollouts:
  * s_endstate(s), s_endstate(s with s_i flipped), s_endstate(s) after the
  * step); no light-cone shortcut.  Pinned against the numpy oracle and the
@@ -73,6 +77,40 @@ static int64_t mt_randint(orc_mt* s, int64_t n)
     }
 }
 
+/* ---- Philox-4x32-10 ---------------------------------------------------------
+ * Salmon, Moraes, Dror, Shaw, "Parallel random numbers: as easy as 1, 2, 3"
+ * (SC'11), Random123's philox4x32_10: ten rounds of two 32x32->64 multiplies
+ * (M0 = 0xD2511F53, M1 = 0xCD9E8D57) with the key bumped by the Weyl constants
+ * (0x9E3779B9, 0xBB67AE85) between rounds.  Not the reference's generator: the
+ * library's counter-based mode for runs that do not replay numpy's stream.
+ * Pinned by Random123's known-answer vectors (tests/test_oracle_c.py). */
+void orc_philox4x32_10(const uint32_t* ctr, const uint32_t* key, uint32_t* out)
+{
+    uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3], k0 = key[0], k1 = key[1];
+    for (int r = 0; r < 10; ++r) {
+        if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n1 = (uint32_t)p1;
+        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1, n3 = (uint32_t)p0;
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+/* proposal t (the replica's step count before it) keyed by the replica's seed:
+ * counter (t_lo, t_hi, 0, 0), key (seed_lo, seed_hi); i = the high 64 bits of
+ * (x0 | x1 << 32) * n, u = numpy rand()'s 53-bit double of (x2, x3) */
+static void philox_prop(uint64_t seed, int64_t t, int64_t n, int64_t* i, double* u)
+{
+    const uint32_t ctr[4] = {(uint32_t)t, (uint32_t)((uint64_t)t >> 32), 0u, 0u};
+    const uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    uint32_t x[4];
+    orc_philox4x32_10(ctr, key, x);
+    const uint64_t w = (uint64_t)x[0] | ((uint64_t)x[1] << 32);
+    *i = (int64_t)(((unsigned __int128)w * (uint64_t)n) >> 64);
+    *u = ((double)(x[2] >> 5) * 67108864.0 + (double)(x[3] >> 6)) / 9007199254740992.0;
+}
+
 /* ---- dynamics -------------------------------------------------------------- */
 void orc_onestep_ell(const int32_t* adj, int64_t n, int d, const int8_t* s, int8_t* out)
 {
@@ -132,9 +170,10 @@ int64_t orc_s_endstate_csr(const int64_t* row_ptr, const int32_t* col, int64_t n
  * Returns the number of steps taken; *done = 1 consensus, 2 cap, 0 stopped.
  * mt_io/idx_io (optional): the stream to continue instead of seeding, and
  * where the stream stands on return. */
-int64_t orc_sa_loop(const int32_t* adj, int64_t n, int d, int p, int c, uint32_t seed, double par_a, double par_b,
-                    int64_t max_steps, int32_t* tr_i, int8_t* tr_acc, int64_t* tr_sum, double* tr_dE, int8_t* conf,
-                    int32_t* done, uint32_t* mt_io, int32_t* idx_io)
+static int64_t sa_loop(const int32_t* adj, int64_t n, int d, int p, int c, uint32_t seed, double par_a,
+                       double par_b, int64_t max_steps, int32_t* tr_i, int8_t* tr_acc, int64_t* tr_sum,
+                       double* tr_dE, int8_t* conf, int32_t* done, uint32_t* mt_io, int32_t* idx_io, int philox,
+                       uint64_t key)
 {
     int T = p + c - 1;
     int8_t* s = (int8_t*)malloc((size_t)n);
@@ -158,7 +197,10 @@ int64_t orc_sa_loop(const int32_t* adj, int64_t n, int d, int p, int c, uint32_t
     *done = 0;
     while (sum_end < n) {                                                      /* :72, m < 1 */
         if (max_steps >= 0 && t >= max_steps) break;
-        int64_t i = mt_randint(&rs, n);                                        /* :73 */
+        int64_t i;
+        double u;
+        if (philox) philox_prop(key, t, n, &i, &u);
+        else i = mt_randint(&rs, n);                                           /* :73 */
         /* E_delta (:32-37): two rollouts, the flipped one on a copy */
         int64_t sum1 = orc_s_endstate_ell(adj, n, d, s, T, e1, tmp);
         memcpy(s2, s, (size_t)n);
@@ -171,7 +213,7 @@ int64_t orc_sa_loop(const int32_t* adj, int64_t n, int d, int p, int c, uint32_t
         double dH = x3 / (double)n;
         double prob = exp(-dH);                                                /* :75 min([1, exp]) */
         if (prob > 1.0) prob = 1.0;
-        double u = mt_double(&rs);                                             /* :76 */
+        if (!philox) u = mt_double(&rs);                                       /* :76 */
         int acc = u < prob;
         if (acc) s[i] = (int8_t)-s[i];                                         /* :77 */
         if (a < a_cap) a = par_a * a;                                          /* :80 */
@@ -199,4 +241,21 @@ int64_t orc_sa_loop(const int32_t* adj, int64_t n, int d, int p, int c, uint32_t
     }
     free(s); free(s2); free(e1); free(tmp);
     return t;
+}
+
+int64_t orc_sa_loop(const int32_t* adj, int64_t n, int d, int p, int c, uint32_t seed, double par_a, double par_b,
+                    int64_t max_steps, int32_t* tr_i, int8_t* tr_acc, int64_t* tr_sum, double* tr_dE, int8_t* conf,
+                    int32_t* done, uint32_t* mt_io, int32_t* idx_io)
+{
+    return sa_loop(adj, n, d, p, c, seed, par_a, par_b, max_steps, tr_i, tr_acc, tr_sum, tr_dE, conf, done, mt_io,
+                   idx_io, 0, 0);
+}
+
+/* key: the replica's 64-bit Philox key (the library uses its seed) */
+int64_t orc_sa_loop_philox(const int32_t* adj, int64_t n, int d, int p, int c, uint32_t seed, uint64_t key,
+                           double par_a, double par_b, int64_t max_steps, int32_t* tr_i, int8_t* tr_acc,
+                           int64_t* tr_sum, double* tr_dE, int8_t* conf, int32_t* done)
+{
+    return sa_loop(adj, n, d, p, c, seed, par_a, par_b, max_steps, tr_i, tr_acc, tr_sum, tr_dE, conf, done, NULL,
+                   NULL, 1, key);
 }

@@ -82,6 +82,12 @@ static int check_sa(int64_t n, int d, int p, int c, int64_t K) {
     for (int64_t k = 0; k < t; ++k)
         if (ti[k] < 0 || ti[k] >= n || (ta[k] != 0 && ta[k] != 1)) { printf("sa trace\n"); return 1; }
     if (idx < 0 || idx > 624) { printf("sa stream index %d\n", idx); return 1; }
+    /* the Philox-stream loop on the same graph */
+    const int64_t tp = orc_sa_loop_philox(adj, n, d, p, c, 7u, 7ull, 1.0005, 1.0005, K, ti, ta, tsum, tde, conf, &done);
+    if (tp < 1 || tp > K) { printf("sa philox: %ld steps\n", (long)tp); return 1; }
+    if (orc_s_endstate_ell(adj, n, d, conf, p + c - 1, e, tmp) != tsum[tp - 1]) { printf("sa philox sum\n"); return 1; }
+    for (int64_t k = 0; k < tp; ++k)
+        if (ti[k] < 0 || ti[k] >= n || (ta[k] != 0 && ta[k] != 1)) { printf("sa philox trace\n"); return 1; }
     free(adj); free(ti); free(ta); free(tsum); free(tde); free(conf); free(e); free(tmp);
     return 0;
 }

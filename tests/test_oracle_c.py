@@ -93,3 +93,55 @@ def test_c_sa_global_stream_two_replicas():
         assert float(r["num_steps"]) == float(full[f"{key}_num_steps"][k])
         assert np.array_equal(r["conf"], full[f"{key}_conf"][k])
         assert r["mag_reached"] == full[f"{key}_mag_reached"][k]
+
+
+# Random123's known-answer vectors for philox4x32_10 (counter, key, result):
+# the library's non-parity proposal stream is pinned by them
+PHILOX_KAT = [
+    ((0x00000000, 0x00000000, 0x00000000, 0x00000000), (0x00000000, 0x00000000),
+     (0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8)),
+    ((0xffffffff, 0xffffffff, 0xffffffff, 0xffffffff), (0xffffffff, 0xffffffff),
+     (0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd)),
+    ((0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344), (0xa4093822, 0x299f31d0),
+     (0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1)),
+]
+
+
+@pytest.mark.parametrize("ctr,key,want", PHILOX_KAT)
+def test_philox4x32_10_known_answers(ctr, key, want):
+    assert [int(x) for x in fast.philox4x32_10(ctr, key)] == list(want)
+
+
+def philox_proposal(seed, t, n):
+    """Proposal t of a replica keyed by its seed (include/mjx.h philox_key):
+    restated in Python integers from the KAT-pinned block."""
+    x = [int(v) for v in fast.philox4x32_10([t & 0xFFFFFFFF, t >> 32, 0, 0], [seed & 0xFFFFFFFF, seed >> 32])]
+    i = ((x[0] | (x[1] << 32)) * n) >> 64
+    u = ((x[2] >> 5) * 67108864.0 + (x[3] >> 6)) / 9007199254740992.0
+    return i, u
+
+
+def test_c_sa_philox_loop_is_the_sa_loop_on_philox_proposals():
+    """orc_sa_loop_philox: the reference's loop (the same code as orc_sa_loop)
+    with proposal t = Philox(seed, t): its trace's i are the Python-restated
+    proposals, each accept is u < min(1, exp(-dE)), the initial configuration
+    is the seeded MT one and the final one is it with the accepted flips."""
+    from mjx import random_regular_graph
+    n, d, p, c, K = 300, 3, 2, 1, 400
+    adj = random_regular_graph(d, n, seed=12)
+    for seed in (0, 5, 4095):
+        r = fast.sa_loop_philox(adj, p, c, seed, max_steps=K, trace=True)
+        tr = r["trace"]
+        s = fast.sa_loop(adj, p, c, seed, max_steps=0)["conf"].copy()
+        for t in range(r["num_steps"]):
+            i, u = philox_proposal(seed, t, n)
+            assert tr["i"][t] == i
+            assert bool(tr["accept"][t]) == (u < min(1.0, float(np.exp(-tr["dE"][t]))))
+            if tr["accept"][t]:
+                s[i] = -s[i]
+        assert np.array_equal(s, r["conf"])
+        assert tr["sum_end"][-1] == int(np.sum(orc.s_endstate(adj, r["conf"], p, c)))
+    # another key, the same initial configuration, another run
+    a = fast.sa_loop_philox(adj, p, c, 5, max_steps=50, trace=True, key=6)
+    b = fast.sa_loop_philox(adj, p, c, 5, max_steps=50, trace=True)
+    assert not np.array_equal(a["trace"]["i"], b["trace"]["i"])

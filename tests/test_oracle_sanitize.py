@@ -18,7 +18,7 @@ def test_c_oracle_under_asan_ubsan(tmp_path):
         pytest.skip("no gcc")
     src = os.path.join(ROOT, "oracle", "orc_sanitize_main.c")
     exe = str(tmp_path / "orc_sanitize")
-    cmd = [gcc, "-std=c99", "-O1", "-g", "-ffp-contract=off", "-fsanitize=address,undefined",
+    cmd = [gcc, "-std=gnu99", "-O1", "-g", "-ffp-contract=off", "-fsanitize=address,undefined",
            "-fno-sanitize-recover=all", "-fno-omit-frame-pointer", src, "-o", exe, "-lm"]
     build = subprocess.run(cmd, capture_output=True, text=True)
     if build.returncode != 0 and "asan" in (build.stderr or "").lower():
