@@ -19,6 +19,7 @@
 // evaluated as ((-2*a)*s_i + b*D)/n with separately rounded operations, as
 // numpy does (code/SA_RRG.py:37).
 #include "mjx_common.h"
+#include <mutex>
 #include "mjx_mt.h"
 #include <math.h>
 #include <stdlib.h>
@@ -1486,6 +1487,9 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
     constexpr int SPEC_HS = 64 * K;                          // hash slots per replica
     constexpr int HB = (K == 8) ? 9 : 10;                    // log2(SPEC_HS)
     constexpr u64 GM = (1ull << K) - 1;
+    // the step chain is latency-bound: its waves issue first on a SIMD they
+    // share with the next chunk's tape waves (drawn on a side stream)
+    __builtin_amdgcn_s_setprio(3);
     const int lane = threadIdx.x;
     const int g = lane / K, k = lane % K;
     const int64_t col = blockIdx.x % W;                       // a column's waves on one XCD when W % 8 == 0
@@ -2158,6 +2162,22 @@ extern "C" int mjx_sa_lightcone_prepare(const int32_t* adj, int64_t n, int d, in
 
 // Shared body of the two light-cone entry points: L.s / ns / cs / s0c set by
 // the caller (separate level arrays or the cone layout).
+// a non-blocking side stream per device for the proposal tapes (created once,
+// kept for the process)
+static hipStream_t tape_side_stream() {
+    static std::mutex mu;
+    static hipStream_t per[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!per[dev]) {
+        hipStream_t s;
+        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+        per[dev] = s;
+    }
+    return per[dev];
+}
+
 static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d, int T, int64_t R, LcLevels L,
                     mjx_sa_state* stp,
                     int64_t nsteps, double par_a, double par_b, double a_cap, double b_cap, int64_t t_cap,
@@ -2193,7 +2213,7 @@ static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d
         MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
                 "lightcone lds");
         kern<<<(unsigned)(W * split), 64, lds, hs>>>(adj, d, n, R, W, L, T, s2, k, par_a, par_b, a_cap, b_cap,
-                                                     t_cap, st.tape_i, st.tape_u, split, st.rep_graph);
+                                                     t_cap, s2.tape_i, s2.tape_u, split, st.rep_graph);
         MJX_LAUNCH_CHECK("k_sa_lightcone");
         return MJX_OK;
     };
@@ -2205,7 +2225,7 @@ static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d
         MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
                 "cone2 lds");
         kern<<<(unsigned)(W * split), 64, lds, hs>>>(adj, (const int4*)adj_pad, n, R, W, L, s2, k, par_a, par_b,
-                                                     a_cap, b_cap, t_cap, st.tape_i, st.tape_u, split, st.rep_graph);
+                                                     a_cap, b_cap, t_cap, s2.tape_i, s2.tape_u, split, st.rep_graph);
         MJX_LAUNCH_CHECK("k_sa_cone2");
         return MJX_OK;
     };
@@ -2224,7 +2244,7 @@ static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d
             MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         (int)lds_spec), "spec lds");
             kern<<<(unsigned)(W * K), 64, lds_spec, hs>>>(adj, rows4, n, R, W, L, s2, k, par_a, par_b,
-                                                                      a_cap, b_cap, t_cap, st.tape_i, st.tape_u,
+                                                                      a_cap, b_cap, t_cap, s2.tape_i, s2.tape_u,
                                                                       hoff, st.rep_graph);
             MJX_LAUNCH_CHECK("k_sa_spec");
             return MJX_OK;
@@ -2236,28 +2256,98 @@ static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d
         if (d == 4) return go(k_sa_spec<4, 1, 8>, 8);
         return (T == 2) ? go(k_sa_spec<3, 2, 8>, 8) : go(k_sa_spec<3, 1, 8>, 8);
     };
+    auto step_chunk = [&](auto kern_tape, mjx_sa_state s2, int64_t k0, int64_t k) -> int {
+        if (s2.tr_i) s2.tr_i += k0 * R;     // trace rows of this chunk
+        if (s2.tr_acc) s2.tr_acc += k0 * R;
+        if (s2.tr_sum) s2.tr_sum += k0 * R;
+        if (s2.tr_dE) s2.tr_dE += k0 * R;
+        return spec ? launch_spec(s2, k) : one_trip ? launch_one_trip(s2, k) : launch(kern_tape, s2, k);
+    };
     auto run = [&](auto kern_plain, auto kern_tape) -> int {
         if (!tape) return launch(kern_plain, st, nsteps);
-        for (int64_t k0 = 0; k0 < nsteps; k0 += st.tape_cap) {
-            const int64_t k = (nsteps - k0 < st.tape_cap) ? nsteps - k0 : st.tape_cap;
-            if (st.philox_key) {
-                const int64_t blocks = (k * R + 255) / 256;
-                k_sa_tape_philox<<<(unsigned)(blocks < 65536 ? blocks : 65536), 256, 0, hs>>>(n, R, k, st, st.tape_i,
-                                                                                              st.tape_u);
-                MJX_LAUNCH_CHECK("k_sa_tape_philox");
-            } else {
-                k_sa_tape<<<(unsigned)R, 64, 0, hs>>>(n, R, k, st, st.tape_i, st.tape_u);
-                MJX_LAUNCH_CHECK("k_sa_tape");
+        const int64_t half = st.tape_cap / 2;
+        if (st.philox_key || half < 1 || nsteps <= 128) {
+            // one tape at a time on the caller's stream (the Philox tape is a
+            // counter function of t: a few microseconds)
+            for (int64_t k0 = 0; k0 < nsteps; k0 += st.tape_cap) {
+                const int64_t k = (nsteps - k0 < st.tape_cap) ? nsteps - k0 : st.tape_cap;
+                if (st.philox_key) {
+                    const int64_t blocks = (k * R + 255) / 256;
+                    k_sa_tape_philox<<<(unsigned)(blocks < 65536 ? blocks : 65536), 256, 0, hs>>>(
+                        n, R, k, st, st.tape_i, st.tape_u);
+                    MJX_LAUNCH_CHECK("k_sa_tape_philox");
+                } else {
+                    k_sa_tape<<<(unsigned)R, 64, 0, hs>>>(n, R, k, st, st.tape_i, st.tape_u);
+                    MJX_LAUNCH_CHECK("k_sa_tape");
+                }
+                const int rc = step_chunk(kern_tape, st, k0, k);
+                if (rc) return rc;
             }
-            mjx_sa_state s2 = st;     // trace rows of this chunk
-            if (s2.tr_i) s2.tr_i += k0 * R;
-            if (s2.tr_acc) s2.tr_acc += k0 * R;
-            if (s2.tr_sum) s2.tr_sum += k0 * R;
-            if (s2.tr_dE) s2.tr_dE += k0 * R;
-            const int rc = spec ? launch_spec(s2, k) : one_trip ? launch_one_trip(s2, k) : launch(kern_tape, s2, k);
-            if (rc) return rc;
+            return MJX_OK;
         }
-        return MJX_OK;
+        // MT19937 tapes drawn a chunk ahead on a side stream into the other
+        // half of the tape buffer: chunk j+1's draws (one wave per replica, a
+        // CU mostly idle under the latency-bound step kernels) overlap chunk
+        // j's steps.  Chunk j+1's tape waits for chunk j-1's steps (which read
+        // that half); chunk j's steps wait for its tape.  A replica that
+        // finishes in chunk j may get chunk j+1 drawn anyway: its stream then
+        // stands past its last proposal, as with any tape (mt_state() and
+        // checkpoint() refuse a tape).
+        hipStream_t side = tape_side_stream();
+        if (!side) return MJX_EHIP;
+        auto hrc = [](hipError_t e) -> int {
+            if (e == hipSuccess) return MJX_OK;
+            set_hip_error(e, "tape side stream");
+            return MJX_EHIP;
+        };
+        hipEvent_t ev[5];
+        for (int q = 0; q < 5; ++q) MJX_HIP(hipEventCreateWithFlags(&ev[q], hipEventDisableTiming), "tape event");
+        hipEvent_t* evT = ev;            // chunk's tape drawn (by half)
+        hipEvent_t* evS = ev + 2;        // chunk's steps done (by half)
+        int rc = MJX_OK;
+        // chunk sizes ramp up (128, x4, ..., half) so that only the first,
+        // short tape is drawn before any step runs: chunk j+1's tape (4x the
+        // rows of chunk j) takes less time than chunk j's steps
+        int64_t c0s[2], cks[2];                          // chunk j's first step and size, at j & 1
+        int64_t next_k0 = 0, next_c = (half < 128) ? half : 128;
+        int64_t nchunks = 0;
+        for (int64_t k0 = 0, c = next_c; k0 < nsteps; ++nchunks) {
+            k0 += (nsteps - k0 < c) ? nsteps - k0 : c;
+            c = (4 * c < half) ? 4 * c : half;
+        }
+        auto tape_into = [&](int64_t j) -> int {
+            c0s[j & 1] = next_k0;
+            cks[j & 1] = (nsteps - next_k0 < next_c) ? nsteps - next_k0 : next_c;
+            next_k0 += cks[j & 1];
+            next_c = (4 * next_c < half) ? 4 * next_c : half;
+            int32_t* ti = st.tape_i + (j & 1) * half * R;
+            double* tu = st.tape_u + (j & 1) * half * R;
+            k_sa_tape<<<(unsigned)R, 64, 0, side>>>(n, R, cks[j & 1], st, ti, tu);
+            MJX_LAUNCH_CHECK("k_sa_tape");
+            MJX_HIP(hipEventRecord(evT[j & 1], side), "tape record");
+            return MJX_OK;
+        };
+        do {
+            // the side stream starts behind everything already on the caller's
+            if ((rc = hrc(hipEventRecord(ev[4], hs))) || (rc = hrc(hipStreamWaitEvent(side, ev[4], 0))))
+                break;
+            if ((rc = tape_into(0))) break;
+            for (int64_t j = 0; j < nchunks && !rc; ++j) {
+                if (j + 1 < nchunks) {
+                    if (j >= 1 && (rc = hrc(hipStreamWaitEvent(side, evS[(j - 1) & 1], 0)))) break;
+                    if ((rc = tape_into(j + 1))) break;
+                }
+                if ((rc = hrc(hipStreamWaitEvent(hs, evT[j & 1], 0)))) break;
+                const int64_t k0 = c0s[j & 1], k = cks[j & 1];
+                mjx_sa_state s2 = st;
+                s2.tape_i = st.tape_i + (j & 1) * half * R;
+                s2.tape_u = st.tape_u + (j & 1) * half * R;
+                if ((rc = step_chunk(kern_tape, s2, k0, k))) break;
+                if ((rc = hrc(hipEventRecord(evS[j & 1], hs)))) break;
+            }
+        } while (false);
+        for (int q = 0; q < 5; ++q) (void)hipEventDestroy(ev[q]);
+        return rc;
     };
     switch (d) {
         case 3: return run(k_sa_lightcone<3, false>, k_sa_lightcone<3, true>);

@@ -96,7 +96,7 @@ class SAReplicas:
     """R bit-packed SA replicas on one random regular graph or on a graph per
     replica (device resident)."""
 
-    def __init__(self, N, p, c, seeds, par_a=PAR_A, par_b=PAR_B, a0=None, b0=None, mode="auto", tape=1024,
+    def __init__(self, N, p, c, seeds, par_a=PAR_A, par_b=PAR_B, a0=None, b0=None, mode="auto", tape=2048,
                  mt_state=None, layout="auto", graph_of=None, kernel=None, rng="mt19937"):
         """``N``: one (n, d) neighbour array (or Graph) for every replica, or a
         sequence of them (or a (G, n, d) array): replica r runs on graph r, or
@@ -266,7 +266,9 @@ class SAReplicas:
                 self.adj_pad = torch.zeros((rows, 4), dtype=torch.int32, device=dev)
                 self.adj_pad[:, :3] = self.adj.view(rows, 3)
             # proposal tape: (i, u) of `tape` steps per replica drawn ahead by
-            # a wave per replica (0 = draw inside the step kernel)
+            # a wave per replica (0 = draw inside the step kernel); the library
+            # draws the MT19937 tape in two halves, one chunk ahead on a side
+            # stream (2048: chunks of 1024 steps)
             self.tape_cap = int(tape) if tape else 0
             if self.tape_cap > 0:
                 self.tape_i = torch.empty(self.tape_cap * R, dtype=torch.int32, device=dev)
