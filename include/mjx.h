@@ -165,7 +165,9 @@ typedef struct mjx_sa_state {
     int32_t*  tr_tie;    /* [R] count of |u - exp(-dE)| < 4 ulp near-ties    */
     /* optional proposal tape for mjx_sa_lightcone_steps (NULL / 0 to draw
      * inside the step kernel): the (i, u) of up to tape_cap steps of every
-     * replica are drawn ahead by a wave per replica, row k = step k */
+     * replica are drawn ahead by a wave per replica; replica-major: entry
+     * (r, k) at r * tape_cap + k, k = step k of the chunk (the library may
+     * split the buffer into two halves of tape_cap / 2 rows per replica) */
     int32_t*  tape_i;    /* [tape_cap*R] */
     double*   tape_u;    /* [tape_cap*R] */
     int64_t   tape_cap;

@@ -809,6 +809,7 @@ __global__ void __launch_bounds__(64) k_sa_tape(int64_t n, int64_t R, int64_t K,
     const int lane = threadIdx.x;
     const u64 ltmask = (1ull << lane) - 1ull;
     if (st.done[r]) return;
+    const int64_t ts = st.tape_cap;                  // the tape's rows per replica (replica-major)
     uint32_t* g = st.mt + r * MT_N;
     for (int k = lane; k < MT_N; k += 64) buf[k] = ld_nc(g + k);
     int idx = st.mt_idx[r];
@@ -832,8 +833,8 @@ __global__ void __launch_bounds__(64) k_sa_tape(int64_t n, int64_t R, int64_t K,
             twist_if_end();
             const uint32_t w2 = mt_temper(buf[idx++]);
             if (lane == 0) {
-                tape_i[k * R + r] = 0;
-                tape_u[k * R + r] = mt_double(w1, w2);
+                tape_i[r * ts + k] = 0;
+                tape_u[r * ts + k] = mt_double(w1, w2);
             }
         }
     }
@@ -865,8 +866,8 @@ __global__ void __launch_bounds__(64) k_sa_tape(int64_t n, int64_t R, int64_t K,
             const uint32_t x2 = (uint32_t)__builtin_amdgcn_ds_bpermute(((lane + 2) & 63) * 4, (int)tw);
             if ((stm >> lane) & 1ull) {
                 const int64_t j = k + __popcll(stm & ltmask);
-                tape_i[j * R + r] = (int32_t)y;
-                tape_u[j * R + r] = mt_double(x1, x2);
+                tape_i[r * ts + j] = (int32_t)y;
+                tape_u[r * ts + j] = mt_double(x1, x2);
             }
             k += got;
             idx += pos;
@@ -884,8 +885,8 @@ __global__ void __launch_bounds__(64) k_sa_tape(int64_t n, int64_t R, int64_t K,
         twist_if_end();
         const uint32_t w2 = mt_temper(buf[idx++]);
         if (lane == 0) {
-            tape_i[k * R + r] = iv;
-            tape_u[k * R + r] = mt_double(w1, w2);
+            tape_i[r * ts + k] = iv;
+            tape_u[r * ts + k] = mt_double(w1, w2);
         }
         ++k;
     }
@@ -919,16 +920,16 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t
 // carry (the step count is the counter).
 __global__ void __launch_bounds__(256) k_sa_tape_philox(int64_t n, int64_t R, int64_t K, mjx_sa_state st,
                                                         int32_t* __restrict__ tape_i, double* __restrict__ tape_u) {
-    const int64_t total = K * R;
+    const int64_t total = K * R, ts = st.tape_cap;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t k = e / R, r = e - k * R;
+        const int64_t r = e / K, k = e - r * K;
         if (st.done[r]) continue;
         const uint64_t t = (uint64_t)(st.t[r] + k), key = st.philox_key[r];
         uint32_t x[4];
         philox4x32_10((uint32_t)t, (uint32_t)(t >> 32), 0u, 0u, (uint32_t)key, (uint32_t)(key >> 32), x);
         const uint64_t w = (uint64_t)x[0] | ((uint64_t)x[1] << 32);
-        tape_i[e] = (int32_t)__umul64hi(w, (uint64_t)n);
-        tape_u[e] = mt_double(x[2], x[3]);
+        tape_i[r * ts + k] = (int32_t)__umul64hi(w, (uint64_t)n);
+        tape_u[r * ts + k] = mt_double(x[2], x[3]);
     }
 }
 
@@ -977,9 +978,9 @@ __global__ void __launch_bounds__(64) k_sa_lightcone(const int32_t* __restrict__
         for (int m = 0; m < DD; ++m) o[m] = adj[base + m];
     };
     if constexpr (TAPE) {
-        if (live && nsteps > 0) { nx_i = tape_i[r]; nx_u = tape_u[r]; }
-        if (live && nsteps > 1) { n1i = tape_i[R + r]; n1u = tape_u[R + r]; }
-        if (live && nsteps > 2) { n2i = tape_i[2 * R + r]; n2u = tape_u[2 * R + r]; }
+        if (live && nsteps > 0) { nx_i = tape_i[r * st.tape_cap]; nx_u = tape_u[r * st.tape_cap]; }
+        if (live && nsteps > 1) { n1i = tape_i[r * st.tape_cap + 1]; n1u = tape_u[r * st.tape_cap + 1]; }
+        if (live && nsteps > 2) { n2i = tape_i[r * st.tape_cap + 2]; n2u = tape_u[r * st.tape_cap + 2]; }
         if (pre) {
             row(nx_i, A0);
 #pragma unroll
@@ -1005,8 +1006,8 @@ __global__ void __launch_bounds__(64) k_sa_lightcone(const int32_t* __restrict__
             nx_i = n1i; nx_u = n1u;
             n1i = n2i; n1u = n2u;
             if (live && step + 3 < nsteps) {
-                n2i = tape_i[(step + 3) * R + r];
-                n2u = tape_u[(step + 3) * R + r];
+                n2i = tape_i[r * st.tape_cap + step + 3];
+                n2u = tape_u[r * st.tape_cap + step + 3];
             }
         } else {
             // randint(low=0, high=n) (code/SA_RRG.py:73): numpy legacy masked rejection
@@ -1208,7 +1209,7 @@ __global__ void __launch_bounds__(64) k_sa_cone2(const int32_t* __restrict__ adj
     };
     auto tape = [&](int64_t k, int32_t& iv, double& uv) {
         iv = 0; uv = 0.0;
-        if (run && k < nsteps) { iv = tape_i[k * R + r]; uv = tape_u[k * R + r]; }
+        if (run && k < nsteps) { iv = tape_i[r * st.tape_cap + k]; uv = tape_u[r * st.tape_cap + k]; }
     };
     // pipeline registers: tape (i, u) of k+1..k+3; row of i_{k+1}, i_{k+2};
     // rows of N(i_{k+1}); current rows of i_k, N(i_k), children of i_k
@@ -1647,7 +1648,7 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
         if (fresh) {
             // rows of i and of its neighbours (two round trips); the rows of the
             // children only where level 2 needs them (below)
-            if (mine) { i = tape_i[kk * R + r]; u = tape_u[kk * R + r]; }
+            if (mine) { i = tape_i[r * st.tape_cap + kk]; u = tape_u[r * st.tape_cap + kk]; }
             row(i, A0);
 #pragma unroll
             for (int m = 0; m < D; ++m) row(A0[m], A1[m]);
@@ -1666,7 +1667,7 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
         const bool pf = going && nk < nsteps;
         int32_t n_i = 0;
         double n_u = 0.0;
-        if (pf) { n_i = tape_i[nk * R + r]; n_u = tape_u[nk * R + r]; }
+        if (pf) { n_i = tape_i[r * st.tape_cap + nk]; n_u = tape_u[r * st.tape_cap + nk]; }
         // tree shape (lc_tree2)
         bool ok = true, simple = true;
 #pragma unroll
@@ -2322,7 +2323,9 @@ static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d
             next_c = (4 * next_c < half) ? 4 * next_c : half;
             int32_t* ti = st.tape_i + (j & 1) * half * R;
             double* tu = st.tape_u + (j & 1) * half * R;
-            k_sa_tape<<<(unsigned)R, 64, 0, side>>>(n, R, cks[j & 1], st, ti, tu);
+            mjx_sa_state sh = st;
+            sh.tape_cap = half;                  // rows per replica in this half
+            k_sa_tape<<<(unsigned)R, 64, 0, side>>>(n, R, cks[j & 1], sh, ti, tu);
             MJX_LAUNCH_CHECK("k_sa_tape");
             MJX_HIP(hipEventRecord(evT[j & 1], side), "tape record");
             return MJX_OK;
@@ -2342,6 +2345,7 @@ static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d
                 mjx_sa_state s2 = st;
                 s2.tape_i = st.tape_i + (j & 1) * half * R;
                 s2.tape_u = st.tape_u + (j & 1) * half * R;
+                s2.tape_cap = half;
                 if ((rc = step_chunk(kern_tape, s2, k0, k))) break;
                 if ((rc = hrc(hipEventRecord(evS[j & 1], hs)))) break;
             }
