@@ -288,19 +288,25 @@ def bench_sa(args, rank, world, dist, dev):
     seeds = np.arange(sa_R, dtype=np.int64) + rank * sa_R
     out = {"config": "configs[1]: d=3 RRG N=1e6 p=2 c=1, 4096 bit-packed SA replicas per GPU "
                      "(numpy MT19937 replay, bit-exact accept sequences)"}
-    for mode, steps in (("lightcone", args.sa_steps), ("rollout", args.sa_rollout_steps)):
+    # "lightcone_philox": the same run on the non-parity Philox-4x32-10 proposal
+    # stream (SAReplicas(rng="philox")) -- not the reference's
+    # proposals; the parity line is "lightcone"
+    for key, steps in (("lightcone", args.sa_steps), ("lightcone_philox", args.sa_steps),
+                       ("rollout", args.sa_rollout_steps)):
         if steps <= 0:
             continue
+        mode = "rollout" if key == "rollout" else "lightcone"
         torch.cuda.synchronize()
         t_init = time.perf_counter()
-        sa = mjx.SAReplicas(sa_adj, sa_p, sa_c, seeds, mode=mode)
+        sa = mjx.SAReplicas(sa_adj, sa_p, sa_c, seeds, mode=mode,
+                            rng="philox" if key == "lightcone_philox" else "mt19937")
         sa.steps(2)
         torch.cuda.synchronize()
         t_init = time.perf_counter() - t_init
         sa.steps(args.sa_warmin)                      # steady state: past the all-accept start
         el = _timed(lambda: sa.steps(steps), dist, dev)
         props = world * sa_R * steps / el
-        out[mode] = {
+        out[key] = {
             "proposals_per_s": props,
             "sweeps_per_s": props / sa_n,
             "ms_per_step": 1e3 * el / steps,
