@@ -59,5 +59,33 @@ __device__ inline void lds_twist(uint32_t* buf, int lane) {
     __builtin_amdgcn_wave_barrier();
 }
 
+// numpy's proposal draws in a window of 64 tempered words (code/SA_RRG.py:73,
+// 76: randint(0, n)'s masked rejection, then rand()'s two words): a proposal
+// starts at the first acceptable word at or after the previous proposal's end.
+// Scanning left to right is a 3-state automaton (0 = looking for an acceptable
+// word, 1 and 2 = inside rand()'s words; an acceptable word in state 0 starts a
+// proposal), so the starts come from a parallel prefix of its transition
+// functions (each a map {0,1,2} -> {0,1,2} packed as three 2-bit fields):
+// four DPP row shifts and two row broadcasts, no serial walk.  Lane l starts a
+// proposal iff the state after word l, from state 0 at the window's start, is 1.
+__device__ __forceinline__ uint32_t mt_walk_compose(uint32_t g, uint32_t h) {   // x -> g(h(x))
+    return ((g >> (2 * (h & 3u))) & 3u) | (((g >> (2 * ((h >> 2) & 3u))) & 3u) << 2) |
+           (((g >> (2 * ((h >> 4) & 3u))) & 3u) << 4);
+}
+__device__ __forceinline__ unsigned long long mt_window_starts(bool ok) {
+    constexpr uint32_t ID = 0u | (1u << 2) | (2u << 4);
+    uint32_t f = ok ? (1u | (2u << 2)) : (2u << 2);          // ok: 0->1, 1->2, 2->0; else 0->0, 1->2, 2->0
+    f = mt_walk_compose(f, (uint32_t)__builtin_amdgcn_update_dpp((int)ID, (int)f, 0x111, 0xf, 0xf, false));  // row_shr:1
+    f = mt_walk_compose(f, (uint32_t)__builtin_amdgcn_update_dpp((int)ID, (int)f, 0x112, 0xf, 0xf, false));  // row_shr:2
+    f = mt_walk_compose(f, (uint32_t)__builtin_amdgcn_update_dpp((int)ID, (int)f, 0x114, 0xf, 0xf, false));  // row_shr:4
+    f = mt_walk_compose(f, (uint32_t)__builtin_amdgcn_update_dpp((int)ID, (int)f, 0x118, 0xf, 0xf, false));  // row_shr:8
+    f = mt_walk_compose(f, (uint32_t)__builtin_amdgcn_update_dpp((int)ID, (int)f, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    f = mt_walk_compose(f, (uint32_t)__builtin_amdgcn_update_dpp((int)ID, (int)f, 0x143, 0xc, 0xf, false));  // row_bcast:31
+    return __ballot((f & 3u) == 1u);
+}
+// lane l + 1's value (wave_shl:1; lane 63 gets 0)
+__device__ __forceinline__ uint32_t mt_next_lane(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false);
+}
 
 }  // namespace mjx

@@ -849,21 +849,14 @@ __global__ void __launch_bounds__(64) k_sa_tape(int64_t n, int64_t R, int64_t K,
             ok = y <= (uint32_t)rng;
         }
         const u64 okm = __ballot(ok);
-        u64 stm = 0;
-        int pos = 0;
-        int64_t got = 0;
-        while (pos < 64 && k + got < K) {
-            const u64 m = okm >> pos;
-            if (!m) break;
-            const int f = pos + __ffsll((unsigned long long)m) - 1;
-            if (f + 2 >= lim) break;
-            stm |= 1ull << f;
-            ++got;
-            pos = f + 3;
-        }
+        // the proposal starts whose rand() words fit the window, at most K - k of them
+        u64 stm = mt_window_starts(ok) & ((lim >= 2) ? ((1ull << (lim - 2)) - 1ull) : 0ull);
+        while ((int64_t)__popcll(stm) > K - k) stm &= ~(1ull << (63 - __clzll(stm)));
+        const int64_t got = __popcll(stm);
+        const int pos = got ? 66 - __clzll(stm) : 0;          // after the last start's two words
         if (got > 0) {
-            const uint32_t x1 = (uint32_t)__builtin_amdgcn_ds_bpermute(((lane + 1) & 63) * 4, (int)tw);
-            const uint32_t x2 = (uint32_t)__builtin_amdgcn_ds_bpermute(((lane + 2) & 63) * 4, (int)tw);
+            const uint32_t x1 = mt_next_lane(tw);
+            const uint32_t x2 = mt_next_lane(x1);
             if ((stm >> lane) & 1ull) {
                 const int64_t j = k + __popcll(stm & ltmask);
                 tape_i[r * ts + j] = (int32_t)y;

@@ -1915,23 +1915,16 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
             ok = y <= rng;
         }
         const u64 okm = __ballot(ok);
-        // proposal starts by a scalar walk over the ballot (each: the first
-        // acceptable word at or after the previous end, then rand()'s two words)
-        u64 stm = 0;
-        int pos = 0;
-        uint32_t got = 0;
-        while (pos < 64 && got < room) {
-            const u64 m = okm >> pos;
-            if (!m) break;
-            const int f = pos + __ffsll((unsigned long long)m) - 1;
-            if (f + 2 >= lim) break;
-            stm |= 1ull << f;
-            ++got;
-            pos = f + 3;
-        }
+        // the proposal starts (each: the first acceptable word at or after the
+        // previous end, then rand()'s two words) whose words fit the window, at
+        // most `room` of them
+        u64 stm = mt_window_starts(ok) & ((lim >= 2) ? ((1ull << (lim - 2)) - 1ull) : 0ull);
+        while ((uint32_t)__popcll(stm) > room) stm &= ~(1ull << (63 - __clzll(stm)));
+        const uint32_t got = (uint32_t)__popcll(stm);
+        const int pos = got ? 66 - __clzll(stm) : 0;          // after the last start's two words
         if (got > 0) {
-            const uint32_t x1 = (uint32_t)__builtin_amdgcn_ds_bpermute(((lane + 1) & 63) * 4, (int)tw);
-            const uint32_t x2 = (uint32_t)__builtin_amdgcn_ds_bpermute(((lane + 2) & 63) * 4, (int)tw);
+            const uint32_t x1 = mt_next_lane(tw);
+            const uint32_t x2 = mt_next_lane(x1);
             if ((stm >> lane) & 1ull) {
                 const int q = (int)((npend + (uint32_t)__popcll(stm & ltmask)) & 63u);
                 q_i[q] = (int)y;
@@ -2546,19 +2539,13 @@ __global__ void __launch_bounds__(64 * (NW + 1)) k_sa_lds_wg1(const int32_t* __r
                 ok = y <= rng;
             }
             const u64 okm = __ballot(ok);
-            u64 stm = 0;
-            int pos = 0, got = 0;
-            while (pos < 64 && got < room) {
-                const u64 m = okm >> pos;
-                if (!m) break;
-                const int f = pos + __ffsll((unsigned long long)m) - 1;
-                if (f + 2 >= lim) break;
-                stm |= 1ull << f;
-                ++got;
-                pos = f + 3;
-            }
-            const uint32_t x1 = (uint32_t)__shfl((int)tw, lane + 1 < 64 ? lane + 1 : 63, 64);
-            const uint32_t x2 = (uint32_t)__shfl((int)tw, lane + 2 < 64 ? lane + 2 : 63, 64);
+            // the proposal starts whose words fit the window, at most `room`
+            u64 stm = mt_window_starts(ok) & ((lim >= 2) ? ((1ull << (lim - 2)) - 1ull) : 0ull);
+            while (__popcll(stm) > room) stm &= ~(1ull << (63 - __clzll(stm)));
+            const int got = __popcll(stm);
+            const int pos = got ? 66 - __clzll(stm) : 0;      // after the last start's two words
+            const uint32_t x1 = mt_next_lane(tw);
+            const uint32_t x2 = mt_next_lane(x1);
             if (got > 0) {
                 if ((stm >> lane) & 1ull) {
                     const int e = (int)((produced + __popcll(stm & ltmask)) & 63);
