@@ -2384,7 +2384,7 @@ struct GeoW1 {
     int off_tag;    // nw * 32 tag words
     int off_mt;
     int off_mtb;    // the MT state before the parser's latest twist
-    int off_q;      // ring: i[64], u[64], end[64]
+    int off_q;      // ring: i[128], u[128], end[128]
     int off_res;    // per proposal: packed word, a, b after its step, dE
     int bytes;
 };
@@ -2399,7 +2399,7 @@ static bool geometry_wg1(int64_t n, int d, int K, GeoW1* g) {
     g->off_mt = (int)off;    off += MT_N * 4;
     g->off_mtb = (int)off;   off += MT_N * 4;
     off = (off + 15) / 16 * 16;
-    g->off_q = (int)off;     off += 64 * 4 + 64 * 8 + 64 * 4;
+    g->off_q = (int)off;     off += 128 * 4 + 128 * 8 + 128 * 4;
     g->off_res = (int)off;   off += 64 * 4 + 64 * 8 * 3 + 4 * 4;
     g->bytes = (int)off;
     return (size_t)off <= kLdsMax;
@@ -2414,8 +2414,8 @@ __global__ void __launch_bounds__(64 * (NW + 1)) k_sa_lds_wg1(const int32_t* __r
     constexpr int K = NW * NQ;                     // proposals per round
     static_assert(D >= 1 && D <= 4 && G >= D + 1 && K <= 32 && NW >= 2, "whole-CU LDS SA at T = 1");
     constexpr int NT = 64 * (NW + 1);
-    constexpr int RCAP = 63;                       // ring entries ahead of the consumer (64 slots)
-    constexpr int TARGET = 60;                     // the parser keeps this many proposals ahead
+    constexpr int QN = 128;                        // ring slots
+    constexpr int RCAP = QN - 1;                   // ring entries ahead of the consumer
     extern __shared__ __align__(16) unsigned char smem[];
     const int tid = threadIdx.x;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2433,8 +2433,8 @@ __global__ void __launch_bounds__(64 * (NW + 1)) k_sa_lds_wg1(const int32_t* __r
     uint32_t* mt = reinterpret_cast<uint32_t*>(smem + geo.off_mt);
     uint32_t* mtb = reinterpret_cast<uint32_t*>(smem + geo.off_mtb);
     int* q_i = reinterpret_cast<int*>(smem + geo.off_q);
-    double* q_u = reinterpret_cast<double*>(q_i + 64);
-    int* q_end = reinterpret_cast<int*>(q_u + 64);
+    double* q_u = reinterpret_cast<double*>(q_i + QN);
+    int* q_end = reinterpret_cast<int*>(q_u + QN);
     uint32_t* res = reinterpret_cast<uint32_t*>(smem + geo.off_res);
     double* res_a = reinterpret_cast<double*>(res + 64);
     double* res_b = res_a + 64;
@@ -2462,7 +2462,7 @@ __global__ void __launch_bounds__(64 * (NW + 1)) k_sa_lds_wg1(const int32_t* __r
         for (int q = tid; q < 2 * nw; q += NT) lev[q] = 0u;
         for (int q = tid; q < nw * 32; q += NT) tag[q] = 0u;
         for (int q = tid; q < MT_N; q += NT) mt[q] = st.mt[r * MT_N + q];
-        for (int q = tid; q < 64; q += NT) q_i[q] = 0;
+        for (int q = tid; q < QN; q += NT) q_i[q] = 0;
         const int64_t col = r >> 6;
         const u64 rbit = 1ull << (r & 63);
         __syncthreads();
@@ -2519,13 +2519,15 @@ __global__ void __launch_bounds__(64 * (NW + 1)) k_sa_lds_wg1(const int32_t* __r
         idx = 0;
     };
     // a second twist while proposals drawn before the first are still to be taken
-    // would lose their state (never: a state yields >= 100 proposals, the ring
-    // holds 63; the last clause keeps the ring from ever running dry)
+    // would lose their state: the parser then waits for the consumer (a state
+    // yields ~170 proposals, the ring holds 127; the last clause keeps the ring
+    // from ever running dry)
     auto can_twist = [&]() -> bool { return bak_at < 0 || k > bak_at || produced == k; };
-    auto refill = [&](int windows) {
+    // up to `windows` windows while fewer than `want` proposals are ready
+    auto refill = [&](int windows, int want) {
         for (int wd = 0; wd < windows; ++wd) {
             const int room = (int)(k + RCAP - produced);
-            if (room <= 0 || produced - k >= TARGET) return;
+            if (room <= 0 || produced - k >= want) return;
             if (idx >= MT_N) {
                 if (!can_twist()) return;
                 twist();
@@ -2548,7 +2550,7 @@ __global__ void __launch_bounds__(64 * (NW + 1)) k_sa_lds_wg1(const int32_t* __r
             const uint32_t x2 = mt_next_lane(x1);
             if (got > 0) {
                 if ((stm >> lane) & 1ull) {
-                    const int e = (int)((produced + __popcll(stm & ltmask)) & 63);
+                    const int e = (int)((produced + __popcll(stm & ltmask)) & (QN - 1));
                     q_i[e] = (int)y;
                     q_u[e] = mt_double(x1, x2);
                     q_end[e] = idx + lane + 3;
@@ -2572,7 +2574,7 @@ __global__ void __launch_bounds__(64 * (NW + 1)) k_sa_lds_wg1(const int32_t* __r
             const uint32_t w2 = mt_temper(mt[idx]);
             idx += 1;
             if (lane == 0) {
-                const int e = (int)(produced & 63);
+                const int e = (int)(produced & (QN - 1));
                 q_i[e] = iv;
                 q_u[e] = mt_double(w1, w2);
                 q_end[e] = idx;
@@ -2586,7 +2588,7 @@ __global__ void __launch_bounds__(64 * (NW + 1)) k_sa_lds_wg1(const int32_t* __r
 #endif
     while (k < nsteps && done == 0) {
         if (parser) {
-            refill(2);
+            refill(4, K);                                  // the round's proposals, if the ring fell short
             if (lane == 0) ctl[0] = (int)(produced - k);   // proposals ready for this round
         }
         __syncthreads();                                   // the round's proposals are published
@@ -2596,18 +2598,22 @@ __global__ void __launch_bounds__(64 * (NW + 1)) k_sa_lds_wg1(const int32_t* __r
         if (nq > K) nq = K;
         if ((int64_t)nq > nsteps - k) nq = (int)(nsteps - k);
         const bool act = !parser && qi < nq;
-        const int iv = act ? q_i[(k + qi) & 63] : 0;
-        const double u = act ? q_u[(k + qi) & 63] : 0.0;
+        const int iv = act ? q_i[(k + qi) & (QN - 1)] : 0;
+        const double u = act ? q_u[(k + qi) & (QN - 1)] : 0.0;
         if (act && gl == 0) atomicOr(&tag[iv], 1u << qi);
-        if (parser) refill(2);                             // while the proposal waves evaluate
         LDS_STAMP(3);
         __syncthreads();                                   // every proposal's tag
         LDS_STAMP(1);
+        int cand = iv;
+        uint32_t cur = 0;
+        bool chg = false;
+        if (parser) {
+            refill(2, RCAP);                               // the next rounds', while the proposal waves evaluate
+        } else {
         const uint32_t old_i = bit_of(0, iv);
         // level 1: i and its neighbours, level 0 with i flipped
         int ri[D];
         nbrs(iv, ri);
-        int cand = iv;
 #pragma unroll
         for (int q = 0; q < D; ++q)
             if (gl == q + 1) cand = ri[q];
@@ -2627,8 +2633,8 @@ __global__ void __launch_bounds__(64 * (NW + 1)) k_sa_lds_wg1(const int32_t* __r
         }
         const uint32_t own = bit_of(0, cand) ^ (cand == iv);
         const uint32_t nb = maj(ones, own);
-        const uint32_t cur = bit_of(1, cand);
-        const bool chg = live && nb != cur;
+        cur = bit_of(1, cand);
+        chg = live && nb != cur;
         const uint32_t cf = live ? (tg & ((1u << qi) - 1u)) : 0u;  // earlier proposals whose i this lane read
         // per group: sum(s_end) change and conflicts
         const u64 up = __ballot(chg && cur == 0u), dn = __ballot(chg && cur != 0u);
@@ -2677,6 +2683,7 @@ __global__ void __launch_bounds__(64 * (NW + 1)) k_sa_lds_wg1(const int32_t* __r
             res_e[qi] = (double)ds;
             if (TRACE) res_e[32 + qi] = dE;
         }
+        }
         LDS_STAMP(4);
         __syncthreads();                                   // every proposal's result
         LDS_STAMP(5);
@@ -2712,7 +2719,7 @@ __global__ void __launch_bounds__(64 * (NW + 1)) k_sa_lds_wg1(const int32_t* __r
         ties += __popcll(__ballot((fl & 2u) != 0u) & tk);
         if (TRACE && w == 0 && lane < taken) {
             const int64_t kk = k + lane;
-            if (st.tr_i) st.tr_i[kk * R + r] = q_i[(k + lane) & 63];
+            if (st.tr_i) st.tr_i[kk * R + r] = q_i[(k + lane) & (QN - 1)];
             if (st.tr_acc) st.tr_acc[kk * R + r] = accq ? 1 : 0;
             if (st.tr_sum) st.tr_sum[kk * R + r] = sum_after;
             if (st.tr_dE) st.tr_dE[kk * R + r] = res_e[32 + lane];
@@ -2772,7 +2779,7 @@ __global__ void __launch_bounds__(64 * (NW + 1)) k_sa_lds_wg1(const int32_t* __r
         // the stream numpy holds after the last proposal taken (before the first:
         // the launch's position), in the state it was drawn from
         const int64_t L = k - 1;
-        const int end = (L < 0) ? idx0 : q_end[L & 63];
+        const int end = (L < 0) ? idx0 : q_end[L & (QN - 1)];
         const bool useb = bak_at >= 0 && L < bak_at;
         for (int q = lane; q < MT_N; q += 64) st.mt[r * MT_N + q] = useb ? mtb[q] : mt[q];
         if (lane == 0) st.mt_idx[r] = end;
