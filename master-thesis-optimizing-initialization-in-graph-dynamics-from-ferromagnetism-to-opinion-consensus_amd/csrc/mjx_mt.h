@@ -29,31 +29,54 @@ __device__ __forceinline__ double mt_double(uint32_t w1, uint32_t w2) {
     return ((double)(w1 >> 5) * 67108864.0 + (double)(w2 >> 6)) / 9007199254740992.0;
 }
 
-// One twist of a 624-word MT19937 state held in LDS, by one wave (the three
-// dependency phases of the recurrence, wave-scope fences between the reads
-// and writes of a phase).
+// One twist of a 624-word MT19937 state held in LDS, by one wave.  The
+// recurrence has three dependency phases (words [0, 227) read only old words,
+// [227, 454) read phase 1's new words, [454, 623) phase 2's, then word 623);
+// within a phase every read is issued before any write (a chunk's last lane
+// reads the next chunk's first word, still old), so a phase is one LDS round
+// trip of reads and one of writes.
 __device__ inline void lds_twist(uint32_t* buf, int lane) {
-    for (int k = lane; k < MT_N - MT_M; k += 64) {
-        const uint32_t v = mt_mix(buf[k], buf[k + 1], buf[k + MT_M]);
-        __builtin_amdgcn_wave_barrier();
-        buf[k] = v;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
+    constexpr int P1 = MT_N - MT_M;                  // 227
+    uint32_t v[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int k = lane + 64 * c;
+        if (k < P1) v[c] = mt_mix(buf[k], buf[k + 1], buf[k + MT_M]);
     }
-    for (int k = MT_N - MT_M + lane; k < 2 * (MT_N - MT_M); k += 64) {
-        const uint32_t v = mt_mix(buf[k], buf[k + 1], buf[k + MT_M - MT_N]);
-        __builtin_amdgcn_wave_barrier();
-        buf[k] = v;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int k = lane + 64 * c;
+        if (k < P1) buf[k] = v[c];
     }
-    for (int k = 2 * (MT_N - MT_M) + lane; k < MT_N - 1; k += 64) {
-        const uint32_t v = mt_mix(buf[k], buf[k + 1], buf[k + MT_M - MT_N]);
-        __builtin_amdgcn_wave_barrier();
-        buf[k] = v;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int k = P1 + lane + 64 * c;
+        if (k < 2 * P1) v[c] = mt_mix(buf[k], buf[k + 1], buf[k - P1]);
     }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int k = P1 + lane + 64 * c;
+        if (k < 2 * P1) buf[k] = v[c];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const int k = 2 * P1 + lane + 64 * c;
+        if (k < MT_N - 1) v[c] = mt_mix(buf[k], buf[k + 1], buf[k - P1]);
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const int k = 2 * P1 + lane + 64 * c;
+        if (k < MT_N - 1) buf[k] = v[c];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
     if (lane == 0) buf[MT_N - 1] = mt_mix(buf[MT_N - 1], buf[0], buf[MT_M - 1]);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
