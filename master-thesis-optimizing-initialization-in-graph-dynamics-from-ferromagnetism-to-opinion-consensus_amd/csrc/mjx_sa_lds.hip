@@ -2065,25 +2065,13 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
             const int np = lc_n[l - 1];
             int nc = 0;
             if (np <= MAXM && lc_fast[l - 1]) {
-                // candidates: member sl = lane / (d+1) of C_{l-1}, j = 0 the member
-                // itself, j > 0 its j-th neighbour; member sl's lane found by
-                // ds_permute (every member pushes its lane id to lane rank) and
-                // ds_bpermute (lane sl's entry pulled)
-                const u64 pm = __ballot(lc_in[l - 1]);
+                // candidates: member sl = lane / (d+1) of C_{l-1} (this wave's list
+                // of level l-1, in lane-rank order), j = 0 the member itself, j > 0
+                // its j-th neighbour: two LDS reads, no cross-lane moves
                 const int sl = lane / DP1, j = lane - sl * DP1;
-                const int rank = __popcll(pm & ltmask);
-                const int slot = __builtin_amdgcn_ds_permute((lc_in[l - 1] ? rank : 63) * 4, lane);
-                const int src = __builtin_amdgcn_ds_bpermute(sl * 4, slot) & 63;
-                const int mc = __shfl(cand, src, 64);
-                int pn[D];
-#pragma unroll
-                for (int e = 0; e < D; ++e) pn[e] = __shfl(nv[e], src, 64);
                 const bool act2 = sl < np;
-                int c2 = mc;
-#pragma unroll
-                for (int e = 0; e < D; ++e)
-                    if (j == e + 1) c2 = pn[e];
-                if (!act2) c2 = iv;
+                const int mc = act2 ? (int)lst[(l - 1) * lc + sl] : iv;
+                int c2 = (act2 && j > 0) ? (int)rows[mc * 4 + (j > 0 ? j - 1 : 0)] : mc;
                 int nv2[D];
                 nbrs(c2, nv2);
                 int ones = 0;
