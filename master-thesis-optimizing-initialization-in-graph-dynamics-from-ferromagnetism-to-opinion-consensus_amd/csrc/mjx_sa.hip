@@ -2260,7 +2260,11 @@ static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d
     auto run = [&](auto kern_plain, auto kern_tape) -> int {
         if (!tape) return launch(kern_plain, st, nsteps);
         const int64_t half = st.tape_cap / 2;
-        if (st.philox_key || half < 1 || nsteps <= 128) {
+        // (a stream under graph capture keeps the one-stream form: no side stream
+        // or per-call events inside a capture)
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        MJX_HIP(hipStreamIsCapturing(hs, &cap), "tape capture status");
+        if (st.philox_key || half < 1 || nsteps <= 128 || cap != hipStreamCaptureStatusNone) {
             // one tape at a time on the caller's stream (the Philox tape is a
             // counter function of t: a few microseconds)
             for (int64_t k0 = 0; k0 < nsteps; k0 += st.tape_cap) {
