@@ -82,3 +82,28 @@ def test_sa_philox_refused_where_mt_is_drawn_in_the_step(mjx_mod):
     sa.layout, sa.cone = "lds", None
     with pytest.raises(mjx_mod.MjxError):
         sa.steps(3)
+
+
+def test_sa_steps_under_graph_capture_equal_eager(mjx_mod):
+    """A stream under hipGraph capture keeps the one-stream MT tape (no side
+    stream inside a capture): steps captured once and replayed twice equal the
+    same steps run eagerly."""
+    import torch
+    n, d, p, c, R = 500, 3, 2, 1, 70
+    adj = mjx_mod.random_regular_graph(d, n, seed=9)
+    seeds = list(range(R))
+    a = mjx_mod.SAReplicas(adj, p, c, seeds, mode="lightcone", layout="rec")
+    b = mjx_mod.SAReplicas(adj, p, c, seeds, mode="lightcone", layout="rec")
+    a.steps(300)                                      # warm-up outside the capture (LDS opt-ins)
+    b.steps(300)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        b.steps(300)
+    g.replay()
+    g.replay()
+    a.steps(300)
+    a.steps(300)
+    torch.cuda.synchronize()
+    ra, rb = a.results(), b.results()
+    assert np.array_equal(ra["conf"], rb["conf"]) and np.array_equal(ra["num_steps"], rb["num_steps"])
