@@ -75,7 +75,8 @@ def parse():
     ap.add_argument("--no-sa", action="store_true")
     ap.add_argument("--giant-n", type=int, default=1_000_000_000)
     ap.add_argument("--giant-d", type=int, default=6)
-    ap.add_argument("--giant-sweeps", type=int, default=10)
+    ap.add_argument("--giant-sweeps", type=int, default=100,
+                    help="timed sweeps of the C5 leg (SURVEY.md 8(d): 100 sweeps)")
     ap.add_argument("--giant-mode", default="binned", choices=["binned", "gather"])
     ap.add_argument("--giant-pieces", type=int, default=None,
                     help="node ranges per rank (exchange of piece g overlaps the sweep of g+1); "
@@ -91,6 +92,10 @@ def parse():
     ap.add_argument("--no-hpr", action="store_true")
     ap.add_argument("--bdcm-iters", type=int, default=100)
     ap.add_argument("--no-bdcm", action="store_true")
+    ap.add_argument("--detail-out", default=None,
+                    help="file for the full JSON object (every leg with its notes and per-replica arrays); the "
+                         "printed line keeps each leg's numbers and ends with a compact `summary` (default "
+                         "gpurun_out/bench_detail.json)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check without a GPU: the ranks join a gloo group, time an empty step and "
                          "rank 0 prints the merged JSON line (tests/test_bench_launch.py)")
@@ -503,6 +508,18 @@ def bench_er(args, rank, world, dist, dev):
 
     step()
     el = _timed(lambda: [step() for _ in range(K)], dist, dev)
+    # the random-row floor of the same step: T sweeps'
+    # rows -- same class arrays, positions, unit mapping and resident grid, no
+    # majority (mjx_gather_floor_class) -- in this process, on this box
+    from mjx import _lib as L, _device as D
+    order, cell, classes = g.class_ell()
+
+    def floor_sweep():
+        L.call("mjx_gather_floor_class", D.ptr(order), D.ptr(cell), classes.ctypes.data, classes.shape[0], n, W,
+               D.ptr(s0), D.ptr(out), D.stream_handle())
+
+    floor_sweep()
+    el_floor = _timed(lambda: [floor_sweep() for _ in range(T * K)], dist, dev)
     nnz = g.nnz
     # degree-class ELL sweep: int32 neighbours + int32 node order + state rows:
     # the deg neighbour rows, the row written, and the node's own row only
@@ -524,6 +541,9 @@ def bench_er(args, rank, world, dist, dev):
         "device_graph_s": gen_s, "class_layout_s": layout_s,
         "layout": "degree-class ELL, one launch per degree class (nb:113-117)",
         "ms_per_step": 1e3 * el / K,
+        # T floor sweeps (the step's rows, no majority, no count): the step over it
+        "floor_ms": 1e3 * el_floor / K, "step_over_floor": el / el_floor,
+        "floor_GBps": bytes_per_sweep * T * K / el_floor / 1e9,
         "node_updates_per_s": world * n * R * T * K / el,
         "algorithmic_bytes_per_sweep": bytes_per_sweep,
         "algorithmic_GBps_per_gpu": bytes_per_sweep * T * K / el / 1e9,
@@ -845,17 +865,24 @@ def bench_giant(args, rank, world, dist, dev):
     el = _timed(run, dist, dev)
     ev_ms = ev0.elapsed_time(ev1)
     per_update_bytes = 4 * d + (d + 2) / 8.0          # 4 d/R + (d+2)/8 at R = 1
+    rows, npieces = sh.range.rows, sh.range.npieces
+    del sh
+    torch.cuda.empty_cache()
     return {
         "config": f"configs[4]: one d={d} RRG N={n} partitioned by node range over {world} GPU(s), "
                   "per-sweep in-place RCCL all-gather of the node-packed state; setup = device generation "
                   "(+ source-binned plan)",
         "scaling": "strong", "ranks": world, "n": n, "d": d, "sweeps": K, "mode": args.giant_mode,
         "setup_s": gen_s,
+        # the C5 job as SURVEY.md 8(d) states it: setup (device generation + plan)
+        # + K sweeps, the two barrier-bracketed regions summed (the state fill
+        # and two warm-up sweeps between them excluded)
+        "job_s": gen_s + el,
         "ms_per_sweep": 1e3 * el / K,
         "node_updates_per_s": n * K / el,
         "algorithmic_GBps": n * K * per_update_bytes / el / 1e9,
         "stream_ms_per_sweep": ev_ms / K,
-        "rows_per_rank": sh.range.rows, "pieces_per_rank": sh.range.npieces,
+        "rows_per_rank": rows, "pieces_per_rank": npieces,
     }
 
 
@@ -888,6 +915,56 @@ def er_sweep_traffic():
     count = sum(v["bytes_per_launch"] for k, v in d.items()
                 if k.startswith("mjx::k_sweep_cls") and ("true" in k or k.startswith("mjx::k_sweep_cls_all_rp")))
     return {"plain_sweep_bytes": plain, "counting_sweep_bytes": count} if plain and count else None
+
+
+LEG_KEYS = ("sa", "sa_c1", "sa_consensus", "sa_global", "er", "hpr", "bdcm", "giant")
+# prose and per-replica arrays: kept in the detail file, not on the printed line
+_DROP = {"config", "sample", "host", "note", "loop_note", "device_loop", "done_num_steps", "source",
+         "replicas", "kind_note"}
+
+
+def compact(v):
+    """A leg's numbers for the printed line: prose, host descriptions and
+    per-replica arrays dropped (they stay in the detail file), floats to 4
+    significant digits."""
+    if isinstance(v, dict):
+        return {k: compact(x) for k, x in v.items() if k not in _DROP and not (isinstance(x, str) and len(x) > 40)}
+    if isinstance(v, list):
+        return [compact(x) for x in v[:8]]
+    if isinstance(v, float):
+        return float(f"{v:.4g}")
+    return v
+
+
+def _get(d, *path):
+    for k in path:
+        if not isinstance(d, dict) or k not in d:
+            return None
+        d = d[k]
+    return float(f"{d:.4g}") if isinstance(d, float) else d
+
+
+def summary(line):
+    """One compact object per SURVEY.md 8 config, the last key of the line:
+    the driver keeps only the tail of stdout, so every leg's headline number
+    sits here."""
+    sg = line.get("sa_global") or {}
+    return {
+        "headline_node_updates_per_s": _get(line, "value"), "headline_frac": _get(line, "roofline", "frac"),
+        "c2_mt_props_per_s": _get(line, "sa", "lightcone", "proposals_per_s"),
+        "c2_philox_props_per_s": _get(line, "sa", "lightcone_philox", "proposals_per_s"),
+        "c2_rollout_props_per_s": _get(line, "sa", "rollout", "proposals_per_s"),
+        "c1_props_per_s": _get(line, "sa_c1", "proposals_per_s"),
+        "c1_cpu_props_per_s": _get(line, "sa_c1", "cpu_baseline", "proposals_per_s"),
+        "sa_global_wall_s": _get(sg, "wall_s_total"), "sa_global_done": sg.get("replicas_done"),
+        "script_size_done": _get(line, "sa_consensus", "script_size", "replicas_done"),
+        "c4_ms_per_step": _get(line, "er", "ms_per_step"), "c4_frac": _get(line, "er", "frac_of_hbm_peak"),
+        "c4_floor_ms": _get(line, "er", "floor_ms"),
+        "c3_hpr_dp_ms": _get(line, "hpr", "loop_state_q", "hpr_dp_ms"),
+        "c3_loop_ms_per_iter": _get(line, "hpr", "loop_state_q", "loop_ms_per_iter"),
+        "c5_ms_per_sweep": _get(line, "giant", "ms_per_sweep"), "c5_setup_s": _get(line, "giant", "setup_s"),
+        "c5_job_s": _get(line, "giant", "job_s"), "c5_sweeps": _get(line, "giant", "sweeps"),
+    }
 
 
 def main():
@@ -1055,7 +1132,17 @@ def main():
             "bdcm": bdcm,
             "giant": giant,
         }
-        print(json.dumps(line), flush=True)
+        detail = args.detail_out or os.path.join(ROOT, "gpurun_out", "bench_detail.json")
+        try:
+            os.makedirs(os.path.dirname(detail), exist_ok=True)
+            with open(detail, "w") as f:
+                json.dump(line, f, indent=1)
+        except OSError as e:
+            print(f"bench.py: could not write {detail}: {e}", file=sys.stderr, flush=True)
+        out = {k: (compact(v) if k in LEG_KEYS else v) for k, v in line.items()}
+        out["detail_file"] = os.path.relpath(detail, ROOT) if detail.startswith(ROOT) else detail
+        out["summary"] = summary(line)                  # the LAST key: inside any tail of the line
+        print(json.dumps(out, separators=(",", ":")), flush=True)
     if dist:
         dist.destroy_process_group()
 

@@ -132,6 +132,12 @@ int mjx_class_ell_fill(const int64_t* row_ptr, const int32_t* col, const int32_t
 int mjx_rollout_class_rp(const int32_t* order, const int32_t* cell, const int64_t* classes, int nclasses,
                          int64_t n, int64_t words, const uint64_t* s_in, uint64_t* s_out, uint64_t* tmp,
                          int steps, unsigned long long* counts, void* stream);
+/* Measurement only (no reference counterpart): the class sweep's memory traffic
+ * without the majority -- per position its D neighbour rows, its own row where D
+ * is even, the rows' XOR written to s_out -- over the same arrays and grid, so
+ * the bench can put the sweeps beside the random-row floor of the state. */
+int mjx_gather_floor_class(const int32_t* order, const int32_t* cell, const int64_t* classes, int nclasses,
+                           int64_t n, int64_t words, const uint64_t* s_in, uint64_t* s_out, void* stream);
 
 /* per-replica count of +1 spins, ADDED into counts (m(s) = (2*count-n)/n) */
 int mjx_popcount_np(const uint64_t* bits, int64_t n, unsigned long long* counts, void* stream);

@@ -36,6 +36,7 @@ SIGNATURES = {
     "mjx_rollout_csr_rp": [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_int, c_vp, c_vp],
     "mjx_class_ell_fill": [c_vp, c_vp, c_vp, c_vp, c_int, c_i64, c_vp, c_vp],
     "mjx_rollout_class_rp": [c_vp, c_vp, c_vp, c_int, c_i64, c_i64, c_vp, c_vp, c_vp, c_int, c_vp, c_vp],
+    "mjx_gather_floor_class": [c_vp, c_vp, c_vp, c_int, c_i64, c_i64, c_vp, c_vp, c_vp],
     "mjx_popcount_np": [c_vp, c_i64, c_vp, c_vp],
     "mjx_popcount_rp": [c_vp, c_i64, c_i64, c_vp, c_vp],
     "mjx_sa_init": [c_vp, c_i64, c_int, c_int, c_int, c_i64, c_vp, c_dbl, c_dbl,

@@ -114,6 +114,11 @@ def run_sa(a):
     from .sa import SAReplicas, sa_run
     R = a.replicas if a.replicas is not None else a.N_stat
     gs = a.graph_seed if a.graph_seed is not None else a.seed
+    if a.stream == "global" and a.gpus > 1:
+        # one numpy stream seeded once (code/SA_RRG.py:58-88): replica k+1's draws
+        # start where replica k's end, so the replicas cannot run side by side
+        raise SystemExit(f"--gpus {a.gpus} with --stream global: the global stream is serial and runs on one "
+                         "device; use --stream independent to spread replicas over devices")
     t0 = time.time()
     if a.stream == "global" or a.gpus == 1:
         res = sa_run(a.d, a.n, a.p, a.c, par_a=a.par_a, par_b=a.par_b, N_stat=R, seed=a.seed, graph_seed=gs,

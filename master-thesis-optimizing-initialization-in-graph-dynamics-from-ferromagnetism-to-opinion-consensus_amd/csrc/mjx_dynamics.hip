@@ -853,6 +853,52 @@ __global__ void __launch_bounds__(kBlock) k_sweep_cls_gen_rp(const int32_t* __re
     count_epilogue<VW, COUNT>(vc, active, unit, 0, Us, lds_cnt, use_lds, counts);
 }
 
+// Gather floor of the degree-class sweep (bench `er.floor_ms`, VERDICT r05
+// item 5): the same positions, class-ELL rows, unit mapping and resident grid
+// as the sweeps, the same rows moved -- a position's D neighbour rows, its own
+// row where D is even (a tie is possible), one row written -- with no majority:
+// the rows' XOR is written instead.  Eight gathers in flight per thread and
+// few VGPRs (more waves than any sweep), so it is what the random 512-B rows
+// of the C4 state cost on this device, not a kernel's choice.
+template <int VW>
+__global__ void __launch_bounds__(kBlock) k_gather_floor_cls(const int32_t* __restrict__ order,
+                                                             const int32_t* __restrict__ cell, GenTable tab,
+                                                             int64_t W, const u64* __restrict__ s_in,
+                                                             u64* __restrict__ s_out, int64_t Us) {
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t slots = ((int64_t)gridDim.x * kBlock) / Us;
+    const int64_t unit = t % Us, slot = t / Us;
+    if (slot >= slots) return;
+    int c = 0;
+    for (int64_t i = slot; i < tab.i0[tab.nc]; i += slots) {
+        while (i >= tab.i0[c + 1]) ++c;
+        const int dd = tab.D[c];
+        const int32_t* row = cell + tab.base[c] + (i - tab.i0[c]) * dd;
+        const int64_t v = order[i];
+        u64 acc[VW];
+        if (dd % 2 == 0) ldv<VW>(s_in + v * W + unit * VW, acc);
+        else {
+#pragma unroll
+            for (int q = 0; q < VW; ++q) acc[q] = 0;
+        }
+        for (int j = 0; j < dd; j += 8) {
+            int32_t k[8];
+#pragma unroll
+            for (int m = 0; m < 8; ++m) k[m] = (j + m < dd) ? row[j + m] : -1;
+            u64 x[8][VW];
+#pragma unroll
+            for (int m = 0; m < 8; ++m)
+                if (k[m] >= 0) ldv<VW>(s_in + (int64_t)k[m] * W + unit * VW, x[m]);
+#pragma unroll
+            for (int m = 0; m < 8; ++m)
+                if (k[m] >= 0)
+#pragma unroll
+                    for (int q = 0; q < VW; ++q) acc[q] ^= x[m][q];
+        }
+        stv<VW>(s_out + v * W + unit * VW, acc);
+    }
+}
+
 // Fills the class-ELL cells of one class from CSR: cell[k*D + j] =
 // col[row_ptr[order[k]] + j], k < cnt.
 __global__ void __launch_bounds__(kBlock) k_class_ell_fill(const int64_t* __restrict__ row_ptr,
@@ -1495,6 +1541,43 @@ extern "C" int mjx_rollout_class_rp(const int32_t* order, const int32_t* cell, c
         return flush_gen();
     };
     return run_rollout(steps, (const u64*)s_in, (u64*)s_out, (u64*)tmp, counts, sweep);
+}
+
+extern "C" int mjx_gather_floor_class(const int32_t* order, const int32_t* cell, const int64_t* classes,
+                                      int nclasses, int64_t n, int64_t words, const uint64_t* s_in, uint64_t* s_out,
+                                      void* stream) {
+    if (n < 1 || words < 1 || !order || !cell || !s_in || !s_out) return MJX_EINVAL;
+    if (n > (int64_t)INT32_MAX) return MJX_ERANGE;
+    if (overlaps(s_in, s_out)) return MJX_EINVAL;
+    int rc = check_classes(classes, nclasses, n);
+    if (rc) return rc;
+    hipStream_t st = as_stream(stream);
+    const int64_t Us = units_of(words);
+    int grid, vw, use_lds; size_t lds;
+    rc = rp_geometry(n, words, Us, &grid, &vw, &use_lds, &lds);
+    if (rc) return rc;
+    // consecutive classes (adjacent in `order`), kMaxGen at a time
+    for (int c0 = 0; c0 < nclasses;) {
+        GenTable tab{};
+        const int64_t g0 = classes[4 * c0];
+        tab.i0[0] = 0;
+        int c = c0;
+        for (; c < nclasses && tab.nc < kMaxGen && classes[4 * c] == g0 + tab.i0[tab.nc]; ++c) {
+            tab.D[tab.nc] = (int)classes[4 * c + 2];
+            tab.base[tab.nc] = classes[4 * c + 3];
+            tab.i0[tab.nc + 1] = tab.i0[tab.nc] + classes[4 * c + 1];
+            ++tab.nc;
+        }
+        auto go = [&](auto kern) {
+            const int g = resident_grid(kern, kBlock, 0, tab.i0[tab.nc] * Us);
+            kern<<<g, kBlock, 0, st>>>(order + g0, cell, tab, words, (const u64*)s_in, (u64*)s_out, Us);
+        };
+        if (vw == 2) go(k_gather_floor_cls<2>);
+        else go(k_gather_floor_cls<1>);
+        MJX_LAUNCH_CHECK("gather_floor_cls");
+        c0 = c;
+    }
+    return MJX_OK;
 }
 
 extern "C" int mjx_rollout_csr_rp(const int64_t* row_ptr, const int32_t* col, int64_t n, int64_t words,

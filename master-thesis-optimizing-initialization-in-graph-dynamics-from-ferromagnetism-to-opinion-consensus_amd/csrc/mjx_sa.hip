@@ -19,6 +19,8 @@
 // evaluated as ((-2*a)*s_i + b*D)/n with separately rounded operations, as
 // numpy does (code/SA_RRG.py:37).
 #include "mjx_common.h"
+#include <map>
+#include <memory>
 #include <mutex>
 #include "mjx_mt.h"
 #include <math.h>
@@ -909,8 +911,9 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t
 // the Philox tape: entry (k, r) = the proposal of step t_r + k of replica r
 // (counter (t lo, t hi, 0, 0), key = philox_key[r]): i = the high 64 bits of
 // (x0 | x1 << 32) * n, u = numpy rand()'s 53-bit double of (x2, x3).  One
-// thread an entry, row k of the tape = k * R + r: coalesced, no state to
-// carry (the step count is the counter).
+// thread an entry, replica-major: entry (k, r) at r * tape_cap + k (the
+// layout include/mjx.h documents; replica r's proposals contiguous), no state
+// to carry (the step count is the counter).
 __global__ void __launch_bounds__(256) k_sa_tape_philox(int64_t n, int64_t R, int64_t K, mjx_sa_state st,
                                                         int32_t* __restrict__ tape_i, double* __restrict__ tape_u) {
     const int64_t total = K * R, ts = st.tape_cap;
@@ -2156,20 +2159,49 @@ extern "C" int mjx_sa_lightcone_prepare(const int32_t* adj, int64_t n, int d, in
 
 // Shared body of the two light-cone entry points: L.s / ns / cs / s0c set by
 // the caller (separate level arrays or the cone layout).
-// a non-blocking side stream per device for the proposal tapes (created once,
-// kept for the process)
-static hipStream_t tape_side_stream() {
+// The proposal-tape side stream of one caller stream: a non-blocking stream
+// on the caller stream's device with the five events of the chunk hand-off,
+// created on first use and kept for the process (a per-device cache keyed by
+// stream): independent callers on different streams draw
+// their tapes on different side streams, never queued behind each other's
+// step events.  `mu` serialises two host threads enqueueing on one stream.
+struct TapeSide {
+    hipStream_t side = nullptr;
+    hipEvent_t ev[5] = {};
+    std::mutex mu;
+};
+
+static TapeSide* tape_side_for(hipStream_t caller) {
     static std::mutex mu;
-    static hipStream_t per[64] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-    std::lock_guard<std::mutex> lk(mu);
-    if (!per[dev]) {
-        hipStream_t s;
-        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
-        per[dev] = s;
+    static std::map<std::pair<int, hipStream_t>, std::unique_ptr<TapeSide>> per;
+    hipDevice_t dev = 0;
+    if (hipStreamGetDevice(caller, &dev) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
     }
-    return per[dev];
+    std::lock_guard<std::mutex> lk(mu);
+    auto& slot = per[{(int)dev, caller}];
+    if (slot) return slot.get();
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess) return nullptr;
+    const bool other = cur != (int)dev;
+    if (other && hipSetDevice(dev) != hipSuccess) return nullptr;
+    auto ts = std::make_unique<TapeSide>();
+    bool ok = hipStreamCreateWithFlags(&ts->side, hipStreamNonBlocking) == hipSuccess;
+    int made = 0;
+    for (; ok && made < 5; ++made)
+        ok = hipEventCreateWithFlags(&ts->ev[made], hipEventDisableTiming) == hipSuccess;
+    if (!ok) {                                   // nothing half-made is kept
+        (void)hipGetLastError();
+        for (int q = 0; q < made; ++q)
+            if (ts->ev[q]) (void)hipEventDestroy(ts->ev[q]);
+        if (ts->side) (void)hipStreamDestroy(ts->side);
+        ts.reset();
+    }
+    if (other) (void)hipSetDevice(cur);
+    if (!ts) return nullptr;
+    slot = std::move(ts);
+    return slot.get();
 }
 
 static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d, int T, int64_t R, LcLevels L,
@@ -2204,8 +2236,7 @@ static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d
     const bool slab32 = L.s0c && n * L.ns * 8 < (int64_t(1) << 31);
     // one launch per tape chunk (the tape kernel fills the chunk's (i, u) first)
     auto launch = [&](auto kern, mjx_sa_state s2, int64_t k) -> int {
-        MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
-                "lightcone lds");
+        MJX_HIP(set_max_lds(kern, (int)lds), "lightcone lds");
         kern<<<(unsigned)(W * split), 64, lds, hs>>>(adj, d, n, R, W, L, T, s2, k, par_a, par_b, a_cap, b_cap,
                                                      t_cap, s2.tape_i, s2.tape_u, split, st.rep_graph);
         MJX_LAUNCH_CHECK("k_sa_lightcone");
@@ -2216,8 +2247,7 @@ static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d
                           !(st.opt_flags & MJX_SA_NO_CONE2);
     auto launch_one_trip = [&](mjx_sa_state s2, int64_t k) -> int {
         auto kern = k_sa_cone2<3>;
-        MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
-                "cone2 lds");
+        MJX_HIP(set_max_lds(kern, (int)lds), "cone2 lds");
         kern<<<(unsigned)(W * split), 64, lds, hs>>>(adj, (const int4*)adj_pad, n, R, W, L, s2, k, par_a, par_b,
                                                      a_cap, b_cap, t_cap, s2.tape_i, s2.tape_u, split, st.rep_graph);
         MJX_LAUNCH_CHECK("k_sa_cone2");
@@ -2235,8 +2265,7 @@ static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d
     const size_t lds_spec = lds + SPEC_LDS;
     auto launch_spec = [&](mjx_sa_state s2, int64_t k) -> int {
         auto go = [&](auto kern, int K) {      // K waves per word column (64 / K replicas per wave)
-            MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)lds_spec), "spec lds");
+            MJX_HIP(set_max_lds(kern, (int)lds_spec), "spec lds");
             kern<<<(unsigned)(W * K), 64, lds_spec, hs>>>(adj, rows4, n, R, W, L, s2, k, par_a, par_b,
                                                                       a_cap, b_cap, t_cap, s2.tape_i, s2.tape_u,
                                                                       hoff, st.rep_graph);
@@ -2291,15 +2320,19 @@ static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d
         // finishes in chunk j may get chunk j+1 drawn anyway: its stream then
         // stands past its last proposal, as with any tape (mt_state() and
         // checkpoint() refuse a tape).
-        hipStream_t side = tape_side_stream();
-        if (!side) return MJX_EHIP;
+        TapeSide* tsd = tape_side_for(hs);
+        if (!tsd) {
+            set_hip_error(hipErrorInvalidValue, "tape side stream");
+            return MJX_EHIP;
+        }
+        std::lock_guard<std::mutex> tlk(tsd->mu);
+        hipStream_t side = tsd->side;
         auto hrc = [](hipError_t e) -> int {
             if (e == hipSuccess) return MJX_OK;
             set_hip_error(e, "tape side stream");
             return MJX_EHIP;
         };
-        hipEvent_t ev[5];
-        for (int q = 0; q < 5; ++q) MJX_HIP(hipEventCreateWithFlags(&ev[q], hipEventDisableTiming), "tape event");
+        hipEvent_t* ev = tsd->ev;        // re-recorded every call: a wait binds the latest record
         hipEvent_t* evT = ev;            // chunk's tape drawn (by half)
         hipEvent_t* evS = ev + 2;        // chunk's steps done (by half)
         int rc = MJX_OK;
@@ -2347,7 +2380,6 @@ static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d
                 if ((rc = hrc(hipEventRecord(evS[j & 1], hs)))) break;
             }
         } while (false);
-        for (int q = 0; q < 5; ++q) (void)hipEventDestroy(ev[q]);
         return rc;
     };
     switch (d) {

@@ -1903,9 +1903,23 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
         idx = 0;
         gen ^= 1;
     };
-    // one window of up to 64 words at idx: at most `room` proposals appended
-    auto parse_window = [&](uint32_t room) {
-        if (idx >= MT_N) twist();
+    // A twist is refused while the last taken proposal (slot pk-1, kept for the
+    // launch's end) still draws from the previous generation: st.mt holds one
+    // old generation only, so the end's generation is never more than one
+    // behind and bit 10's parity names it.  (With nothing pending -- 624 words
+    // parsed without one acceptable proposal, never in practice -- the twist
+    // goes ahead rather than stall.)
+    auto twist_ok = [&]() -> bool {
+        const int lg = (pk > 0u) ? ((q_end[(pk - 1u) & 63u] >> 10) & 1) : 0;
+        return lg == gen || npend == pk;
+    };
+    // one window of up to 64 words at idx: at most `room` proposals appended;
+    // false when a refused twist leaves it for after the round
+    auto parse_window = [&](uint32_t room) -> bool {
+        if (idx >= MT_N) {
+            if (!twist_ok()) return false;
+            twist();
+        }
         const int lim = (MT_N - idx < 64) ? MT_N - idx : 64;
         uint32_t tw = 0, y = 0;
         bool ok = false;
@@ -1933,12 +1947,13 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
             }
             npend += got;
             idx += pos;
-            return;
+            return true;
         }
-        if (room == 0) return;
-        if (!okm) { idx += lim; return; }
+        if (room == 0) return true;
+        if (!okm) { idx += lim; return true; }
         const int f = __ffsll((unsigned long long)okm) - 1;
-        if (f > 0) { idx += f; return; }
+        if (f > 0) { idx += f; return true; }
+        if (idx + 2 >= MT_N && !twist_ok()) return false;
         // i is the window's first word and rand()'s two words cross the end of
         // the state: the serial draw twists between them, as numpy does
         const int iv = __builtin_amdgcn_readlane((int)y, 0);
@@ -1956,6 +1971,7 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
             q_end[q] = idx | (gen << 10);
         }
         npend += 1;
+        return true;
     };
     auto room = [&]() -> uint32_t { return 63u - (npend - pk); };     // slot pk-1 kept
 
@@ -1975,7 +1991,9 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
         if (w == NE) {
             // a full round's proposals before it starts (the ring is normally
             // that far ahead: this parses only at launch start or after a dry spell)
-            while (npend - pk < (uint32_t)NE) parse_window(room());
+            // (a refused twist ends the loop: the round runs on what is pending)
+            while (npend - pk < (uint32_t)NE)
+                if (!parse_window(room())) break;
             if (lane == 0) ctl[0] = (int)npend;
         }
         __syncthreads();                                   // the round's proposals are published
@@ -2198,7 +2216,8 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
 #endif
         } else {
             // the parse wave: windows into the ring's free slots while the round evaluates
-            for (int it = 0; it < 2 && room() >= 8u; ++it) parse_window(room());
+            for (int it = 0; it < 2 && room() >= 8u; ++it)
+                if (!parse_window(room())) break;
             LDS_STAMP(9);
         }
         __syncthreads();                                   // every proposal's marks of every level
@@ -2856,8 +2875,7 @@ extern "C" int mjx_sa_lds_steps(const int32_t* adj, int64_t n, int d, int p, int
     const int64_t W = (R + 63) / 64;
     hipStream_t hs = as_stream(stream);
     auto go = [&](auto kern) -> int {
-        MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, g.bytes),
-                "sa_lds lds");
+        MJX_HIP(set_max_lds(kern, g.bytes), "sa_lds lds");
         kern<<<(unsigned)R, 64, (size_t)g.bytes, hs>>>(adj, d, n, T, R, W, (u64*)s, st, nsteps, par_a, par_b, a_cap,
                                                        b_cap, t_cap, g);
         MJX_LAUNCH_CHECK("k_sa_lds");
@@ -2880,8 +2898,7 @@ extern "C" int mjx_sa_lds_steps(const int32_t* adj, int64_t n, int d, int p, int
     if (!(st.opt_flags & (MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE | MJX_SA_LDS_PAIR)) && (d == 3 || d == 4) && T == 1) {
         const bool trm = st.tr_i || st.tr_acc || st.tr_sum || st.tr_dE;
         auto gom = [&](auto kern) -> int {
-            MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, g.bytes),
-                    "sa_lds lds");
+            MJX_HIP(set_max_lds(kern, g.bytes), "sa_lds lds");
             kern<<<(unsigned)R, 64, (size_t)g.bytes, hs>>>(adj, n, R, W, (u64*)s, st, nsteps, par_a, par_b, a_cap,
                                                            b_cap, t_cap, g);
             MJX_LAUNCH_CHECK("k_sa_lds_multi");
@@ -2921,8 +2938,7 @@ extern "C" int mjx_sa_lds_steps(const int32_t* adj, int64_t n, int d, int p, int
     if (!(st.opt_flags & (MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE)) && (d == 3 || d == 4) && T <= 4 &&
         salds::geometry(n, d, T, &g2, 2)) {
         auto gop = [&](auto kern) -> int {
-            MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, g2.bytes),
-                    "sa_lds lds");
+            MJX_HIP(set_max_lds(kern, g2.bytes), "sa_lds lds");
             kern<<<(unsigned)R, 64, (size_t)g2.bytes, hs>>>(adj, n, R, W, (u64*)s, st, nsteps, par_a, par_b, a_cap,
                                                             b_cap, t_cap, g2);
             MJX_LAUNCH_CHECK("k_sa_lds_pair");
@@ -2942,8 +2958,7 @@ extern "C" int mjx_sa_lds_steps(const int32_t* adj, int64_t n, int d, int p, int
     }
     if (!(st.opt_flags & MJX_SA_LDS_SERIAL) && (d == 3 || d == 4) && T <= 4) {
         auto gof = [&](auto kern) -> int {
-            MJX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, g.bytes),
-                    "sa_lds lds");
+            MJX_HIP(set_max_lds(kern, g.bytes), "sa_lds lds");
             kern<<<(unsigned)R, 64, (size_t)g.bytes, hs>>>(adj, n, R, W, (u64*)s, st, nsteps, par_a, par_b, a_cap,
                                                            b_cap, t_cap, g);
             MJX_LAUNCH_CHECK("k_sa_lds_fast");

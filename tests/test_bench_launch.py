@@ -24,7 +24,7 @@ def _json_lines(out):
     return [json.loads(x) for x in out.splitlines() if x.strip().startswith("{")]
 
 
-@pytest.mark.parametrize("n", [2, 3])
+@pytest.mark.parametrize("n", [2, 3, 8])
 def test_gpus_n_starts_n_ranks_and_prints_one_line(n):
     p = _run(["--gpus", str(n), "--dry-run", "--steps", "3", "--warmup", "1"])
     assert p.returncode == 0, p.stderr
@@ -36,6 +36,24 @@ def test_gpus_n_starts_n_ranks_and_prints_one_line(n):
     assert len(pids) == n and len(set(pids)) == n           # n distinct processes
     assert os.getpid() not in pids
     assert line["steps"] == 3 and line["warmup"] == 1
+
+
+def test_torch_distributed_run_launch_8_ranks():
+    """The driver's own N = 8 command line (python -m torch.distributed.run
+    --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 ... bench.py --gpus 8),
+    dry-run: eight ranks from the launcher's environment, one line from rank 0."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), BENCH, "--gpus", "8", "--dry-run",
+                        "--steps", "3", "--warmup", "1"], capture_output=True, text=True, timeout=240, env=env,
+                       cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    (line,) = _json_lines(p.stdout)
+    assert line["n_gpus"] == 8 and len(set(line["rank_pids"])) == 8
 
 
 def test_gpus_1_is_one_process():

@@ -60,3 +60,13 @@ def test_defaults_match_the_reference_files(mjx_mod):
             assert bd[k] == "np.linspace(1, 2, 3)" and np.allclose(np.linspace(1, 2, 3), v)
         else:
             assert bd[k] == v, k
+
+
+def test_global_stream_refuses_several_gpus(mjx_mod):
+    """--stream global is one numpy stream seeded once (code/SA_RRG.py:58-88),
+    serial by construction: with --gpus > 1 the front refuses instead of
+    quietly running on one device."""
+    cli = _cli(mjx_mod)
+    a = cli.build_parser().parse_args(["sa", "--n", "100", "--gpus", "2", "--stream", "global"])
+    with pytest.raises(SystemExit, match="serial"):
+        cli.run_sa(a)

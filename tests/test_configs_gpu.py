@@ -5,10 +5,12 @@ covered by tests/test_hpr_gpu.py::test_c3_size_sampled_rows).
       sampled replicas' (i, accept, sum_end, delta_H) traces and conf against
       the C restatement of code/SA_RRG.py:63-88 (oracle/orc_majority.c), in
       both SA modes; all 64 replicas identical across the modes.
-  C2  d=3 RRG, N=1e6, p=2, c=1, 4096 replicas: light-cone and full-rollout
-      traces identical for every replica over 50 steps; after 2000 further
-      light-cone steps the cached levels equal fresh rollouts; 20 steps of two
-      sampled replicas against the oracle.
+  C2  d=3 RRG, N=1e6, p=2, c=1, 4096 replicas: light-cone (record layout,
+      side-stream MT19937 tape) and full-rollout traces identical for every
+      replica over one 3000-step call; sampled proposal columns equal
+      np.random.RandomState replays; after 2000 further light-cone steps the
+      cached levels equal fresh rollouts; 20 steps of two sampled replicas
+      against the oracle; two callers on two streams equal sequential runs.
   C4  ER mean degree 5, N=1e7 (device generator), 4096 replicas, p+c-1 = 2:
       degree-class layout == CSR layout (words and per-replica counts); two
       sampled replicas against the oracle's s_endstate (nb:113-123).
@@ -84,21 +86,55 @@ def test_c1_modes_agree_on_every_replica(mjx_mod):
 
 
 # ---------------------------------------------------------------- C2 --------
+C2_K = 3000          # one call: tape chunks 128, 512, 1024, 1024, 312 (ramp + half swaps)
+
+
+def _numpy_proposals(seed, n, K):
+    """The reference's draws for one replica (code/SA_RRG.py:65,73,76): s0 from
+    binomial, then (randint, rand) per step, on np.random.RandomState(seed)."""
+    rs = np.random.RandomState(seed)
+    s0 = 2 * rs.binomial(n=1, p=0.5, size=[n]) - 1
+    i = np.empty(K, dtype=np.int64)
+    u = np.empty(K, dtype=np.float64)
+    for t in range(K):
+        i[t] = rs.randint(low=0, high=n)
+        u[t] = rs.rand()
+    return s0, i, u
+
+
 def test_c2_sa_full_size(mjx_mod):
+    """configs[1] at full size through the side-stream MT19937 tape: one
+    3000-step traced call of the record layout (tape 2048: chunks drawn a chunk
+    ahead on the caller stream's side stream, ramp 128 -> 512 -> 1024, halves
+    swapped) equals the full-rollout mode (proposals drawn in the step) on every
+    replica; sampled replicas' proposal columns equal a RandomState replay."""
     n, d, p, c, R = 1_000_000, 3, 2, 1, 4096
     g = mjx_mod.random_regular_graph_device(d, n, seed=0)
     adj_h = g.adj.cpu().numpy()
     seeds = list(range(R))
     lc = mjx_mod.SAReplicas(g.adj, p, c, seeds, mode="lightcone")
+    assert lc.layout == "rec" and lc.tape_cap == 2048
     ro = mjx_mod.SAReplicas(g.adj, p, c, seeds, mode="rollout")
     assert torch.equal(lc.s, ro.s)                                       # s0 draws
-    K = 50
+    W = lc.W
+    sampled = (0, 1, 2047, R - 1)
+    s0 = {r: _replica(lc.s, n, W, r) for r in sampled}
+    K = C2_K
     ta = {k: v.cpu().numpy() for k, v in lc.steps(K, trace=True).items()}
     tb = {k: v.cpu().numpy() for k, v in ro.steps(K, trace=True).items()}
-    for k in ta:
+    assert ta["i"].shape == (K, R)
+    for k in ta:                                                         # all 4096 replicas, every step
         assert np.array_equal(ta[k], tb[k]), k
     assert torch.equal(lc.s, ro.s) and torch.equal(lc.sum_end, ro.sum_end)
-    assert int(ta["accept"].sum()) > 0
+    assert torch.equal(lc.t, ro.t) and int(lc.t.min().item()) == K
+    assert int(ta["accept"].sum()) > 0 and int((ta["accept"] == 0).sum()) > 0
+    for r in sampled:
+        want_s0, i, u = _numpy_proposals(seeds[r], n, K)
+        assert np.array_equal(s0[r], want_s0), r
+        assert np.array_equal(ta["i"][:, r], i), r
+        # accept = rand() < min(1, exp(-delta_H)) on the traced delta_H (SA_RRG.py:74-77)
+        acc = u < np.minimum(1.0, np.exp(-ta["dE"][:, r]))
+        assert np.array_equal(ta["accept"][:, r].astype(bool), acc), r
     # two sampled replicas against the oracle (20 steps: 3 full rollouts each)
     for r in (0, R - 1):
         o = fast.sa_loop(adj_h, p, c, seeds[r], max_steps=20, trace=True)["trace"]
@@ -106,10 +142,9 @@ def test_c2_sa_full_size(mjx_mod):
         assert np.array_equal(ta["accept"][:20, r], o["accept"]), r
         assert np.array_equal(ta["sum_end"][:20, r], o["sum_end"]), r
         assert np.array_equal(ta["dE"][:20, r], o["dE"]), r
-    del ro
+    del ro, ta, tb
     # 2000 more light-cone steps: the cached levels are still onestep^t(s)
     lc.steps(2000)
-    W = lc.W
     cur = lc.s
     for lvl in lc.levels:
         cur = mjx_mod.rollout(g, cur, 1, words=W)
@@ -118,6 +153,52 @@ def test_c2_sa_full_size(mjx_mod):
     mjx_mod.rollout(g, lc.s, p + c - 1, words=W, counts=cnt)
     assert torch.equal(2 * cnt[:R] - n, lc.sum_end)
     assert int(lc.ties.sum().item()) == 0
+
+
+def test_c2_two_callers_on_two_streams(mjx_mod):
+    """Two independent SAReplicas (configs[1]'s graph, 1024 replicas each, the
+    side-stream tape) driven in alternation on two torch streams, 600-step
+    calls (past the one-stream limit of 128): every trace and final state equals
+    the same runs made one after the other on the default stream.  Each caller
+    stream has its own tape side stream (mjx_sa.hip tape_side_for)."""
+    n, d, p, c, R = 1_000_000, 3, 2, 1, 1024
+    g = mjx_mod.random_regular_graph_device(d, n, seed=0)
+    sa_seeds = (list(range(R)), list(range(50_000, 50_000 + R)))
+    chunks, K = 3, 600
+
+    def run(concurrent):
+        sas = [mjx_mod.SAReplicas(g.adj, p, c, sd, mode="lightcone") for sd in sa_seeds]
+        torch.cuda.synchronize()
+        trs = [[], []]
+        if concurrent:
+            streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+            for _ in range(chunks):
+                for j in (0, 1):
+                    with torch.cuda.stream(streams[j]):
+                        trs[j].append(sas[j].steps(K, trace=True))
+        else:
+            for j in (0, 1):
+                for _ in range(chunks):
+                    trs[j].append(sas[j].steps(K, trace=True))
+        torch.cuda.synchronize()
+        out = []
+        for j in (0, 1):
+            tr = {k: torch.cat([t[k] for t in trs[j]]).cpu().numpy() for k in trs[j][0]}
+            out.append((tr, sas[j].s.clone(), sas[j].sum_end.clone(), sas[j].t.clone()))
+        return out
+
+    seq = run(False)
+    con = run(True)
+    for j in (0, 1):
+        ta, sa_, ea, ta_t = seq[j]
+        tb, sb_, eb, tb_t = con[j]
+        assert ta["i"].shape == (chunks * K, R)
+        for k in ta:
+            assert np.array_equal(ta[k], tb[k]), (j, k)
+        assert torch.equal(sa_, sb_) and torch.equal(ea, eb) and torch.equal(ta_t, tb_t), j
+    # and the first caller's proposals are its own seeds' numpy streams
+    _, i, _ = _numpy_proposals(sa_seeds[0][5], n, chunks * K)
+    assert np.array_equal(con[0][0]["i"][:, 5], i)
 
 
 # ---------------------------------------------------------------- C4 --------

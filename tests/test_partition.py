@@ -1,7 +1,8 @@
 """Node-range partition of one giant graph on CPU:
-world_size 2 and 3 over gloo, the exchange logic of ShardedRRG driven with a
-reference sweep of each rank's rows (oracle/majority.py) must reproduce the
-single-process s_endstate bit for bit.  The HIP local sweep is covered by
+world_size 2, 3 and 8 over gloo (8 with the P > 1 default of two pieces per
+rank, the world and pieces bench.py --gpus 8 runs the C5 leg at), the
+exchange logic of ShardedRRG driven with a reference sweep of each rank's rows
+(oracle/majority.py) must reproduce the single-process s_endstate bit for bit.  The HIP local sweep is covered by
 tests/test_graph_gpu.py."""
 import os
 import socket
@@ -51,7 +52,8 @@ def _worker(rank, world, port, n, d, steps, s0, adj, out, pieces):
 
 @pytest.mark.parametrize("world,n,d,steps,pieces", [(2, 1000, 4, 3, 1), (3, 778, 3, 2, 1), (2, 64, 6, 1, 1),
                                                     (3, 130, 4, 4, 1), (2, 5000, 4, 3, 4), (3, 2000, 3, 2, 3),
-                                                    (2, 300, 6, 2, 4)])
+                                                    (2, 300, 6, 2, 4), (8, 4000, 6, 2, 2), (8, 1000, 3, 3, 2),
+                                                    (8, 640, 4, 2, 2)])
 def test_sharded_rollout_matches_oracle(world, n, d, steps, pieces, mjx_mod):
     from oracle import majority as orc
     adj = mjx_mod.random_regular_graph(d, n, seed=world * 100 + n)
