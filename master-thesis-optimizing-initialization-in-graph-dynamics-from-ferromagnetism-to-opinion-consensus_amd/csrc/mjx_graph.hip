@@ -23,13 +23,18 @@
 namespace mjx {
 namespace gen {
 
-constexpr int kRounds = 6;
+constexpr int kRounds = 4;
 constexpr int kMaxD = 16;
 
+// A keyed pseudorandom permutation of [0, M): an alternating (unbalanced)
+// Feistel network on [0, 2^B), B = ceil(log2 M) split into a high part of a
+// and a low part of B - a bits whose widths swap every round (an even number
+// of rounds restores them), restricted to [0, M) by cycle walking (2^B < 2M:
+// under two steps on average).
 struct Perm {
     uint64_t M;        // domain [0, M)
-    uint32_t mask;     // half-width mask
-    int h;             // half width in bits
+    int a, b;          // widths of the high and low parts, a + b = B
+    uint64_t dmul;     // ceil(2^64 / d) for the stub -> node division (0: d = 1)
     uint32_t key[kRounds];
 };
 
@@ -49,28 +54,37 @@ __host__ __device__ inline uint64_t splitmix64(uint64_t& s) {
     return z ^ (z >> 31);
 }
 
-// balanced Feistel network on [0, 2^(2h))
+__host__ __device__ inline uint32_t wmask(int w) { return (w >= 32) ? 0xffffffffu : ((1u << w) - 1u); }
+
 __host__ __device__ inline uint64_t feistel(const Perm& P, uint64_t v) {
-    uint32_t L = (uint32_t)(v >> P.h), R = (uint32_t)v & P.mask;
+    uint32_t hi = (uint32_t)(v >> P.b), lo = (uint32_t)v & wmask(P.b);
+    int wh = P.a, wl = P.b;
     for (int r = 0; r < kRounds; ++r) {
-        const uint32_t t = L ^ (mix32(R ^ P.key[r]) & P.mask);
-        L = R;
-        R = t;
+        const uint32_t t = hi ^ (mix32(lo ^ P.key[r]) & wmask(wh));
+        hi = lo;
+        lo = t;
+        const int x = wh;
+        wh = wl;
+        wl = x;
     }
-    return ((uint64_t)L << P.h) | R;
+    return ((uint64_t)hi << wl) | lo;
 }
 
 __host__ __device__ inline uint64_t feistel_inv(const Perm& P, uint64_t v) {
-    uint32_t L = (uint32_t)(v >> P.h), R = (uint32_t)v & P.mask;
+    uint32_t hi = (uint32_t)(v >> P.b), lo = (uint32_t)v & wmask(P.b);
+    int wh = P.a, wl = P.b;
     for (int r = kRounds - 1; r >= 0; --r) {
-        const uint32_t t = R ^ (mix32(L ^ P.key[r]) & P.mask);
-        R = L;
-        L = t;
+        const uint32_t ol = hi, oh = lo ^ (mix32(ol ^ P.key[r]) & wmask(wl));
+        hi = oh;
+        lo = ol;
+        const int x = wh;
+        wh = wl;
+        wl = x;
     }
-    return ((uint64_t)L << P.h) | R;
+    return ((uint64_t)hi << wl) | lo;
 }
 
-// cycle walking restricts the permutation to [0, M) (domain < 4M, so a few steps)
+// cycle walking restricts the permutation to [0, M)
 __host__ __device__ inline uint64_t perm_fwd(const Perm& P, uint64_t v) {
     uint64_t x = feistel(P, v);
     while (x >= P.M) x = feistel(P, x);
@@ -85,14 +99,24 @@ __host__ __device__ inline uint64_t perm_inv(const Perm& P, uint64_t v) {
 
 __host__ __device__ inline uint64_t partner(const Perm& P, uint64_t s) { return perm_fwd(P, perm_inv(P, s) ^ 1ull); }
 
-static Perm make_perm(uint64_t M, uint64_t seed) {
+// stub -> node: s / d exactly for s < 2^36 (s * ceil(2^64/d) / 2^64 is off by
+// less than s / 2^64 < 1/d)
+__host__ __device__ inline int64_t stub_node(const Perm& P, uint64_t s) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return P.dmul ? (int64_t)__umul64hi(s, P.dmul) : (int64_t)s;
+#else
+    return P.dmul ? (int64_t)(((unsigned __int128)s * P.dmul) >> 64) : (int64_t)s;
+#endif
+}
+
+static Perm make_perm(uint64_t M, uint64_t seed, int d) {
     Perm P;
     P.M = M;
-    int bits = 1;
+    int bits = 2;
     while ((1ull << bits) < M) ++bits;
-    if (bits & 1) ++bits;
-    P.h = bits / 2;
-    P.mask = (uint32_t)((1ull << P.h) - 1ull);
+    P.a = bits / 2;
+    P.b = bits - P.a;
+    P.dmul = (d > 1) ? (~0ull / (uint64_t)d) + 1ull : 0ull;
     uint64_t s = seed ^ 0x6a09e667f3bcc909ull;
     for (int r = 0; r < kRounds; ++r) P.key[r] = (uint32_t)splitmix64(s);
     return P;
@@ -103,34 +127,35 @@ static Perm make_perm(uint64_t M, uint64_t seed) {
 __global__ void __launch_bounds__(256) k_rrg_rows(Perm P, int64_t n, int d, int64_t lo, int64_t hi,
                                                   int32_t* __restrict__ adj, unsigned long long* __restrict__ defects,
                                                   int64_t cap) {
-    __shared__ unsigned long long ps[kMaxD * 256];
+    __shared__ int32_t ws[kMaxD * 256];          // the row's neighbours
     const int tid = threadIdx.x;
     const int64_t stride = (int64_t)gridDim.x * 256;
     for (int64_t v = (int64_t)blockIdx.x * 256 + tid; v < n; v += stride) {
         const bool mine = v >= lo && v < hi;
         for (int k = 0; k < d; ++k) {
-            const uint64_t p = partner(P, (uint64_t)v * d + k);
-            ps[k * 256 + tid] = p;
-            if (mine) adj[(v - lo) * d + k] = (int32_t)(p / (uint64_t)d);
-        }
-        for (int k = 0; k < d; ++k) {
-            const uint64_t s = (uint64_t)v * d + k, p = ps[k * 256 + tid];
-            const int64_t w = (int64_t)(p / (uint64_t)d);
-            bool bad = false;
-            if (w == v) {
-                bad = s < p;                                   // self-loop, recorded once
-            } else if (v < w) {                                // a repeated neighbour, recorded from the lower end
-                for (int j = 0; j < k; ++j)
-                    if ((int64_t)(ps[j * 256 + tid] / (uint64_t)d) == w) {
-                        bad = true;
-                        break;
-                    }
-            }
-            if (bad) {
+            const uint64_t s = (uint64_t)v * d + k, p = partner(P, s);
+            const int32_t w = (int32_t)stub_node(P, p);
+            ws[k * 256 + tid] = w;
+            if (mine) adj[(v - lo) * d + k] = w;
+            if (w == v && s < p) {                         // a self-loop, recorded once
                 const unsigned long long q = atomicAdd(defects, 1ull);
                 if ((int64_t)q < cap) {
                     defects[1 + 2 * q] = s;
                     defects[2 + 2 * q] = p;
+                }
+            }
+        }
+        for (int k = 1; k < d; ++k) {
+            const int32_t w = ws[k * 256 + tid];
+            if (w == v || v >= w) continue;                // a repeated neighbour, recorded from the lower end
+            bool bad = false;
+            for (int j = 0; j < k; ++j) bad |= ws[j * 256 + tid] == w;
+            if (bad) {
+                const uint64_t s = (uint64_t)v * d + k;
+                const unsigned long long q = atomicAdd(defects, 1ull);
+                if ((int64_t)q < cap) {
+                    defects[1 + 2 * q] = s;
+                    defects[2 + 2 * q] = partner(P, s);     // (rare: recomputed)
                 }
             }
         }
@@ -187,7 +212,7 @@ struct Pairing {
         auto it = ov.find(s);
         return it == ov.end() ? partner(P, s) : it->second;
     }
-    int64_t node(uint64_t s) const { return (int64_t)(s / d); }
+    int64_t node(uint64_t s) const { return stub_node(P, s); }
     int mult(int64_t u, int64_t w) const {
         int m = 0;
         for (uint64_t k = 0; k < d; ++k) m += node(part((uint64_t)u * d + k)) == w;
@@ -237,7 +262,7 @@ using namespace mjx::gen;
 
 extern "C" int64_t mjx_rrg_partner_host(int64_t n, int d, uint64_t seed, int64_t stub) {
     if (n < 2 || d < 1 || stub < 0 || stub >= n * (int64_t)d || (n * (int64_t)d) % 2) return -1;
-    const Perm P = make_perm((uint64_t)n * (uint64_t)d, seed);
+    const Perm P = make_perm((uint64_t)n * (uint64_t)d, seed, d);
     return (int64_t)partner(P, (uint64_t)stub);
 }
 
@@ -248,7 +273,7 @@ extern "C" int mjx_rrg_generate(int64_t n, int d, uint64_t seed, int64_t row_lo,
     if (d > kMaxD || n > (int64_t)INT32_MAX) return MJX_ERANGE;
     if ((row_hi > row_lo && !adj) || !work || work_words < 3) return MJX_EINVAL;
     const int64_t cap = (work_words - 1) / 2;
-    const Perm P = make_perm((uint64_t)n * (uint64_t)d, seed);
+    const Perm P = make_perm((uint64_t)n * (uint64_t)d, seed, d);
     hipStream_t st = as_stream(stream);
     MJX_HIP(hipMemsetAsync(work, 0, sizeof(uint64_t), st), "rrg memset");
     k_rrg_rows<<<grid_for(n, 8), 256, 0, st>>>(P, n, d, row_lo, row_hi, adj, (unsigned long long*)work, cap);
@@ -373,7 +398,7 @@ inline Shape shape(int64_t n, int d, int64_t rows) {
     s.off_len = s.slots + 8 * s.S + 8;
     s.index_len = (s.K + 1) + s.S + (s.S + 1);
     s.msg_words = s.src_len / 64 + 2;
-    s.work_bytes = align256(4 * s.S) + align256(8 * s.S) + kScanScratch + 4 * s.src_len;
+    s.work_bytes = align256(4 * s.S) + align256(8 * s.S) + kScanScratch;
     return s;
 }
 
@@ -448,43 +473,232 @@ __global__ void k_bin_finish(long long* __restrict__ p1, const long long* __rest
     }
 }
 
-// place every slot: rank r inside segment (b, t) (LDS cursor; any order works
-// as long as both layouts use the same r)
-__global__ void __launch_bounds__(256) k_bin_fill(const int32_t* __restrict__ adj, int64_t rows, int d, int64_t n,
-                                                  int64_t K, int64_t T, const long long* __restrict__ p1,
-                                                  const long long* __restrict__ p2, int32_t* __restrict__ src,
-                                                  uint16_t* __restrict__ off) {
-    extern __shared__ unsigned cur[];
-    const int64_t t = blockIdx.x;
-    for (int64_t b = threadIdx.x; b < K; b += 256) cur[b] = 0;
+// the phase-1 stream: per 512-slot chunk 1024 B of 16-bit state-word indices
+// then 256 B of 4-bit bit positions (one contiguous 1280-B piece per chunk,
+// kChunkU16 entries)
+constexpr int kChunkU16 = kChunk + kChunk / 4;
+
+// Place every slot of tile t (one workgroup per tile) straight into the packed
+// phase-1 stream and the phase-2 offsets.  The tile's slots are taken in
+// chunks that fit the LDS; a chunk is counting-sorted by source block there
+// (rank = LDS atomic, so slot order inside a segment is arbitrary: both
+// layouts use the same rank), and its segment runs are written as 4-slot quads
+// by consecutive lanes: a quad is four 16-bit word indices (one 8-B store), one
+// 16-bit entry of four bit positions and four 16-bit destination offsets (one
+// 8-B store), so no slot is scattered on its own and no int32 intermediate
+// exists.  A segment's last 0-3 slots of a chunk are carried in LDS to the
+// next chunk (every run starts quad-aligned); the tile's last carries and the
+// segments' pad slots (zeros) are written at the end, and the last tile also
+// zeroes each source block's tail up to its 512-slot chunk end.  The segment
+// bases come from the t-major index (p1T, p2): one contiguous K-entry read per
+// tile, kept in LDS (the per-slot reads of the b-major p1 they replace were
+// ~0.77 TB of random lines at N=1e9, d=6).
+constexpr int kFillThreads = 1024;
+constexpr int kFillSpt = 16;                    // slots per thread per chunk (at most)
+constexpr int kFillLds = 160 * 1024;
+
+struct FillLds {
+    int64_t cap, ch;                            // staging capacity and chunk slots
+    int64_t bytes;
+};
+inline FillLds fill_lds(int64_t K) {
+    FillLds f;
+    // b1, b2 (8 B each), so and qo (4 B, K+1 each), 32 wave sums, carries (3 slots
+    // of 6 B a segment), cc (1 B)
+    const int64_t fixed = 16 * K + 8 * (K + 1) + 128 + 18 * K + K + 16;
+    const int64_t cap = (kFillLds - fixed) / 6;
+    int64_t ch = ((cap - 3 * K) / kFillThreads) * kFillThreads;
+    if (ch > kFillSpt * kFillThreads) ch = kFillSpt * kFillThreads;
+    f.ch = ch;
+    f.cap = ch + 3 * K;
+    f.bytes = fixed + 6 * f.cap;
+    return f;
+}
+
+// exclusive scans over K <= 2048 entries by 1024 threads, two entries a
+// thread: x -> xs and floor(x/4) -> ys (K+1 entries each; xs may be x: every
+// thread reads its entries before the first barrier)
+__device__ __forceinline__ void scan2(uint32_t* x, uint32_t* xs, uint32_t* ys, int64_t K, uint32_t* wsum) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t i0 = 2 * (int64_t)tid;
+    const uint32_t a0 = (i0 < K) ? x[i0] : 0u, a1 = (i0 + 1 < K) ? x[i0 + 1] : 0u;
+    const uint32_t s = a0 + a1, q = (a0 >> 2) + (a1 >> 2);
+    uint32_t is = s, iq = q;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t us = __shfl_up(is, o, 64), uq = __shfl_up(iq, o, 64);
+        if (lane >= o) {
+            is += us;
+            iq += uq;
+        }
+    }
+    if (lane == 63) {
+        wsum[wave] = is;
+        wsum[16 + wave] = iq;
+    }
     __syncthreads();
-    const int64_t r1 = ((t + 1) * kTile < rows) ? (t + 1) * kTile : rows;
-    for (int64_t q = t * kTile * d + threadIdx.x; q < r1 * d; q += 256) {
-        const int32_t u = adj[q];
-        if (u < 0 || u >= n) continue;
-        const int64_t b = u >> kSrcShift;
-        const unsigned r = atomicAdd(&cur[b], 1u);
-        src[p1[b * T + t] + r] = (int32_t)(u & (kSrc - 1));
-        off[(p2[t * K + b] & ~7ll) + r] = (uint16_t)(q / d - t * kTile);
+    uint32_t bs = 0, bq = 0;
+    for (int w = 0; w < wave; ++w) {
+        bs += wsum[w];
+        bq += wsum[16 + w];
+    }
+    const uint32_t es = bs + is - s, eq = bq + iq - q;
+    if (i0 < K) {
+        xs[i0] = es;
+        ys[i0] = eq;
+    }
+    if (i0 + 1 < K) {
+        xs[i0 + 1] = es + a0;
+        ys[i0 + 1] = eq + (a0 >> 2);
+    }
+    if (tid == kFillThreads - 1) {
+        xs[K] = bs + is;
+        ys[K] = bq + iq;
     }
 }
 
-// int32 source offsets (20 bits) -> the phase-1 stream: per 512-slot chunk
-// 1024 B of 16-bit state-word indices then 256 B of 4-bit bit positions (one
-// contiguous 1280-B piece per chunk, kChunkU16 entries)
-constexpr int kChunkU16 = kChunk + kChunk / 4;
-__global__ void k_bin_pack(const int32_t* __restrict__ src32, int64_t chunks, uint16_t* __restrict__ stream) {
-    const int64_t quads = chunks * (kChunk / 4);
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < quads; i += (int64_t)gridDim.x * blockDim.x) {
-        const int4 x = reinterpret_cast<const int4*>(src32)[i];
-        const int64_t c = i / (kChunk / 4), q = i - c * (kChunk / 4);
-        uint16_t* ch = stream + c * kChunkU16;
-        uint2 l;
-        l.x = ((unsigned)x.x >> 4) | (((unsigned)x.y >> 4) << 16);
-        l.y = ((unsigned)x.z >> 4) | (((unsigned)x.w >> 4) << 16);
-        reinterpret_cast<uint2*>(ch)[q] = l;
-        ch[kChunk + q] = (uint16_t)(((unsigned)x.x & 15u) | (((unsigned)x.y & 15u) << 4) |
-                                    (((unsigned)x.z & 15u) << 8) | (((unsigned)x.w & 15u) << 12));
+// one quad of phase-1 slots at global position g (a multiple of 4): the word
+// indices and bit positions of four 20-bit source offsets
+__device__ __forceinline__ void put_src_quad(uint16_t* __restrict__ stream, int64_t g, const uint32_t* u) {
+    uint16_t* ch = stream + (g >> 9) * kChunkU16;
+    const int w = (int)(g & 511);
+    uint2 l;
+    l.x = (u[0] >> 4) | ((u[1] >> 4) << 16);
+    l.y = (u[2] >> 4) | ((u[3] >> 4) << 16);
+    *reinterpret_cast<uint2*>(ch + w) = l;
+    ch[kChunk + (w >> 2)] =
+        (uint16_t)((u[0] & 15u) | ((u[1] & 15u) << 4) | ((u[2] & 15u) << 8) | ((u[3] & 15u) << 12));
+}
+
+__device__ __forceinline__ void put_off_quad(uint16_t* __restrict__ off, int64_t g, const uint32_t* v) {
+    uint2 l;
+    l.x = v[0] | (v[1] << 16);
+    l.y = v[2] | (v[3] << 16);
+    *reinterpret_cast<uint2*>(off + g) = l;
+}
+
+__global__ void __launch_bounds__(kFillThreads) k_bin_fill(const int32_t* __restrict__ adj, int64_t rows, int d,
+                                                           int64_t n, int64_t K, int64_t T, FillLds fl,
+                                                           const long long* __restrict__ p1T,
+                                                           const long long* __restrict__ p2,
+                                                           const uint32_t* __restrict__ cntB,
+                                                           const long long* __restrict__ blk,
+                                                           uint16_t* __restrict__ stream, uint16_t* __restrict__ off) {
+    extern __shared__ __align__(16) unsigned char fl_raw[];
+    long long* b1 = reinterpret_cast<long long*>(fl_raw);                 // next phase-1 position of (b, t)
+    long long* b2 = b1 + K;                                               // next phase-2 position
+    uint32_t* so = reinterpret_cast<uint32_t*>(b2 + K);                   // chunk counts, then staging starts
+    uint32_t* qo = so + (K + 1);                                          // quad starts
+    uint32_t* wsum = qo + (K + 1);                                        // 32 wave sums
+    uint32_t* cs = wsum + 32;                                             // carried source offsets (3 a segment)
+    uint32_t* ss = cs + 3 * K;                                            // staged source offsets
+    uint16_t* co = reinterpret_cast<uint16_t*>(ss + fl.cap);              // carried destination offsets
+    uint16_t* sv = co + 3 * K;                                            // staged destination offsets
+    uint8_t* cc = reinterpret_cast<uint8_t*>(sv + fl.cap);                // carried count (0..3)
+    const int tid = threadIdx.x;
+    const int64_t t = blockIdx.x;
+    for (int64_t b = tid; b < K; b += kFillThreads) {
+        b1[b] = p1T[t * K + b];
+        b2[b] = p2[t * K + b] & ~7ll;
+        cc[b] = 0;
+    }
+    __syncthreads();
+    const int64_t r1 = ((t + 1) * kTile < rows) ? (t + 1) * kTile : rows;
+    const int64_t qbeg = t * kTile * d, qend = r1 * d;
+    const int per = (int)(fl.ch / kFillThreads);
+    for (int64_t q0 = qbeg; q0 < qend; q0 += fl.ch) {
+        for (int64_t b = tid; b < K; b += kFillThreads) so[b] = cc[b];     // counts start at the carries
+        __syncthreads();
+        // x0 = (u & 0xfffff) | b << 20 (~0: no slot), x1 = v | rank << 16
+        uint32_t x0[kFillSpt], x1[kFillSpt];
+#pragma unroll
+        for (int k = 0; k < kFillSpt; ++k) {
+            x0[k] = 0xffffffffu;
+            x1[k] = 0;
+            const int64_t q = q0 + (int64_t)k * kFillThreads + tid;
+            if (k < per && q < qend) {
+                const int32_t u = adj[q];
+                if (u >= 0 && u < n) {
+                    const uint32_t b = (uint32_t)u >> kSrcShift;
+                    const uint32_t r = atomicAdd(&so[b], 1u);
+                    x0[k] = ((uint32_t)u & (uint32_t)(kSrc - 1)) | (b << kSrcShift);
+                    x1[k] = ((uint32_t)(q - qbeg) / (uint32_t)d) | (r << 16);   // row in the tile
+                }
+            }
+        }
+        __syncthreads();
+        scan2(so, so, qo, K, wsum);                  // staging starts (in place) and quad starts
+        __syncthreads();
+        for (int64_t b = tid; b < K; b += kFillThreads)
+            for (int j = 0; j < cc[b]; ++j) {
+                ss[so[b] + j] = cs[3 * b + j];
+                sv[so[b] + j] = co[3 * b + j];
+            }
+#pragma unroll
+        for (int k = 0; k < kFillSpt; ++k)
+            if (x0[k] != 0xffffffffu) {
+                const uint32_t b = x0[k] >> kSrcShift, at = so[b] + (x1[k] >> 16);
+                ss[at] = x0[k] & (uint32_t)(kSrc - 1);
+                sv[at] = (uint16_t)(x1[k] & 0xffffu);
+            }
+        __syncthreads();
+        // the runs' whole quads: consecutive lanes take consecutive quads
+        const uint32_t Q = qo[K];
+        for (uint32_t qi = tid; qi < Q; qi += kFillThreads) {
+            int64_t lo_b = 0, hi_b = K;                 // the last b with qo[b] <= qi
+            while (hi_b - lo_b > 1) {
+                const int64_t mid = (lo_b + hi_b) >> 1;
+                if (qo[mid] <= qi) lo_b = mid;
+                else hi_b = mid;
+            }
+            const int64_t b = lo_b;
+            const uint32_t j = qi - qo[b], at = so[b] + 4 * j;
+            uint32_t u[4], v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                u[e] = ss[at + e];
+                v[e] = sv[at + e];
+            }
+            put_src_quad(stream, b1[b] + 4 * j, u);
+            put_off_quad(off, b2[b] + 4 * j, v);
+        }
+        __syncthreads();
+        // carries and the segments' next positions
+        for (int64_t b = tid; b < K; b += kFillThreads) {
+            const uint32_t L = so[b + 1] - so[b], nq = L >> 2, rem = L & 3u;
+            for (uint32_t j = 0; j < rem; ++j) {
+                cs[3 * b + j] = ss[so[b] + 4 * nq + j];
+                co[3 * b + j] = sv[so[b] + 4 * nq + j];
+            }
+            cc[b] = (uint8_t)rem;
+            b1[b] += 4 * (int64_t)nq;
+            b2[b] += 4 * (int64_t)nq;
+        }
+        __syncthreads();
+    }
+    // the carries and the pad slots up to each segment's 8-slot end; the last
+    // tile also zeroes each block's tail up to its chunk end
+    for (int64_t b = tid; b < K; b += kFillThreads) {
+        const int64_t c = (int64_t)cntB[b * T + t];
+        const int64_t pend = p1T[t * K + b] + ((c + 7) & ~7ll);
+        int64_t g1 = b1[b], g2 = b2[b];
+        int j = 0;
+        for (; g1 < pend; g1 += 4, g2 += 4) {
+            uint32_t u[4], v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const bool real = j < cc[b];
+                u[e] = real ? cs[3 * b + j] : 0u;
+                v[e] = real ? (uint32_t)co[3 * b + j] : 0u;
+                ++j;
+            }
+            put_src_quad(stream, g1, u);
+            put_off_quad(off, g2, v);
+        }
+        if (t == T - 1) {
+            const uint32_t z[4] = {0u, 0u, 0u, 0u};
+            for (; g1 < blk[b + 1]; g1 += 4) put_src_quad(stream, g1, z);
+        }
     }
 }
 
@@ -928,7 +1142,6 @@ extern "C" int mjx_binned_build(const int32_t* adj, int64_t n, int d, int64_t ro
     uint32_t* cntB = reinterpret_cast<uint32_t*>(work);
     long long* p1 = reinterpret_cast<long long*>(static_cast<char*>(work) + align256(4 * S));
     void* scan = static_cast<char*>(work) + align256(4 * S) + align256(8 * S);
-    int32_t* src = reinterpret_cast<int32_t*>(static_cast<char*>(scan) + kScanScratch);
     long long* blk = index;
     long long* p1T = index + (K + 1);
     long long* p2 = p1T + S;
@@ -937,8 +1150,8 @@ extern "C" int mjx_binned_build(const int32_t* adj, int64_t n, int d, int64_t ro
     MJX_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, need2, p2, p2, S + 1, st), "bin scan size");
     MJX_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, needk, blk, blk, K + 1, st), "bin scan size");
     if ((int64_t)need2 > kScanScratch || (int64_t)needk > kScanScratch) return MJX_ERANGE;
-    MJX_HIP(hipMemsetAsync(src, 0, sizeof(int32_t) * s.src_len, st), "bin memset src");
-    MJX_HIP(hipMemsetAsync(off, 0, sizeof(uint16_t) * s.off_len, st), "bin memset off");
+    const FillLds fl = fill_lds(K);
+    if (K > 2 * kFillThreads || fl.ch < kFillThreads) return MJX_ERANGE;     // (K <= 2048 for n <= INT32_MAX)
     MJX_HIP(hipMemsetAsync(p2 + S, 0, sizeof(long long), st), "bin memset p2");
     MJX_HIP(hipMemsetAsync(blk + K, 0, sizeof(long long), st), "bin memset blk");
     k_bin_count<<<(unsigned)T, 256, K * sizeof(unsigned), st>>>(adj, rows, d, n, K, T, cntB, p2);
@@ -951,10 +1164,10 @@ extern "C" int mjx_binned_build(const int32_t* adj, int64_t n, int d, int64_t ro
     MJX_HIP(hipcub::DeviceScan::ExclusiveSum(scan, needk, blk, blk, K + 1, st), "bin scan blk");
     k_bin_finish<<<mjx::grid_for(S), 256, 0, st>>>(p1, blk, K, T, p1T);
     MJX_LAUNCH_CHECK("k_bin_finish");
-    k_bin_fill<<<(unsigned)T, 256, K * sizeof(unsigned), st>>>(adj, rows, d, n, K, T, p1, p2, src, off);
+    MJX_HIP(mjx::set_max_lds(k_bin_fill, (int)fl.bytes), "k_bin_fill lds");
+    k_bin_fill<<<(unsigned)T, kFillThreads, (size_t)fl.bytes, st>>>(adj, rows, d, n, K, T, fl, p1T, p2, cntB, blk,
+                                                                     src_lo, off);
     MJX_LAUNCH_CHECK("k_bin_fill");
-    k_bin_pack<<<mjx::grid_for(s.src_len / 4), 256, 0, st>>>(src, s.src_len / kChunk, src_lo);
-    MJX_LAUNCH_CHECK("k_bin_pack");
     return MJX_OK;
 }
 
