@@ -93,3 +93,28 @@ def test_bench_reads_committed_pmc_traffic():
     er = bench.er_sweep_traffic()
     assert er is not None
     assert abs(er["counting_sweep_bytes"] / er["plain_sweep_bytes"] - 1) < 0.05
+
+
+def test_printed_line_is_compact_and_ends_with_the_summary():
+    """the driver keeps only the tail of stdout (~8 KB, the
+    record's `tail` 2 KB), so the printed line keeps each leg's numbers, moves
+    prose and per-replica arrays to the detail file, and ends with `summary`
+    (every config's headline number).  Built here from a committed full bench
+    object (round 5's last bench, all legs present)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    line = json.load(open(os.path.join(ROOT, "profiles", "r05_final_b_bench.json")))
+    out = {k: (bench.compact(v) if k in bench.LEG_KEYS else v) for k, v in line.items()}
+    out["detail_file"] = "gpurun_out/bench_detail.json"
+    out["summary"] = bench.summary(line)
+    text = json.dumps(out, separators=(",", ":"))
+    assert len(text) < 7000
+    assert list(out)[-1] == "summary"
+    tail = text[-2000:]
+    for key in ("c2_mt_props_per_s", "c1_props_per_s", "c4_ms_per_step", "c3_hpr_dp_ms", "c5_ms_per_sweep",
+                "c5_setup_s", "sa_global_wall_s"):
+        assert f'"{key}":' in tail, key
+    assert out["summary"]["c2_mt_props_per_s"] > 1e9
+    # the contract's own keys stay whole, cpu_baseline with its sample
+    assert out["cpu_baseline"]["sample"] and out["roofline"]["frac"] == line["roofline"]["frac"]
+    assert "done_num_steps" not in json.dumps(out["sa_consensus"])
