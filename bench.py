@@ -506,11 +506,11 @@ def bench_er(args, rank, world, dist, dev):
         counts.zero_()
         mjx.rollout(g, s0, T, words=W, out=out, tmp=tmp, counts=counts)
 
-    step()
-    el = _timed(lambda: [step() for _ in range(K)], dist, dev)
     # the random-row floor of the same step: T sweeps'
     # rows -- same class arrays, positions, unit mapping and resident grid, no
-    # majority (mjx_gather_floor_class) -- in this process, on this box
+    # majority (mjx_gather_floor_class) -- in this process, on this box.  Step
+    # and floor blocks alternate three times; each is reported as the median
+    # (one block alone can catch a slow spell of the box)
     from mjx import _lib as L, _device as D
     order, cell, classes = g.class_ell()
 
@@ -518,8 +518,13 @@ def bench_er(args, rank, world, dist, dev):
         L.call("mjx_gather_floor_class", D.ptr(order), D.ptr(cell), classes.ctypes.data, classes.shape[0], n, W,
                D.ptr(s0), D.ptr(out), D.stream_handle())
 
+    step()
     floor_sweep()
-    el_floor = _timed(lambda: [floor_sweep() for _ in range(T * K)], dist, dev)
+    els, floors = [], []
+    for _ in range(3):
+        els.append(_timed(lambda: [step() for _ in range(K)], dist, dev))
+        floors.append(_timed(lambda: [floor_sweep() for _ in range(T * K)], dist, dev))
+    el, el_floor = float(np.median(els)), float(np.median(floors))
     nnz = g.nnz
     # degree-class ELL sweep: int32 neighbours + int32 node order + state rows:
     # the deg neighbour rows, the row written, and the node's own row only
@@ -543,6 +548,7 @@ def bench_er(args, rank, world, dist, dev):
         "ms_per_step": 1e3 * el / K,
         # T floor sweeps (the step's rows, no majority, no count): the step over it
         "floor_ms": 1e3 * el_floor / K, "step_over_floor": el / el_floor,
+        "step_ms_reps": [1e3 * x / K for x in els], "floor_ms_reps": [1e3 * x / K for x in floors],
         "floor_GBps": bytes_per_sweep * T * K / el_floor / 1e9,
         "node_updates_per_s": world * n * R * T * K / el,
         "algorithmic_bytes_per_sweep": bytes_per_sweep,
