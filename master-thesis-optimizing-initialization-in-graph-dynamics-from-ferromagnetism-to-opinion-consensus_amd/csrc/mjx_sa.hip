@@ -1476,8 +1476,9 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
                                                 const double* __restrict__ tape_u, int hoff, int gpw,
                                                 const int32_t* __restrict__ rep_graph) {
     // rows as one 16-B load: the padded adjacency (d = 3) or the adjacency itself (d = 4)
-    // gpw: replicas (lane groups) per wave, 64/K (every lane) or fewer (more,
-    // thinner waves: a latency-bound chain per replica, on more SIMDs)
+    // gpw: replicas (lane groups) per wave, 64/K (every lane, the default) or
+    // fewer (more, thinner waves; at configs[1] half-filled waves run 1.5x
+    // slower: the batches are bound by the memory system, not by SIMDs idle)
     static_assert((D == 3 && (TT == 1 || TT == 2)) || (D == 4 && TT == 1), "speculative batches: d=3 T<=2, d=4 T=1");
     extern __shared__ uint32_t lc_lists[];
     static_assert(K == 8 || K == 16, "8 or 16 proposals per batch");
