@@ -1473,12 +1473,9 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
                                                 int64_t n, int64_t R, int64_t W, LcLevels L, mjx_sa_state st,
                                                 int64_t nsteps, double par_a, double par_b, double a_cap,
                                                 double b_cap, int64_t t_cap, const int32_t* __restrict__ tape_i,
-                                                const double* __restrict__ tape_u, int hoff, int gpw,
+                                                const double* __restrict__ tape_u, int hoff,
                                                 const int32_t* __restrict__ rep_graph) {
     // rows as one 16-B load: the padded adjacency (d = 3) or the adjacency itself (d = 4)
-    // gpw: replicas (lane groups) per wave, 64/K (every lane, the default) or
-    // fewer (more, thinner waves; at configs[1] half-filled waves run 1.5x
-    // slower: the batches are bound by the memory system, not by SIMDs idle)
     static_assert((D == 3 && (TT == 1 || TT == 2)) || (D == 4 && TT == 1), "speculative batches: d=3 T<=2, d=4 T=1");
     extern __shared__ uint32_t lc_lists[];
     static_assert(K == 8 || K == 16, "8 or 16 proposals per batch");
@@ -1493,9 +1490,9 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
     const int lane = threadIdx.x;
     const int g = lane / K, k = lane % K;
     const int64_t col = blockIdx.x % W;                       // a column's waves on one XCD when W % 8 == 0
-    const int rl = (int)(blockIdx.x / W) * gpw + g;
+    const int rl = (int)(blockIdx.x / W) * (64 / K) + g;
     const int64_t r = col * 64 + rl;
-    const bool live = g < gpw && r < R;
+    const bool live = r < R;
     const u64 bit = 1ull << (rl & 63);
     const int64_t NS = L.ns, colo = col * L.cs;
     const u64* cone = L.s[0];
@@ -2267,14 +2264,11 @@ static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d
     const int hoff = slots * 64;
     const size_t lds_spec = lds + SPEC_LDS;
     auto launch_spec = [&](mjx_sa_state s2, int64_t k) -> int {
-        auto go = [&](auto kern, int K) {      // wpc waves per word column, 64 / wpc replicas per wave
-            // (opt_split: K = every lane of a wave, 2K / 4K: half / quarter-filled waves)
-            const int wpc = st.opt_split ? st.opt_split : K;
-            if (wpc < K || wpc > 64 || (wpc % K)) return MJX_EINVAL;
+        auto go = [&](auto kern, int K) {      // K waves per word column (64 / K replicas per wave)
             MJX_HIP(set_max_lds(kern, (int)lds_spec), "spec lds");
-            kern<<<(unsigned)(W * wpc), 64, lds_spec, hs>>>(adj, rows4, n, R, W, L, s2, k, par_a, par_b,
-                                                                        a_cap, b_cap, t_cap, s2.tape_i, s2.tape_u,
-                                                                        hoff, 64 / wpc, st.rep_graph);
+            kern<<<(unsigned)(W * K), 64, lds_spec, hs>>>(adj, rows4, n, R, W, L, s2, k, par_a, par_b,
+                                                                      a_cap, b_cap, t_cap, s2.tape_i, s2.tape_u,
+                                                                      hoff, st.rep_graph);
             MJX_LAUNCH_CHECK("k_sa_spec");
             return MJX_OK;
         };

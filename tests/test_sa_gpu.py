@@ -202,31 +202,6 @@ def test_sa_lightcone_wave_split_is_bit_exact(mjx_mod, split):
         assert np.array_equal(tr["sum_end"][:L, r], o["sum_end"])
 
 
-@pytest.mark.parametrize("layout,spec_k,split", [("rec", 8, 16), ("rec", 8, 32), ("cone", 8, 16),
-                                                   ("rec", 16, 32)])
-def test_sa_spec_thin_waves_are_bit_exact(mjx_mod, layout, spec_k, split):
-    """The speculative kernel with fewer replicas per wave (opt_split = waves
-    per word column: 2K -> half the lanes, 4K -> a quarter) only changes the
-    schedule: every trace equals the full-wave kernel's, sampled replicas the
-    oracle's."""
-    n, d, p, c, R = 3000, 3, 2, 1, 200
-    adj = mjx_mod.random_regular_graph(d, n, seed=11)
-    runs = []
-    for kern in ({"spec_k": spec_k}, {"spec_k": spec_k, "split": split}):
-        sa = mjx_mod.SAReplicas(adj, p, c, list(range(R)), mode="lightcone", layout=layout, kernel=kern)
-        tr = {k: v.cpu().numpy() for k, v in sa.steps(700, trace=True).items()}
-        runs.append((tr, sa.s.cpu().numpy(), sa.t.cpu().numpy()))
-    (ta, sa_, tta), (tb, sb_, ttb) = runs
-    for k in ta:
-        assert np.array_equal(ta[k], tb[k]), k
-    assert np.array_equal(sa_, sb_) and np.array_equal(tta, ttb)
-    for r in (0, 77, R - 1):
-        o = orc.sa_loop(adj, p, c, r, max_steps=700, trace=True)["trace"]
-        L = len(o["i"])
-        assert np.array_equal(tb["accept"][:L, r], o["accept"]), r
-        assert np.array_equal(tb["dE"][:L, r], o["dE"]), r
-
-
 def _ref_sa_arrays(full, key):
     return {k: full[f"{key}_{k}"] for k in ("mag_reached", "num_steps", "conf", "graphs")}
 
