@@ -780,13 +780,13 @@ def bench_hpr(args, rank, world, dist, dev):
         "hpr_dp_ms": upd_q, "marginals_ms": marg_q, "hpr_dp_bytes_per_iter": qbytes,
         "hpr_dp_algorithmic_GBps": qbytes / (upd_q / 1e3) / 1e9,
         "hpr_dp_frac_of_hbm_peak": qbytes / (upd_q / 1e3) / 1e9 / HBM_PEAK_GBS,
-        "hpr_dp_traffic_bytes": rocprof_traffic("k_hpr_update_q2"),
+        "hpr_dp_traffic_bytes": rocprof_traffic("k_hpr_update_q3"),
         "marginals_edge_z_traffic_bytes": rocprof_traffic("k_hpr_edge_z_q")}
     # the compute side of the same launch (the DP is a mixed contraction)
     fl = msgs * hpr_dp_flops(d, p, c)
     res["loop_state_q"]["hpr_dp_compute"] = {
         "flops_per_launch": fl, "achieved_tflops": fl / (upd_q / 1e3) / 1e12, "peak_tflops": FP32_VECTOR_PEAK_TFLOPS,
-        "frac": fl / (upd_q / 1e3) / 1e12 / FP32_VECTOR_PEAK_TFLOPS, "sq": sq_counters("k_hpr_update_q2")}
+        "frac": fl / (upd_q / 1e3) / 1e12 / FP32_VECTOR_PEAK_TFLOPS, "sq": sq_counters("k_hpr_update_q3")}
     # the whole loop iteration of code/HPR_pytorch_RRG.py:344-356 (update,
     # marginals, bias refresh, trial configuration, majority check) in
     # hipGraph-replayed batches of 16 with one host read per batch

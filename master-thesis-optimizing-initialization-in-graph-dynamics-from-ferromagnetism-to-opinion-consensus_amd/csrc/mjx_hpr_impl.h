@@ -410,7 +410,7 @@ __host__ __device__ constexpr int qpos(int xs, int xr, int T, int pv) {
 //     biases of tile i+1, read back from LDS (round 5: scalar index loads
 //     share lgkmcnt with the DP's LDS reads and held up its first one, and a
 //     per-lane out_row load made the loop latch wait for the epilogue's
-//     stores; see hpr_update_q2 below, the decay-split form).
+//     stores; see hpr_update_q3 below, the decay-split form).
 constexpr int PIPE_HRS = 129;       // half-row stride (floats) of the incoming-row buffers
 constexpr int PIPE_ORS = 260;       // old-row stride (floats): 1040 B, 16-B aligned DMA bases
 
@@ -662,33 +662,47 @@ struct XaDeal {
 
 constexpr int PIPE_QORS = 132;      // old half-row stride (floats): 528 B, 16-B aligned DMA bases
 
+// The decay-split update with the epilogue of tile t-G run beside the DP of
+// tile t (round 6).  Round 5's form (hpr_update_q2, in git history) separated
+// the two by a barrier (the row sums of every wave), so per tile it ran DP ->
+// barrier -> normalise, damp, store -> barrier.  Here the outputs of the previous tile wait in registers
+// (16 floats a lane) and its row sums in a second `red` slot, and iteration i
+// issues tile i+1's reads, computes tile i's DP, normalises / damps / stores
+// tile i-1 and meets ONE barrier: the epilogue's arithmetic and stores
+// interleave with the DP of the next tile instead of standing between two
+// barriers.  Buffers: incoming halves and biases by tile parity (read by the
+// DP of tile i, written for tile i+1), old half rows by tile parity (written
+// for tile i, read by the epilogue of tile i one iteration later), the index
+// rows in four slots (tiles i-1 .. i+2 live), row sums in two.
 template <int T, int P, int D>
-struct PipeQCfg {
+struct PipeQ3Cfg {
     using C = Cfg<float, T, P, D>;
     static constexpr int NW = 8, NL = C::NL, NT = C::NT;
     static constexpr int RPW = (NL + NW - 1) / NW;
     static constexpr size_t IN = (size_t)64 * PIPE_HRS;         // floats per incoming slot
     static constexpr size_t OLD = (size_t)64 * PIPE_QORS;       // floats per old-row slot
-    static constexpr size_t LDS = (2 * IN + 2 * OLD + 2 * 128 + 3 * 192 + (size_t)NW * 64) * sizeof(float);
+    static constexpr size_t LDS = (2 * IN + 2 * OLD + 2 * 128 + 4 * 192 + 2 * (size_t)NW * 64) * sizeof(float);
     static constexpr int N_A = 2 * RPW + RPW;                   // DMA per wave in A (+3 on wave 0, +2 on wave 1)
+    static constexpr int N_E = 4;                               // 16-B stores per lane in the epilogue
 };
 
 template <int T, int P, int D>
-__device__ __forceinline__ void hpr_update_q2(const float* __restrict__ chi_in, float* __restrict__ chi_out,
+__device__ __forceinline__ void hpr_update_q3(const float* __restrict__ chi_in, float* __restrict__ chi_out,
                                               const float* __restrict__ biases, const int32_t* __restrict__ nbr,
                                               const int32_t* __restrict__ in_row, const int32_t* __restrict__ out_row,
                                               int64_t n, int attr_plus, float w_plus, float w_minus, float damp,
                                               float sc) {
-    using PC = PipeQCfg<T, P, D>;
+    using PC = PipeQ3Cfg<T, P, D>;
     constexpr int X = 1 << T, NC = X * X, H = X / 2, NT = PC::NT, NL = PC::NL, NW = PC::NW, RPW = PC::RPW;
     static_assert(NC == 256 && RPW == 8 && NL <= 64, "decay-split update: 1 KB rows (T = 4, fp32), 64-lane tiles");
     static_assert(Cfg<float, T, P, D>::NVALID == NW, "one valid x_a per wave");
+    static_assert(2 * (H / 4) == PC::N_E, "epilogue stores per lane");
     extern __shared__ __align__(16) unsigned char smem[];
     float* inb = reinterpret_cast<float*>(smem);                  // [2][64][PIPE_HRS] VV | IV halves
     float* oldb = inb + 2 * PC::IN;                               // [2][64][PIPE_QORS] first half rows
     float* biasb = oldb + 2 * PC::OLD;                            // [2][2][64]: b(+1) then b(-1) per lane
-    int32_t* idxb = reinterpret_cast<int32_t*>(biasb + 2 * 128);  // [3][3][64]: in_row, out_row, nbr per slot
-    float* red = reinterpret_cast<float*>(idxb + 3 * 192);        // [NW][64]
+    int32_t* idxb = reinterpret_cast<int32_t*>(biasb + 2 * 128);  // [4][3][64]: in_row, out_row, nbr per slot
+    float* red = reinterpret_cast<float*>(idxb + 4 * 192);        // [2][NW][64]
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int64_t ntiles = (n + NT - 1) / NT;
@@ -713,7 +727,6 @@ __device__ __forceinline__ void hpr_update_q2(const float* __restrict__ chi_in, 
 #pragma unroll
         for (int k = 0; k < RPW; ++k) {
             const int slot = wave * RPW + k;
-            // the M0 base computed outside the lane branch (an SGPR operand)
             const uint32_t dst = __builtin_amdgcn_readfirstlane(
                 old_lds + (uint32_t)((s * PC::OLD + (size_t)slot * PIPE_QORS) * sizeof(float)));
             if (lane < 32) glds16(chi_in + (int64_t)r[k] * NC + lane * 4, dst);
@@ -724,7 +737,7 @@ __device__ __forceinline__ void hpr_update_q2(const float* __restrict__ chi_in, 
     if (t >= ntiles) return;
     const int64_t G = gridDim.x;
     int32_t r[RPW];
-    // ---- prologue: indices of tiles t and t+G; tile t's rows, biases and old rows
+    // ---- prologue: indices of tiles t and t+G; tile t's incoming rows and biases
     if (wave == 0) {
         ti.dma_idx(t, 0);
         ti.dma_idx(t + G, 1);
@@ -734,125 +747,106 @@ __device__ __forceinline__ void hpr_update_q2(const float* __restrict__ chi_in, 
     ti.rows_of(0, 0, r);
     dma_in(r, 0);
     if (wave == 1) ti.dma_bias(0, 0);
-    ti.rows_of(0, 1, r);
-    dma_old(r, 0);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-#ifdef MJX_HPR_PROF
-    unsigned long long _ph[6] = {0, 0, 0, 0, 0, 0}, _tp = __builtin_amdgcn_s_memtime();
-#define PIPE_STAMP(k) do { const unsigned long long _c = __builtin_amdgcn_s_memtime(); _ph[k] += _c - _tp; _tp = _c; } while (0)
-#else
-#define PIPE_STAMP(k) do {} while (0)
-#endif
 
-    for (int it = 0; t < ntiles; ++it, t += G) {
-        const int b = it & 1, s3 = it % 3, s3n = (it + 1) % 3;
-        const int nl = ti.tile_nl(t);
-        const bool active = lane < nl;
-        // ---- A: everything tile t+G reads; the indices of tile t+2G
-        ti.rows_of(s3n, 0, r);
-        dma_in(r, 1 - b);
-        if (wave == 0) ti.dma_idx(t + 2 * G, (it + 2) % 3);
-        if (wave == 1) ti.dma_bias(s3n, 1 - b);
-        ti.rows_of(s3n, 1, r);
-        dma_old(r, 1 - b);
-        PIPE_STAMP(0);
-        // ---- B: DP of tile t
-        const float* rb = inb + b * PC::IN;
-        const float* bb = biasb + b * 128;
+    float outp[X];                 // the previous tile's outputs (this wave's x_a), kept for its epilogue
+#pragma unroll
+    for (int x = 0; x < X; ++x) outp[x] = 0.f;
+    int64_t tp = -1;               // the previous tile (-1: none)
+    for (int it = 0;; ++it, t += G) {
+        const bool cur = t < ntiles;                              // (block-uniform)
+        if (!cur && tp < 0) break;
+        const int b = it & 1, s4 = it & 3, s4n = (it + 1) & 3, s4p = (it + 3) & 3;
         float out[X];
-        float rs = 0.f;
-        if (active) {
-            static_for<0, NW>([&](auto ww) {
-                constexpr int wv = decltype(ww)::value;
-                if (wave == wv) {
-                    constexpr int XP = 2 * XaDeal<T, P, D, 0>::v.q[wv], XM = 2 * XaDeal<T, P, D, 1>::v.q[wv] + 1;
-                    if (attr_plus) rs = xa_messages<float, T, P, D, XP, PIPE_HRS, true, true, 64>(
-                                         rb, bb, a_local_of<D>(lane), lane % D, (XP < X / 2) ? w_plus : w_minus,
-                                         out, sc);
-                    else rs = xa_messages<float, T, P, D, XM, PIPE_HRS, true, true, 64>(
-                                   rb, bb, a_local_of<D>(lane), lane % D, (XM < X / 2) ? w_plus : w_minus, out, sc);
-                }
-            });
-        }
-        red[wave * 64 + lane] = rs;
-        PIPE_STAMP(1);
-        // ---- C: old rows of tile t retired (all but this iteration's A)
-        if (wave == 0) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(PC::N_A + 3) : "memory");
-        else if (wave == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(PC::N_A + 2) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(PC::N_A) : "memory");
-        PIPE_STAMP(2);
-        __builtin_amdgcn_s_barrier();
-        PIPE_STAMP(3);
-        // ---- E: normalise, damp (code/HPR_pytorch_RRG.py:215), store the first half row
-        float4 v[H / 2];
-        int32_t orow = 0;
-        if (active) {
-            float tot = 0.f;
+        if (cur) {
+            // ---- A: tile t+G's incoming halves and biases, tile t+2G's indices,
+            // tile t's old half rows (read by its epilogue, next iteration)
+            ti.rows_of(s4n, 0, r);
+            dma_in(r, 1 - b);
+            if (wave == 0) ti.dma_idx(t + 2 * G, (it + 2) & 3);
+            if (wave == 1) ti.dma_bias(s4n, 1 - b);
+            ti.rows_of(s4, 1, r);
+            dma_old(r, b);
+            // ---- B: DP of tile t
+            const float* rb = inb + b * PC::IN;
+            const float* bb = biasb + b * 128;
+            float rs = 0.f;
 #pragma unroll
-            for (int w = 0; w < NW; ++w) tot += red[w * 64 + lane];
-            const float inv = 1.0f / tot;
-            const float* ol = oldb + b * PC::OLD + lane * PIPE_QORS;
-            orow = ti.orow(s3);
-            // entries (x_a = this wave's valid sender, x_b): VV at q*H + (x_b>>1) for
-            // valid x_b, VI at H*H + q*H + (x_b>>1) for the others
-#pragma unroll
-            for (int half = 0; half < 2; ++half) {
-                const int base = half * H * H + q * H;
-#pragma unroll
-                for (int k = 0; k < H / 4; ++k) {
-                    const float4 ov = *reinterpret_cast<const float4*>(ol + base + 4 * k);
-                    float o[4];
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const int j = 4 * k + e;                        // x_b >> 1
-                        const bool odd = (half == 0) != (attr_plus != 0);
-                        o[e] = odd ? out[2 * j + 1] : out[2 * j];
+            for (int x = 0; x < X; ++x) out[x] = 0.f;
+            if (lane < ti.tile_nl(t)) {
+                static_for<0, NW>([&](auto ww) {
+                    constexpr int wv = decltype(ww)::value;
+                    if (wave == wv) {
+                        constexpr int XP = 2 * XaDeal<T, P, D, 0>::v.q[wv], XM = 2 * XaDeal<T, P, D, 1>::v.q[wv] + 1;
+                        if (attr_plus) rs = xa_messages<float, T, P, D, XP, PIPE_HRS, true, true, 64>(
+                                             rb, bb, a_local_of<D>(lane), lane % D, (XP < X / 2) ? w_plus : w_minus,
+                                             out, sc);
+                        else rs = xa_messages<float, T, P, D, XM, PIPE_HRS, true, true, 64>(
+                                       rb, bb, a_local_of<D>(lane), lane % D, (XM < X / 2) ? w_plus : w_minus, out,
+                                       sc);
                     }
-                    float4 rr;
-                    rr.x = damp * (o[0] * inv) + keep * ov.x;
-                    rr.y = damp * (o[1] * inv) + keep * ov.y;
-                    rr.z = damp * (o[2] * inv) + keep * ov.z;
-                    rr.w = damp * (o[3] * inv) + keep * ov.w;
-                    v[half * (H / 4) + k] = rr;
+                });
+            }
+            red[b * NW * 64 + wave * 64 + lane] = rs;
+        }
+        // ---- E: normalise, damp (code/HPR_pytorch_RRG.py:215) and store the
+        // previous tile's first half rows: sums in red[1-b], old rows in oldb[1-b]
+        if (tp >= 0) {
+            if (lane < ti.tile_nl(tp)) {
+                float tot = 0.f;
+#pragma unroll
+                for (int w = 0; w < NW; ++w) tot += red[(1 - b) * NW * 64 + w * 64 + lane];
+                const float inv = 1.0f / tot;
+                const float* ol = oldb + (1 - b) * PC::OLD + lane * PIPE_QORS;
+                float* dst = chi_out + (int64_t)ti.orow(s4p) * NC;
+                // entries (x_a = this wave's valid sender, x_b): VV at q*H + (x_b>>1) for
+                // valid x_b, VI at H*H + q*H + (x_b>>1) for the others
+#pragma unroll
+                for (int half = 0; half < 2; ++half) {
+                    const int base = half * H * H + q * H;
+#pragma unroll
+                    for (int k = 0; k < H / 4; ++k) {
+                        const float4 ov = *reinterpret_cast<const float4*>(ol + base + 4 * k);
+                        float o[4];
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const int j = 4 * k + e;                        // x_b >> 1
+                            const bool odd = (half == 0) != (attr_plus != 0);
+                            o[e] = odd ? outp[2 * j + 1] : outp[2 * j];
+                        }
+                        float4 rr;
+                        rr.x = damp * (o[0] * inv) + keep * ov.x;
+                        rr.y = damp * (o[1] * inv) + keep * ov.y;
+                        rr.z = damp * (o[2] * inv) + keep * ov.z;
+                        rr.w = damp * (o[3] * inv) + keep * ov.w;
+                        *reinterpret_cast<float4*>(dst + base + 4 * k) = rr;
+                    }
                 }
             }
         }
-        // tile t+G's incoming rows, biases and tile t+2G's indices retired
-        // (tile t+G's old rows may fly on)
-        asm volatile("s_waitcnt vmcnt(%0)" :: "n"(RPW) : "memory");
-        if (active) {
-            float* dst = chi_out + (int64_t)orow * NC;
-#pragma unroll
-            for (int half = 0; half < 2; ++half)
-#pragma unroll
-                for (int k = 0; k < H / 4; ++k)
-                    *reinterpret_cast<float4*>(dst + half * H * H + q * H + 4 * k) = v[half * (H / 4) + k];
-        }
-        PIPE_STAMP(4);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        // every read of A landed (the epilogue's stores, issued after them, may fly);
+        // LDS reads of B and E done before the buffers turn over
+        if (cur && tp >= 0) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(PC::N_E) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        PIPE_STAMP(5);
+        if (!cur) break;
+#pragma unroll
+        for (int x = 0; x < X; ++x) outp[x] = out[x];
+        tp = t;
     }
-#ifdef MJX_HPR_PROF
-    if (lane == 0) {
-        for (int k = 0; k < 6; ++k) atomicAdd(&mjx_hpr_prof[4 + k], _ph[k]);
-        atomicAdd(&mjx_hpr_prof[10 + wave], _ph[1]);
-    }
-#endif
-#undef PIPE_STAMP
 }
 
 // the decay-split layout; scale_in = decay of chi_in's IV quadrants
 template <int T, int P, int D>
-__global__ void __launch_bounds__(512) k_hpr_update_q2(const float* __restrict__ chi_in, float* __restrict__ chi_out,
+__global__ void __launch_bounds__(512) k_hpr_update_q3(const float* __restrict__ chi_in, float* __restrict__ chi_out,
                                                         const float* __restrict__ biases,
                                                         const int32_t* __restrict__ nbr,
                                                         const int32_t* __restrict__ in_row,
                                                         const int32_t* __restrict__ out_row, int64_t n, int attr_plus,
                                                         float w_plus, float w_minus, float damp,
                                                         const float* __restrict__ scale_in) {
-    hpr_update_q2<T, P, D>(chi_in, chi_out, biases, nbr, in_row, out_row, n, attr_plus, w_plus, w_minus, damp,
+    hpr_update_q3<T, P, D>(chi_in, chi_out, biases, nbr, in_row, out_row, n, attr_plus, w_plus, w_minus, damp,
                            *scale_in);
 }
 
@@ -1196,9 +1190,9 @@ static int launch_update_q(const void* chi_in, void* chi_out, const void* biases
     } else {
         const int64_t tiles = (n + C::NT - 1) / C::NT;
         if (tiles > INT32_MAX) return MJX_ERANGE;
-        using PQ = PipeQCfg<T, P, D>;
+        using PQ = PipeQ3Cfg<T, P, D>;
+        auto pk = k_hpr_update_q3<T, P, D>;
         static_assert(PQ::LDS <= 160 * 1024, "decay-split update LDS");
-        auto pk = k_hpr_update_q2<T, P, D>;
         MJX_HIP(set_max_lds(pk, (int)PQ::LDS), "hpr update q set lds");
         const int per = resident_blocks_per_cu((const void*)pk, 512, PQ::LDS);
         int64_t grid = (int64_t)device_cus() * (per > 0 ? per : 1);
@@ -1206,7 +1200,7 @@ static int launch_update_q(const void* chi_in, void* chi_out, const void* biases
         pk<<<(unsigned)grid, 512, PQ::LDS, st>>>((const float*)chi_in, (float*)chi_out, (const float*)biases, nbr,
                                                  in_row, out_row, n, attr_plus, (float)w_plus, (float)w_minus,
                                                  (float)damp, scale_in);
-        MJX_LAUNCH_CHECK("k_hpr_update_q2");
+        MJX_LAUNCH_CHECK("k_hpr_update_q");
         return MJX_OK;
     }
 }

@@ -82,7 +82,7 @@ def main():
     fams = {"k_hpr_update_pipe": lambda b: b == "k_hpr_update_pipe",
             "k_hpr_update": lambda b: b == "k_hpr_update",
             "k_hpr_edge_z": lambda b: b == "k_hpr_edge_z",
-            "k_hpr_update_q2": lambda b: b == "k_hpr_update_q2",
+            "k_hpr_update_q3": lambda b: b == "k_hpr_update_q3",
             "k_hpr_edge_z_q": lambda b: b == "k_hpr_edge_z_q",
             "k_sweep_cls_rp": lambda b: b.startswith("k_sweep_cls"),
             "k_hpr_node_marg": lambda b: b == "k_hpr_node_marg",
