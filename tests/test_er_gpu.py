@@ -103,3 +103,30 @@ def test_er_dynamics_on_device_csr_match_oracle(mjx_mod):
     got = mjx_mod.s_endstate(g, S0, 2, 1)
     for r in (0, 17, 63):
         assert np.array_equal(got[r], orc.s_endstate_er(rp, col, S0[r], 2, 1))
+
+
+def test_gather_floor_moves_the_class_sweep_rows(mjx_mod):
+    """The measurement kernel behind bench.py's er.floor_ms
+    (mjx_gather_floor_class) reads exactly a class sweep's rows: row v of its
+    output is the XOR of v's neighbour rows, and of v's own row where deg(v)
+    is even (nb:113-117: the own spin only breaks ties, which need an even
+    degree) -- on a device ER graph with isolated nodes and a D > 8 tail."""
+    from mjx import _lib as L, _device as D
+    n, W = 20_000, 2
+    g = mjx_mod.erdos_renyi_device(n, 6.0 / (n - 1), seed=5)          # ~50 isolated nodes, a D > 8 tail
+    order, cell, classes = g.class_ell()
+    assert int(classes[:, 2].max()) > 8 and int(classes[0, 2]) == 0
+    s = torch.randint(-2 ** 62, 2 ** 62, (n * W,), dtype=torch.int64, device="cuda")
+    out = torch.zeros_like(s)
+    L.call("mjx_gather_floor_class", D.ptr(order), D.ptr(cell), classes.ctypes.data, classes.shape[0], n, W,
+           D.ptr(s), D.ptr(out), D.stream_handle())
+    rp, col = g.row_ptr.cpu().numpy(), g.col.cpu().numpy()
+    sh = s.view(n, W).cpu().numpy()
+    want = np.zeros_like(sh)
+    deg = np.diff(rp)
+    for v in range(n):
+        acc = np.bitwise_xor.reduce(sh[col[rp[v]:rp[v + 1]]], axis=0) if deg[v] else np.zeros(W, dtype=np.int64)
+        if deg[v] % 2 == 0:
+            acc = acc ^ sh[v]
+        want[v] = acc
+    assert np.array_equal(out.view(n, W).cpu().numpy(), want)
