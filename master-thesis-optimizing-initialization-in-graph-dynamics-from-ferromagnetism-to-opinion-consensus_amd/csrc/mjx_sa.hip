@@ -2161,47 +2161,63 @@ extern "C" int mjx_sa_lightcone_prepare(const int32_t* adj, int64_t n, int d, in
 // the caller (separate level arrays or the cone layout).
 // The proposal-tape side stream of one caller stream: a non-blocking stream
 // on the caller stream's device with the five events of the chunk hand-off,
-// created on first use and kept for the process (a per-device cache keyed by
-// stream): independent callers on different streams draw
-// their tapes on different side streams, never queued behind each other's
-// step events.  `mu` serialises two host threads enqueueing on one stream.
+// created on first use and kept (a per-device cache keyed by stream, SURVEY.md
+// 8(b)): independent callers on different streams draw their tapes on
+// different side streams, never queued behind each other's step events.  `mu`
+// serialises two host threads enqueueing on one stream.  A call holds its
+// entry by shared_ptr, so the cache may retire an entry only when no call holds
+// it and its side stream is idle: past 64 entries (a caller making a fresh
+// stream per call must not grow the cache without bound) one such entry goes.
 struct TapeSide {
     hipStream_t side = nullptr;
     hipEvent_t ev[5] = {};
     std::mutex mu;
+    ~TapeSide() {
+        for (hipEvent_t e : ev)
+            if (e) (void)hipEventDestroy(e);
+        if (side) (void)hipStreamDestroy(side);
+    }
 };
 
-static TapeSide* tape_side_for(hipStream_t caller) {
+static std::shared_ptr<TapeSide> tape_side_for(hipStream_t caller) {
     static std::mutex mu;
-    static std::map<std::pair<int, hipStream_t>, std::unique_ptr<TapeSide>> per;
+    // never destroyed: no HIP call from static destructors at process exit
+    static auto& per = *new std::map<std::pair<int, hipStream_t>, std::shared_ptr<TapeSide>>();
     hipDevice_t dev = 0;
     if (hipStreamGetDevice(caller, &dev) != hipSuccess) {
         (void)hipGetLastError();
         return nullptr;
     }
     std::lock_guard<std::mutex> lk(mu);
-    auto& slot = per[{(int)dev, caller}];
-    if (slot) return slot.get();
+    const std::pair<int, hipStream_t> key{(int)dev, caller};
+    auto hit = per.find(key);
+    if (hit != per.end()) return hit->second;
+    if (per.size() >= 64) {
+        for (auto it = per.begin(); it != per.end(); ++it) {
+            if (it->second.use_count() > 1) continue;                  // a call holds it
+            if (hipStreamQuery(it->second->side) != hipSuccess) {      // tapes still drawing
+                (void)hipGetLastError();
+                continue;
+            }
+            per.erase(it);                                             // (the destructor releases it)
+            break;
+        }
+    }
     int cur = 0;
     if (hipGetDevice(&cur) != hipSuccess) return nullptr;
     const bool other = cur != (int)dev;
     if (other && hipSetDevice(dev) != hipSuccess) return nullptr;
-    auto ts = std::make_unique<TapeSide>();
+    auto ts = std::make_shared<TapeSide>();
     bool ok = hipStreamCreateWithFlags(&ts->side, hipStreamNonBlocking) == hipSuccess;
-    int made = 0;
-    for (; ok && made < 5; ++made)
-        ok = hipEventCreateWithFlags(&ts->ev[made], hipEventDisableTiming) == hipSuccess;
-    if (!ok) {                                   // nothing half-made is kept
+    for (int q = 0; ok && q < 5; ++q)
+        ok = hipEventCreateWithFlags(&ts->ev[q], hipEventDisableTiming) == hipSuccess;
+    if (!ok) {                                   // nothing half-made is kept (the destructor frees it)
         (void)hipGetLastError();
-        for (int q = 0; q < made; ++q)
-            if (ts->ev[q]) (void)hipEventDestroy(ts->ev[q]);
-        if (ts->side) (void)hipStreamDestroy(ts->side);
         ts.reset();
     }
     if (other) (void)hipSetDevice(cur);
-    if (!ts) return nullptr;
-    slot = std::move(ts);
-    return slot.get();
+    if (ts) per[key] = ts;
+    return ts;
 }
 
 static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d, int T, int64_t R, LcLevels L,
@@ -2320,7 +2336,7 @@ static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d
         // finishes in chunk j may get chunk j+1 drawn anyway: its stream then
         // stands past its last proposal, as with any tape (mt_state() and
         // checkpoint() refuse a tape).
-        TapeSide* tsd = tape_side_for(hs);
+        const std::shared_ptr<TapeSide> tsd = tape_side_for(hs);
         if (!tsd) {
             set_hip_error(hipErrorInvalidValue, "tape side stream");
             return MJX_EHIP;

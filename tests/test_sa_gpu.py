@@ -285,3 +285,34 @@ def test_sa_lds_stream_position_in_ragged_calls(mjx_mod, d, p, c, kern):
             rs.rand()
         st = rs.get_state()
         assert np.array_equal(mt[r], st[1].astype(np.uint32)) and int(idx[r]) == st[2], r
+
+
+def test_tape_side_stream_cache_with_a_fresh_stream_per_call(mjx_mod):
+    """A caller that makes a fresh stream for every call: 70 calls of 200
+    steps (the side-stream tape path, > 128 steps a call) on 70 new streams
+    retire idle entries of the per-stream side-stream cache past 64 (no
+    unbounded growth) and give the same traces as the same calls on one
+    stream."""
+    n, d, p, c, R = 3000, 3, 2, 1, 128
+    adj = mjx_mod.random_regular_graph(d, n, seed=13)
+    runs = []
+    for fresh in (False, True):
+        sa = mjx_mod.SAReplicas(adj, p, c, list(range(R)), mode="lightcone", layout="rec")
+        torch.cuda.synchronize()
+        trs = []
+        for _ in range(70):
+            if fresh:
+                st = torch.cuda.Stream()
+                st.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(st):
+                    tr = sa.steps(200, trace=True)
+                torch.cuda.current_stream().wait_stream(st)
+            else:
+                tr = sa.steps(200, trace=True)
+            trs.append({k: v.cpu().numpy() for k, v in tr.items()})
+        runs.append((trs, sa.s.cpu().numpy()))
+    (ta, sa_), (tb, sb_) = runs
+    for x, y in zip(ta, tb):
+        for k in x:
+            assert np.array_equal(x[k], y[k]), k
+    assert np.array_equal(sa_, sb_)
