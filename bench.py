@@ -958,6 +958,7 @@ def summary(line):
     return {
         "headline_node_updates_per_s": _get(line, "value"), "headline_frac": _get(line, "roofline", "frac"),
         "c2_mt_props_per_s": _get(line, "sa", "lightcone", "proposals_per_s"),
+        "c2_sa_sweeps_per_s": _get(line, "sa", "lightcone", "sweeps_per_s"),     # BASELINE.json: SA sweeps/s
         "c2_philox_props_per_s": _get(line, "sa", "lightcone_philox", "proposals_per_s"),
         "c2_rollout_props_per_s": _get(line, "sa", "rollout", "proposals_per_s"),
         "c1_props_per_s": _get(line, "sa_c1", "proposals_per_s"),
