@@ -1443,9 +1443,19 @@ __global__ void __launch_bounds__(64) k_sa_cone2(const int32_t* __restrict__ adj
 // its radius-3 tree; it is the one a sequential run computes unless an earlier
 // proposal of the batch may write one of those nodes, so every proposal's
 // potential writes W_k (i and the positions whose level values it changes) go
-// into a per-replica LDS hash set tagged with the smallest k, and j stands only
-// while no node of R_j carries a tag below j (a ball that is not a tree stands
-// only as the first of a batch).  The batch consumes the proposals before the
+// into a per-replica LDS filter, and j stands only while no node of R_j may be
+// in an earlier W_k (a ball that is not a tree stands only as the first of a
+// batch).  The filter is conservative, never exact-or-nothing: two tables of
+// K-bit proposal masks, slot h1(v) of one and h2(v) of the other, both get
+// proposal k's bit for every v of W_k (a non-returning LDS OR); node v of R_j
+// is taken as written by an earlier proposal when the two slots' masks share a
+// bit below j.  A node that is written is always found; a node that is not is
+// found only when other keys of one earlier proposal cover both of its slots
+// (h1, h2 together are the node's low 22 bits: ~|W_k|^2 / 2048^2), and such a
+// false conflict only ends the batch early -- the proposals after it are
+// evaluated again against the updated state, as after a real one.  (Round 6;
+// before, an exact hash set of (node, min tag) keys: CAS inserts, probe loops
+// on collisions, 20 % of the step and most of a launch's tail.)  The batch consumes the proposals before the
 // first that does not stand and ends after the first that finishes the replica;
 // the rest are drawn again as the next batch.  Acceptance needs no ordering
 // (the schedule a, b depends on the step count only; delta_H on the proposal's
@@ -1456,8 +1466,8 @@ __global__ void __launch_bounds__(64) k_sa_cone2(const int32_t* __restrict__ adj
 // (Two-hop adjacency records -- a node's row and its neighbours' rows in one
 // line -- measured no faster: the 16 MB adjacency is served on-die.)
 // ---------------------------------------------------------------------------
-constexpr int SPEC_LDS = 16384 + 256;  // bytes of hash sets per wave: 64 * K slots per replica (<= K * 18
-                                       // keys), then a dummy insert word per lane
+constexpr int SPEC_FS = 2048;          // filter slots per table per replica (two tables)
+constexpr int SPEC_LDS = 64 * 2 * SPEC_FS / 8;   // bytes of filters per wave: 64/K replicas, K-bit slots
 
 // Diagnostic build only (-DMJX_SA_PROF, tools/sa_prof.py): per-phase s_memtime
 // cycles of k_sa_spec summed over waves; every stamp drains the wave's memory
@@ -1480,9 +1490,8 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
     extern __shared__ uint32_t lc_lists[];
     static_assert(K == 8 || K == 16, "8 or 16 proposals per batch");
     constexpr int T = TT;
-    constexpr int KB = (K == 8) ? 3 : 4;                     // tag bits
-    constexpr int SPEC_HS = 64 * K;                          // hash slots per replica
-    constexpr int HB = (K == 8) ? 9 : 10;                    // log2(SPEC_HS)
+    constexpr int SPW = 32 / K;                              // filter slots per 32-bit word
+    constexpr int FTW = SPEC_FS / SPW;                       // words per filter table
     constexpr u64 GM = (1ull << K) - 1;
     // the step chain is latency-bound: its waves issue first on a SIMD they
     // share with the next chunk's tape waves (drawn on a side stream)
@@ -1497,7 +1506,7 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
     const int64_t NS = L.ns, colo = col * L.cs;
     const u64* cone = L.s[0];
     uint32_t* lists = lc_lists + lane;
-    uint32_t* htab = lc_lists + hoff + g * SPEC_HS;
+    uint32_t* ftab = lc_lists + hoff + g * 2 * FTW;           // this replica's two tables
     if (rep_graph && live) {                                  // this replica's graph of the stack
         const int64_t gi = rep_graph[r];
         adj += gi * n * D;
@@ -1527,83 +1536,44 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
     };
     auto bv = [&](u64 x) -> uint32_t { return (x & bit) ? 1u : 0u; };
     auto maj = [&](int ones, uint32_t own) -> uint32_t { return (2 * ones > D) ? 1u : ((2 * ones < D) ? 0u : own); };
-    auto hslot = [](int32_t v) { return ((uint32_t)v * 0x9E3779B1u) >> (32 - HB); };
-    auto hins = [&](int32_t v) {                             // tag v with min(k) over the group's inserts
-        const uint32_t key = ((uint32_t)v << KB) | (uint32_t)k;
-        uint32_t h = hslot(v);
-        for (;;) {
-            const uint32_t old = atomicCAS(&htab[h], 0xffffffffu, key);
-            if (old == 0xffffffffu) break;
-            if ((old >> KB) == (uint32_t)v) { atomicMin(&htab[h], key); break; }
-            h = (h + 1) & (SPEC_HS - 1);
-        }
+    // the two slots of v: its low 11 bits, and bits 11..21 (xor the next 11)
+    auto fslot1 = [](int32_t v) { return (uint32_t)v & (uint32_t)(SPEC_FS - 1); };
+    auto fslot2 = [](int32_t v) { return (((uint32_t)v >> 11) ^ ((uint32_t)v >> 22)) & (uint32_t)(SPEC_FS - 1); };
+    const uint32_t kbit = 1u << k;
+    const uint32_t below = kbit - 1u;                        // the earlier proposals' bits
+    auto fword = [&](int tbl, uint32_t h) -> uint32_t* { return ftab + tbl * FTW + h / SPW; };
+    auto fshift = [](uint32_t h) -> uint32_t { return (h % SPW) * K; };
+    auto fins = [&](int32_t v) {                             // proposal k may write v
+        const uint32_t h1 = fslot1(v), h2 = fslot2(v);
+        atomicOr(fword(0, h1), kbit << fshift(h1));
+        atomicOr(fword(1, h2), kbit << fshift(h2));
     };
-    // the probe loops past a first slot held by another node (rare: ~40 keys in 512 slots)
-    auto hins_from = [&](int32_t v, uint32_t h) {
-        const uint32_t key = ((uint32_t)v << KB) | (uint32_t)k;
-        for (;;) {
-            const uint32_t old = atomicCAS(&htab[h], 0xffffffffu, key);
-            if (old == 0xffffffffu) return;
-            if ((old >> KB) == (uint32_t)v) { atomicMin(&htab[h], key); return; }
-            h = (h + 1) & (SPEC_HS - 1);
-        }
-    };
-    auto hearlier_from = [&](int32_t v, uint32_t h) -> bool {  // an earlier proposal may write v
-        for (;;) {
-            const uint32_t e = htab[h];
-            if (e == 0xffffffffu) return false;
-            if ((e >> KB) == (uint32_t)v) return (e & (uint32_t)(K - 1)) < (uint32_t)k;
-            h = (h + 1) & (SPEC_HS - 1);
-        }
-    };
-    // N nodes at once, branch-free: every first-slot probe issued before any
-    // result is used (one LDS round trip for the group instead of one per
-    // node), results combined by selects; the probe loops run only where a
-    // first slot holds another node (rare: ~40 keys in 512 slots).  Masked-off
-    // entries probe slot 0 (reads) or the lane's own dummy word (inserts).
-    uint32_t* hdummy = lc_lists + hoff + (64 / K) * SPEC_HS + lane;
-    auto hins_n = [&](const int32_t* vv, const bool* mm, auto nn) {
+    // N nodes at once, branch-free (masked-off entries OR zero / test nothing)
+    auto fins_n = [&](const int32_t* vv, const bool* mm, auto nn) {
         constexpr int N = decltype(nn)::value;
-        uint32_t old[N];
 #pragma unroll
         for (int q = 0; q < N; ++q) {
-            uint32_t* a = mm[q] ? &htab[hslot(vv[q])] : hdummy;
-            old[q] = atomicCAS(a, 0xffffffffu, ((uint32_t)vv[q] << KB) | (uint32_t)k);
-        }
-        bool more = false;
-#pragma unroll
-        for (int q = 0; q < N; ++q) more |= mm[q] && old[q] != 0xffffffffu;
-        if (more) {                       // the node is there already (min tag), or another node is
-#pragma unroll
-            for (int q = 0; q < N; ++q) {
-                if (!mm[q] || old[q] == 0xffffffffu) continue;
-                const uint32_t h = hslot(vv[q]);
-                if ((old[q] >> KB) == (uint32_t)vv[q]) atomicMin(&htab[h], ((uint32_t)vv[q] << KB) | (uint32_t)k);
-                else hins_from(vv[q], (h + 1) & (SPEC_HS - 1));
-            }
+            const uint32_t h1 = fslot1(vv[q]), h2 = fslot2(vv[q]);
+            const uint32_t kb = mm[q] ? kbit : 0u;
+            atomicOr(fword(0, h1), kb << fshift(h1));
+            atomicOr(fword(1, h2), kb << fshift(h2));
         }
     };
-    auto hearlier_n = [&](const int32_t* vv, const bool* mm, auto nn) -> bool {
+    auto fearlier_n = [&](const int32_t* vv, const bool* mm, auto nn) -> bool {
         constexpr int N = decltype(nn)::value;
-        uint32_t e[N];
-#pragma unroll
-        for (int q = 0; q < N; ++q) e[q] = htab[mm[q] ? hslot(vv[q]) : 0u];
-        bool hit = false, slow = false;
+        uint32_t e1[N], e2[N];
 #pragma unroll
         for (int q = 0; q < N; ++q) {
-            const bool occ = mm[q] && e[q] != 0xffffffffu;
-            const bool same = (e[q] >> KB) == (uint32_t)vv[q];
-            hit |= occ && same && (e[q] & (uint32_t)(K - 1)) < (uint32_t)k;
-            slow |= occ && !same;
+            e1[q] = *fword(0, fslot1(vv[q]));
+            e2[q] = *fword(1, fslot2(vv[q]));
         }
-        if (slow) {
+        uint32_t hit = 0;
 #pragma unroll
-            for (int q = 0; q < N; ++q) {
-                if (!mm[q] || e[q] == 0xffffffffu || (e[q] >> KB) == (uint32_t)vv[q]) continue;
-                hit |= hearlier_from(vv[q], (hslot(vv[q]) + 1) & (SPEC_HS - 1));
-            }
+        for (int q = 0; q < N; ++q) {
+            const uint32_t m = (e1[q] >> fshift(fslot1(vv[q]))) & (e2[q] >> fshift(fslot2(vv[q])));
+            hit |= mm[q] ? m : 0u;
         }
-        return hit;
+        return (hit & below) != 0u;
     };
 #ifdef MJX_SA_PROF
     unsigned long long _acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, _t0 = __builtin_amdgcn_s_memtime();
@@ -1628,10 +1598,10 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
     for (;;) {
         const bool going = live && done == 0 && pos < nsteps;
         if (!__any(going)) break;
-        // empty hash sets (16 KB per wave, 16-B stores); lanes then insert into
+        // empty filters (32 KB per wave, 16-B stores); lanes then insert into
         // and read slots other lanes wrote: wave-scope fences at each hand-off
-        for (int q = lane; q < (64 / K) * SPEC_HS / 4; q += 64)
-            reinterpret_cast<uint4*>(lc_lists + hoff)[q] = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
+        for (int q = lane; q < SPEC_LDS / 16; q += 64)
+            reinterpret_cast<uint4*>(lc_lists + hoff)[q] = make_uint4(0u, 0u, 0u, 0u);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
         SA_STAMP(5);
@@ -1804,17 +1774,17 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
             else ds = lc_delta_mlp<D, false>(adj, NS, colo, bit, T, L, lists, i, cnt, &old_i, A0, A1);
         }
         SA_STAMP(2);
-        // the next batch: the rows of its i's neighbours (land during the hash
+        // the next batch: the rows of its i's neighbours (land during the filter
         // phase and the resolution)
 #pragma unroll
         for (int m = 0; m < D; ++m) row(n_A0[m], n_A1[m]);
-        // potential writes of every proposal into the replica's hash set
+        // potential writes of every proposal into the replica's filter
         constexpr int NTW = 1 + D + D * D;                  // tree positions: i, the a_m, their children
         if (mine && listpath) {
-            hins(i);
+            fins(i);
 #pragma unroll
             for (int lv = 1; lv <= T; ++lv)
-                for (int q = 0; q < cnt[lv]; ++q) hins((int32_t)(lists[(L.off[lv] + q) * 64] & 0x7fffffffu));
+                for (int q = 0; q < cnt[lv]; ++q) fins((int32_t)(lists[(L.off[lv] + q) * 64] & 0x7fffffffu));
         } else if (mine && ok) {
             const uint32_t chg = ch1 | ch2;
             int32_t wv[NTW];
@@ -1831,7 +1801,7 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
                     wm[1 + D + m * D + x] = (ch2 >> (1 + D + m * D + x)) & 1u;
                 }
             }
-            hins_n(wv, wm, std::integral_constant<int, NTW>{});
+            fins_n(wv, wm, std::integral_constant<int, NTW>{});
         }
         SA_STAMP(6);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1855,7 +1825,7 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
                     rm[1 + D + m * D + x] = A1[m][x] != i;
                 }
             }
-            bool hit = hearlier_n(rv, rm, std::integral_constant<int, NTW>{});
+            bool hit = fearlier_n(rv, rm, std::integral_constant<int, NTW>{});
             if constexpr (TT == 2) {
                 // the grandchildren, read only under the neighbours that changed at level 1
 #pragma unroll
@@ -1870,7 +1840,7 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
                             gv[x * D + y] = C[m][x][y];
                             gm[x * D + y] = A1[m][x] != i && C[m][x][y] != A0[m];
                         }
-                    hit |= hearlier_n(gv, gm, std::integral_constant<int, D * D>{});
+                    hit |= fearlier_n(gv, gm, std::integral_constant<int, D * D>{});
                 }
             }
             stands = !hit;
@@ -1960,7 +1930,7 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
 #pragma unroll
             for (int x = 0; x < D; ++x) pf_A1[m][x] = n_A1[m][x];
         }
-        // flips land before the next batch reads; the hash reads end before the next clear
+        // flips land before the next batch reads; the filter reads end before the next clear
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
