@@ -2129,6 +2129,7 @@ extern "C" int mjx_sa_lightcone_prepare(const int32_t* adj, int64_t n, int d, in
 
 // Shared body of the two light-cone entry points: L.s / ns / cs / s0c set by
 // the caller (separate level arrays or the cone layout).
+constexpr int64_t kTapeRamp = 16;      // MT19937 tape chunks: 128, 16x, ..., half the tape
 // The proposal-tape side stream of one caller stream: a non-blocking stream
 // on the caller stream's device with the five events of the chunk hand-off,
 // created on first use and kept (a per-device cache keyed by stream, SURVEY.md
@@ -2322,21 +2323,23 @@ static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d
         hipEvent_t* evT = ev;            // chunk's tape drawn (by half)
         hipEvent_t* evS = ev + 2;        // chunk's steps done (by half)
         int rc = MJX_OK;
-        // chunk sizes ramp up (128, x4, ..., half) so that only the first,
-        // short tape is drawn before any step runs: chunk j+1's tape (4x the
-        // rows of chunk j) takes less time than chunk j's steps
+        // chunk sizes ramp up (128, x16, ..., half) so that only the first,
+        // short tape is drawn before any step runs: chunk j+1's tape (16x the
+        // rows of chunk j) takes less time than chunk j's steps (a tape row of
+        // R = 4096 replicas ~0.1 us, a step ~2.5 us), and a call makes few step
+        // launches (each ends on its slowest wave: ~0.1 ms of tail)
         int64_t c0s[2], cks[2];                          // chunk j's first step and size, at j & 1
         int64_t next_k0 = 0, next_c = (half < 128) ? half : 128;
         int64_t nchunks = 0;
         for (int64_t k0 = 0, c = next_c; k0 < nsteps; ++nchunks) {
             k0 += (nsteps - k0 < c) ? nsteps - k0 : c;
-            c = (4 * c < half) ? 4 * c : half;
+            c = (kTapeRamp * c < half) ? kTapeRamp * c : half;
         }
         auto tape_into = [&](int64_t j) -> int {
             c0s[j & 1] = next_k0;
             cks[j & 1] = (nsteps - next_k0 < next_c) ? nsteps - next_k0 : next_c;
             next_k0 += cks[j & 1];
-            next_c = (4 * next_c < half) ? 4 * next_c : half;
+            next_c = (kTapeRamp * next_c < half) ? kTapeRamp * next_c : half;
             int32_t* ti = st.tape_i + (j & 1) * half * R;
             double* tu = st.tape_u + (j & 1) * half * R;
             mjx_sa_state sh = st;

@@ -96,7 +96,7 @@ class SAReplicas:
     """R bit-packed SA replicas on one random regular graph or on a graph per
     replica (device resident)."""
 
-    def __init__(self, N, p, c, seeds, par_a=PAR_A, par_b=PAR_B, a0=None, b0=None, mode="auto", tape=2048,
+    def __init__(self, N, p, c, seeds, par_a=PAR_A, par_b=PAR_B, a0=None, b0=None, mode="auto", tape=4096,
                  mt_state=None, layout="auto", graph_of=None, kernel=None, rng="mt19937"):
         """``N``: one (n, d) neighbour array (or Graph) for every replica, or a
         sequence of them (or a (G, n, d) array): replica r runs on graph r, or
@@ -268,7 +268,8 @@ class SAReplicas:
             # proposal tape: (i, u) of `tape` steps per replica drawn ahead by
             # a wave per replica (0 = draw inside the step kernel); the library
             # draws the MT19937 tape in two halves, one chunk ahead on a side
-            # stream (2048: chunks of 1024 steps)
+            # stream (4096: chunks 128, 2048, 2048, ...: few step launches per
+            # call, each ending on its slowest wave; 12 B per replica and row)
             self.tape_cap = int(tape) if tape else 0
             if self.tape_cap > 0:
                 self.tape_i = torch.empty(self.tape_cap * R, dtype=torch.int32, device=dev)

@@ -86,7 +86,7 @@ def test_c1_modes_agree_on_every_replica(mjx_mod):
 
 
 # ---------------------------------------------------------------- C2 --------
-C2_K = 3000          # one call: tape chunks 128, 512, 1024, 1024, 312 (ramp + half swaps)
+C2_K = 3000          # one call: tape chunks 128, 2048, 824 (ramp + a half reused)
 
 
 def _numpy_proposals(seed, n, K):
@@ -104,16 +104,16 @@ def _numpy_proposals(seed, n, K):
 
 def test_c2_sa_full_size(mjx_mod):
     """configs[1] at full size through the side-stream MT19937 tape: one
-    3000-step traced call of the record layout (tape 2048: chunks drawn a chunk
-    ahead on the caller stream's side stream, ramp 128 -> 512 -> 1024, halves
-    swapped) equals the full-rollout mode (proposals drawn in the step) on every
+    3000-step traced call of the record layout (tape 4096: chunks drawn a chunk
+    ahead on the caller stream's side stream, ramp 128 -> 2048, then the first
+    half again) equals the full-rollout mode (proposals drawn in the step) on every
     replica; sampled replicas' proposal columns equal a RandomState replay."""
     n, d, p, c, R = 1_000_000, 3, 2, 1, 4096
     g = mjx_mod.random_regular_graph_device(d, n, seed=0)
     adj_h = g.adj.cpu().numpy()
     seeds = list(range(R))
     lc = mjx_mod.SAReplicas(g.adj, p, c, seeds, mode="lightcone")
-    assert lc.layout == "rec" and lc.tape_cap == 2048
+    assert lc.layout == "rec" and lc.tape_cap == 4096
     ro = mjx_mod.SAReplicas(g.adj, p, c, seeds, mode="rollout")
     assert torch.equal(lc.s, ro.s)                                       # s0 draws
     W = lc.W
