@@ -19,10 +19,12 @@ cases = [x.split(":") for x in os.environ.get(
     "SA_CASES", "mt19937:2048:2000,mt19937:8192:2000,philox:2048:2000,philox:512:2000").split(",")]
 reps = int(os.environ.get("SA_REPS", "3"))
 sas = {}
-for rng, tape, K in cases:
-    sa = mjx.SAReplicas(adj, p, c, np.arange(R), mode="lightcone", rng=rng, tape=int(tape))
+for case in cases:                     # rng:tape:K[:spec_k]
+    rng, tape, K = case[:3]
+    kern = {"spec_k": int(case[3])} if len(case) > 3 else None
+    sa = mjx.SAReplicas(adj, p, c, np.arange(R), mode="lightcone", rng=rng, tape=int(tape), kernel=kern)
     sa.steps(10000)
-    sas[(rng, tape, K)] = sa
+    sas[tuple(case)] = sa
 torch.cuda.synchronize()
 res = {k: [] for k in sas}
 for rep in range(reps):
@@ -33,7 +35,7 @@ for rep in range(reps):
         sa.steps(K)
         torch.cuda.synchronize()
         res[key].append(1e6 * (time.perf_counter() - t0) / K)
-        print(f"rep {rep} {key[0]} tape={key[1]} K={K}: {res[key][-1]:.3f} us/step", flush=True)
+        print(f"rep {rep} {':'.join(key)}: {res[key][-1]:.3f} us/step", flush=True)
 for key, v in res.items():
-    print(f"{key[0]:8s} tape={key[1]:>5s} K={key[2]:>5s}: median {np.median(v):.3f} us/step "
+    print(f"{':'.join(key):24s}: median {np.median(v):.3f} us/step "
           f"= {R / np.median(v) * 1e6:.3e} proposals/s", flush=True)
