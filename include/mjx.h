@@ -198,6 +198,12 @@ typedef struct mjx_sa_state {
      * steps that draw inside the kernel (mjx_sa_steps, mjx_sa_lds_steps)
      * refuse it (MJX_EINVAL). */
     const uint64_t* philox_key;   /* [R] */
+    /* library-kept: 1 while the neighbour words of a d = 3, p+c-1 = 2 record
+     * array (mjx_sa_rec_*) are current.  mjx_sa_rec_pack writes them; the
+     * speculative steps keep them; any other light-cone kernel leaves them
+     * stale and sets 0; the next speculative call rebuilds them first.  Start
+     * at 0 (a zeroed struct). */
+    int32_t   rec_nb;
 } mjx_sa_state;
 
 #define MJX_SA_NO_SPEC   1u   /* no speculative batches (k_sa_spec) */
@@ -284,10 +290,14 @@ int mjx_sa_cone_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int
  * node's adjacency row (int32 x4, zero padded): rec[(w*n + v)*LV + e], words
  * 0..1 = the row, word 2 + t = level t, LV = mjx_sa_rec_words(d,p,c) (4 or 8;
  * -1 if unsupported: d <= 4, p+c-1 <= 5).  The speculative step then fetches a
- * ball node's row and levels in one line.  One graph shared by every replica
+ * ball node's row and levels in one line.  At d = 3, p+c-1 = 2 the record's
+ * spare 28 bytes (the row's pad int, words 5..7) hold its neighbours' level-1
+ * bits, 3 per replica (st->rec_nb).  One graph shared by every replica
  * (st->rep_graph must be NULL).  Same proposals, accepts and outputs as every
  * other layout. */
 int mjx_sa_rec_words(int d, int p, int c);
+/* sizeof(mjx_sa_state) as the library was built (a binding checks its mirror) */
+int mjx_sa_state_bytes(void);
 int mjx_sa_rec_pack(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R, const uint64_t* s,
                     uint64_t* const* levels, uint64_t* rec, void* stream);
 int mjx_sa_rec_unpack(int64_t n, int d, int p, int c, int64_t R, const uint64_t* rec, uint64_t* s,

@@ -60,6 +60,7 @@ SIGNATURES = {
     "mjx_sa_cone_steps": [c_vp, c_vp, c_i64, c_int, c_int, c_int, c_i64, c_vp, c_vp, c_vp,
                           c_i64, c_dbl, c_dbl, c_dbl, c_dbl, c_i64, c_vp],
     "mjx_sa_rec_words": [c_int, c_int, c_int],
+    "mjx_sa_state_bytes": [],
     "mjx_sa_rec_pack": [c_vp, c_i64, c_int, c_int, c_int, c_i64, c_vp, c_vp, c_vp, c_vp],
     "mjx_sa_rec_unpack": [c_i64, c_int, c_int, c_int, c_i64, c_vp, c_vp, c_vp, c_vp],
     "mjx_sa_rec_steps": [c_vp, c_vp, c_i64, c_int, c_int, c_int, c_i64, c_vp, c_vp, c_vp,
@@ -126,7 +127,7 @@ class MjxSaState(ctypes.Structure):
         ("tr_i", c_vp), ("tr_acc", c_vp), ("tr_sum", c_vp), ("tr_dE", c_vp), ("tr_tie", c_vp),
         ("tape_i", c_vp), ("tape_u", c_vp), ("tape_cap", c_i64),
         ("rep_graph", c_vp), ("opt_split", ctypes.c_int32), ("opt_spec_k", ctypes.c_int32),
-        ("opt_flags", ctypes.c_uint32), ("philox_key", c_vp),
+        ("opt_flags", ctypes.c_uint32), ("philox_key", c_vp), ("rec_nb", ctypes.c_int32),
     ]
 
 
@@ -154,9 +155,13 @@ def verify_build_id(lib, csrc=None, include=None):
 
 def open_library(path, verify=True):
     """dlopen a build of libmjx.so and declare every entry point; with
-    ``verify`` the build id must match the source tree (verify_build_id)."""
+    ``verify`` the build id must match the source tree (verify_build_id).
+    Unverified (an A/B build of older sources, tools/ab_lib.py) an entry point
+    the build lacks is left undeclared."""
     lib = ctypes.CDLL(path)
     for name, argtypes in SIGNATURES.items():
+        if not verify and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.argtypes = argtypes
         fn.restype = _RESTYPES.get(name, c_int)

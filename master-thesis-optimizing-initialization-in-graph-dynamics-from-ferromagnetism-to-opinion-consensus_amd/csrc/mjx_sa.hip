@@ -1166,7 +1166,47 @@ struct ConeRd {
         const v4u32_t x = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(idx * 8u), 0, kSc1);
         return make_int4((int)x.x, (int)x.y, (int)x.z, (int)x.w);
     }
+    __device__ __forceinline__ uint32_t u32(uint32_t idx, uint32_t byte) const {  // 4 B at a byte offset of a record
+        return __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(idx * 8u + byte), 0, kSc1);
+    }
 };
+
+// The neighbour words of a d = 3, p+c-1 = 2 record (64 B: row in bytes 0..11,
+// levels 0..2 in bytes 16..39): level 1 of the node's three neighbours, 3 bits
+// per replica of the column -- replica q's bits (neighbour y = 0..2 of the row)
+// at bit 3*(q % 10) + y of the 32-bit word q / 10, words 0..5 in bytes 40..63
+// and word 6 in the row's pad (bytes 12..15).  The speculative batch reads a
+// child's record whole and so has its children's level-1 values with its own
+// (no round trip of their own after level 1); every level-1 flip of a node
+// XORs its bit into the records of its neighbours.
+__host__ __device__ inline uint32_t nb_byte(int q) { return (q / 10 < 6) ? 40u + 4u * (uint32_t)(q / 10) : 12u; }
+__host__ __device__ inline int nb_shift(int q) { return 3 * (q % 10); }
+__device__ inline uint32_t nb_pack(const u64 (&L)[3], int j) {     // word j from the neighbours' level-1 words
+    uint32_t x = 0;
+    for (int qq = 0; qq < 10 && 10 * j + qq < 64; ++qq)
+        for (int y = 0; y < 3; ++y) x |= (uint32_t)((L[y] >> (10 * j + qq)) & 1ull) << (3 * qq + y);
+    return x;
+}
+
+// the neighbour words of every d = 3, p+c-1 = 2 record, from the records' own
+// rows and level-1 words (after steps that did not keep them: every kernel but
+// the speculative one)
+__global__ void __launch_bounds__(kBlock) k_rec_nb_fill(u64* __restrict__ rec, int64_t n, int64_t W) {
+    for (int64_t w = (int64_t)blockIdx.x * kBlock + threadIdx.x; w < n * W; w += (int64_t)gridDim.x * kBlock) {
+        const int64_t col = w / n;                       // (record order: column-major)
+        u64* dst = rec + w * 8;
+        const int4 r = *reinterpret_cast<const int4*>(dst);
+        const int32_t nbr[3] = {r.x, r.y, r.z};
+        u64 L[3];
+        for (int y = 0; y < 3; ++y) L[y] = rec[(col * n + nbr[y]) * 8 + 3];
+        uint32_t nb[7];
+        for (int j = 0; j < 7; ++j) nb[j] = nb_pack(L, j);
+        reinterpret_cast<int32_t*>(dst)[3] = (int32_t)nb[6];
+        dst[5] = (u64)nb[0] | ((u64)nb[1] << 32);
+        dst[6] = (u64)nb[2] | ((u64)nb[3] << 32);
+        dst[7] = (u64)nb[4] | ((u64)nb[5] << 32);
+    }
+}
 
 template <int D>
 __global__ void __launch_bounds__(64) k_sa_cone2(const int32_t* __restrict__ adj, const int4* __restrict__ adj_pad,
@@ -1478,7 +1518,7 @@ __device__ unsigned long long mjx_sa_prof[8];
 #else
 #define SA_STAMP(k) do {} while (0)
 #endif
-template <int D, int TT, int K>
+template <int D, int TT, int K, bool NB>
 __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj, const int4* __restrict__ adj_pad,
                                                 int64_t n, int64_t R, int64_t W, LcLevels L, mjx_sa_state st,
                                                 int64_t nsteps, double par_a, double par_b, double a_cap,
@@ -1489,6 +1529,9 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
     static_assert((D == 3 && (TT == 1 || TT == 2)) || (D == 4 && TT == 1), "speculative batches: d=3 T<=2, d=4 T=1");
     extern __shared__ uint32_t lc_lists[];
     static_assert(K == 8 || K == 16, "8 or 16 proposals per batch");
+    // NB: records with neighbour words (nb_byte): the children's level-1
+    // neighbours come with their records, and level-1 flips keep them
+    static_assert(!NB || (D == 3 && TT == 2), "neighbour words: d = 3, p+c-1 = 2 records");
     constexpr int T = TT;
     constexpr int SPW = 32 / K;                              // filter slots per 32-bit word
     constexpr int FTW = SPEC_FS / SPW;                       // words per filter table
@@ -1535,6 +1578,12 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
         o[2] = (TT == 2) ? crd.word(q + 2) : 0ull;
     };
     auto bv = [&](u64 x) -> uint32_t { return (x & bit) ? 1u : 0u; };
+    const uint32_t nbo = nb_byte(rl & 63);                   // this replica's neighbour word and bits
+    const int nbs = nb_shift(rl & 63);
+    // XOR bits (neighbour slots) into v's neighbour word (records only)
+    auto nbx = [&](int32_t v, uint32_t slots) {
+        atomicXor((uint32_t*)(cone - lo + colo + (int64_t)v * NS) + nbo / 4, slots << nbs);
+    };
     auto maj = [&](int ones, uint32_t own) -> uint32_t { return (2 * ones > D) ? 1u : ((2 * ones < D) ? 0u : own); };
     // the two slots of v: its low 11 bits, and bits 11..21 (xor the next 11)
     auto fslot1 = [](int32_t v) { return (uint32_t)v & (uint32_t)(SPEC_FS - 1); };
@@ -1667,6 +1716,7 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
         bool listpath = false;
         int cnt[LC_MAXT + 1] = {0, 0, 0, 0, 0, 0, 0};
         u64 wi[3], wa[D][3], wc[D][D][3], wg[D][D][D];
+        uint32_t wn[D][D];                       // NB: the children's neighbour words
         const bool tree = mine && ok;
         if (tree) {
             // rows of the children (T = 2) and the level sectors of i, the a_m and
@@ -1685,7 +1735,11 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
 #pragma unroll
                 for (int x = 0; x < D; ++x) {
                     wc[m][x][0] = wc[m][x][1] = wc[m][x][2] = 0ull;
-                    if (A1[m][x] != i) sector(A1[m][x], wc[m][x]);
+                    wn[m][x] = 0u;
+                    if (A1[m][x] != i) {
+                        sector(A1[m][x], wc[m][x]);
+                        if constexpr (NB) wn[m][x] = crd.u32((uint32_t)A1[m][x] * (uint32_t)NS, nbo);
+                    }
                 }
             }
         }
@@ -1723,7 +1777,9 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
                 ds = acc;
             } else {
             // the level-1 words of the children's other neighbours, only for the
-            // branches level 2 re-evaluates (one more round trip)
+            // branches level 2 re-evaluates (one more round trip; with NB they
+            // came with the children's records)
+            if constexpr (!NB) {
 #pragma unroll
             for (int m = 0; m < D; ++m)
 #pragma unroll
@@ -1732,6 +1788,7 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
                     for (int y = 0; y < D; ++y)
                         wg[m][x][y] = (((ch1 >> (1 + m)) & 1u) && A1[m][x] != i && C[m][x][y] != A0[m])
                                           ? w(C[m][x][y], 1) : 0ull;
+            }
             const bool c0 = ch1 & 1u;
             const uint32_t vi1 = c0 ? (nv1 & 1u) : bv(wi[1]);
             int64_t acc = 0;
@@ -1759,7 +1816,12 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
                         if (A1[m][x] == i) continue;
                         int ones = 0;
 #pragma unroll
-                        for (int y = 0; y < D; ++y) ones += (int)((C[m][x][y] == A0[m]) ? va1 : bv(wg[m][x][y]));
+                        for (int y = 0; y < D; ++y) {
+                            uint32_t gv;
+                            if constexpr (NB) gv = (wn[m][x] >> (nbs + y)) & 1u;
+                            else gv = bv(wg[m][x][y]);
+                            ones += (int)((C[m][x][y] == A0[m]) ? va1 : gv);
+                        }
                         const uint32_t nb = maj(ones, bv(wc[m][x][1]));
                         if (nb != bv(wc[m][x][2])) { ch2 |= 1u << (1 + D + m * D + x); acc += nb ? 2 : -2; }
                     }
@@ -1887,6 +1949,28 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
 #pragma unroll
                     for (int lv = 1; lv <= T; ++lv)
                         for (int q = 0; q < cnt[lv]; ++q) flip((int32_t)(lists[(L.off[lv] + q) * 64] & 0x7fffffffu), lv);
+                    if constexpr (NB) {
+                        // a level-1 change of v: its bit in each neighbour's record, at
+                        // the slots where that neighbour's row holds v (rows re-read)
+                        for (int q = 0; q < cnt[1]; ++q) {
+                            const int32_t v = (int32_t)(lists[(L.off[1] + q) * 64] & 0x7fffffffu);
+                            int32_t rv[D];
+                            row(v, rv);
+#pragma unroll
+                            for (int e = 0; e < D; ++e) {
+                                bool seen = false;               // (a multi-edge: that neighbour once)
+#pragma unroll
+                                for (int e2 = 0; e2 < e; ++e2) seen |= rv[e2] == rv[e];
+                                if (seen) continue;
+                                int32_t ru[D];
+                                row(rv[e], ru);
+                                uint32_t sl = 0;
+#pragma unroll
+                                for (int y = 0; y < D; ++y) sl |= (ru[y] == v) ? (1u << y) : 0u;
+                                nbx(rv[e], sl);
+                            }
+                        }
+                    }
                 } else {
                     if (ch1 & 1u) flip(i, 1);
                     if (ch2 & 1u) flip(i, 2);
@@ -1897,6 +1981,36 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
 #pragma unroll
                         for (int x = 0; x < D; ++x)
                             if ((ch2 >> (1 + D + m * D + x)) & 1u) flip(A1[m][x], 2);
+                    }
+                    if constexpr (NB) {
+                        // level-1 changes into the neighbours' records: i's (tree: a_m
+                        // is slot m of i's row) and the a_m's (i at its slots of a_m's
+                        // row; a_m at its slots of each child's row)
+                        if (ch1 & 1u) {
+#pragma unroll
+                            for (int m = 0; m < D; ++m) {
+                                uint32_t sl = 0;
+#pragma unroll
+                                for (int x = 0; x < D; ++x) sl |= (A1[m][x] == i) ? (1u << x) : 0u;
+                                nbx(A0[m], sl);
+                            }
+                        }
+                        uint32_t si = 0;
+#pragma unroll
+                        for (int m = 0; m < D; ++m) si |= ((ch1 >> (1 + m)) & 1u) << m;
+                        if (si) nbx(i, si);
+#pragma unroll
+                        for (int m = 0; m < D; ++m) {
+                            if (!((ch1 >> (1 + m)) & 1u)) continue;
+#pragma unroll
+                            for (int x = 0; x < D; ++x) {
+                                if (A1[m][x] == i) continue;
+                                uint32_t sl = 0;
+#pragma unroll
+                                for (int y = 0; y < D; ++y) sl |= (C[m][x][y] == A0[m]) ? (1u << y) : 0u;
+                                nbx(A1[m][x], sl);
+                            }
+                        }
                     }
                 }
             }
@@ -2250,6 +2364,16 @@ static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d
                       !(st.opt_flags & MJX_SA_NO_SPEC) && ((d == 3 && (T == 1 || T == 2)) || (d == 4 && T == 1));
     const int hoff = slots * 64;
     const size_t lds_spec = lds + SPEC_LDS;
+    // d = 3, p+c-1 = 2 records carry their neighbours' level-1 words (nb_byte),
+    // kept by the speculative kernel; another kernel's steps leave them stale
+    // (stp->rec_nb = 0), and they are rebuilt before the next speculative one
+    const bool nbw = L.lo == 2 && d == 3 && T == 2;
+    if (nbw && spec && !stp->rec_nb && nsteps > 0) {
+        k_rec_nb_fill<<<grid_for(n * W), kBlock, 0, hs>>>((u64*)L.s[0] - L.lo, n, W);
+        MJX_LAUNCH_CHECK("k_rec_nb_fill");
+        stp->rec_nb = 1;
+    }
+    if (nbw && !spec && nsteps > 0) stp->rec_nb = 0;
     auto launch_spec = [&](mjx_sa_state s2, int64_t k) -> int {
         auto go = [&](auto kern, int K) {      // K waves per word column (64 / K replicas per wave)
             MJX_HIP(set_max_lds(kern, (int)lds_spec), "spec lds");
@@ -2260,11 +2384,13 @@ static int lc_steps(const int32_t* adj, const int32_t* adj_pad, int64_t n, int d
             return MJX_OK;
         };
         if (spec_k == 16) {
-            if (d == 4) return go(k_sa_spec<4, 1, 16>, 16);
-            return (T == 2) ? go(k_sa_spec<3, 2, 16>, 16) : go(k_sa_spec<3, 1, 16>, 16);
+            if (d == 4) return go(k_sa_spec<4, 1, 16, false>, 16);
+            if (T == 2) return nbw ? go(k_sa_spec<3, 2, 16, true>, 16) : go(k_sa_spec<3, 2, 16, false>, 16);
+            return go(k_sa_spec<3, 1, 16, false>, 16);
         }
-        if (d == 4) return go(k_sa_spec<4, 1, 8>, 8);
-        return (T == 2) ? go(k_sa_spec<3, 2, 8>, 8) : go(k_sa_spec<3, 1, 8>, 8);
+        if (d == 4) return go(k_sa_spec<4, 1, 8, false>, 8);
+        if (T == 2) return nbw ? go(k_sa_spec<3, 2, 8, true>, 8) : go(k_sa_spec<3, 2, 8, false>, 8);
+        return go(k_sa_spec<3, 1, 8, false>, 8);
     };
     auto step_chunk = [&](auto kern_tape, mjx_sa_state s2, int64_t k0, int64_t k) -> int {
         if (s2.tr_i) s2.tr_i += k0 * R;     // trace rows of this chunk
@@ -2425,14 +2551,27 @@ __global__ void __launch_bounds__(kBlock) k_cone_xfer(int64_t words, int T, int 
         const int64_t v = w / W;
         u64* dst = cone + ((w % W) * n + v) * LV;
         if constexpr (PACK) {
+            const bool nbw = lo && d == 3 && T == 2 && LV == 8;      // the record carries neighbour words
+            uint32_t nb[7] = {0, 0, 0, 0, 0, 0, 0};
+            if (nbw) {
+                u64 L[3];
+                for (int y = 0; y < 3; ++y) L[y] = src.s[1][(int64_t)adj[v * 3 + y] * W + (w % W)];
+                for (int j = 0; j < 7; ++j) nb[j] = nb_pack(L, j);
+            }
             if (lo) {                 // record layout: the node's row (int32 x4, zero padded) first
                 int32_t r[4] = {0, 0, 0, 0};
                 for (int e = 0; e < d; ++e) r[e] = adj[v * d + e];
+                if (nbw) r[3] = (int32_t)nb[6];
                 *reinterpret_cast<int4*>(dst) = make_int4(r[0], r[1], r[2], r[3]);
             }
             for (int t = 0; t + lo < LV; t += 2) {
-                const u64 a = (t <= T) ? src.s[t][w] : 0ull;
-                const u64 b = (t + 1 <= T) ? src.s[t + 1][w] : 0ull;
+                u64 a = (t <= T) ? src.s[t][w] : 0ull;
+                u64 b = (t + 1 <= T) ? src.s[t + 1][w] : 0ull;
+                if (nbw && t == 2) b = (u64)nb[0] | ((u64)nb[1] << 32);           // words 5, 6, 7
+                if (nbw && t == 4) {
+                    a = (u64)nb[2] | ((u64)nb[3] << 32);
+                    b = (u64)nb[4] | ((u64)nb[5] << 32);
+                }
                 *reinterpret_cast<ulonglong2*>(dst + lo + t) = make_ulonglong2(a, b);
             }
         } else {
@@ -2489,6 +2628,8 @@ static int rec_lv(int d, int T) {
 }
 
 extern "C" int mjx_sa_rec_words(int d, int p, int c) { return rec_lv(d, p + c - 1); }
+
+extern "C" int mjx_sa_state_bytes(void) { return (int)sizeof(mjx_sa_state); }
 
 extern "C" int mjx_sa_rec_pack(const int32_t* adj, int64_t n, int d, int p, int c, int64_t R, const uint64_t* s,
                                uint64_t* const* levels, uint64_t* rec, void* stream) {

@@ -39,6 +39,9 @@ def test_sa_state_struct_matches_header(mjx_mod):
     body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
     fields = re.findall(r"([A-Za-z_][A-Za-z_0-9]*)\s*;", body)
     assert fields == [f for f, _ in mjx_mod._lib.MjxSaState._fields_]
+    # and the same size as the library was built with (no compute call)
+    lib = mjx_mod._lib.load()
+    assert lib.mjx_sa_state_bytes() == ctypes.sizeof(mjx_mod._lib.MjxSaState)
 
 
 def test_invalid_arguments_return_status_without_gpu(mjx_mod):

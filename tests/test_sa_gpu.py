@@ -151,6 +151,55 @@ def test_sa_cone_layout_equals_separate_levels(mjx_mod, d, p, c, kernel, layout)
         assert torch.equal(getattr(a, f), getattr(b, f)), f
 
 
+def _rec_neighbour_words_ok(rec, n, W):
+    """The record layout's neighbour words (d = 3, p+c-1 = 2; include/mjx.h
+    mjx_sa_rec_words): replica q's level-1 bit of row neighbour y at bit
+    3*(q % 10) + y of 32-bit word q // 10 (words 0..5 in bytes 40..63, word 6
+    in the row's pad int), recomputed here from the records' rows and levels."""
+    r = rec.cpu().numpy().view(np.uint64).reshape(W, n, 8)
+    rows = r[:, :, :2].copy().view(np.int32).reshape(W, n, 4)[:, :, :3].astype(np.int64)
+    lev1 = r[:, :, 3]
+    u32 = r[:, :, 5:8].copy().view(np.uint32).reshape(W, n, 6)
+    pad = r[:, :, :2].copy().view(np.uint32).reshape(W, n, 4)[:, :, 3]
+    got = np.concatenate([u32, pad[:, :, None]], axis=2)
+    want = np.zeros_like(got)
+    for w in range(W):
+        L = lev1[w][rows[w]]                                  # (n, 3) neighbours' level-1 words
+        for q in range(64):
+            bits = ((L >> np.uint64(q)) & np.uint64(1)).astype(np.uint32)
+            for y in range(3):
+                want[w, :, q // 10] |= bits[:, y] << np.uint32(3 * (q % 10) + y)
+    return np.array_equal(got, want)
+
+
+def test_sa_rec_neighbour_words_across_kernels(mjx_mod):
+    """d = 3, p+c-1 = 2 records carry their neighbours' level-1 bits for the
+    speculative batches (round 6: no separate round trip for the children's
+    other neighbours).  Calls alternate between the speculative kernel (keeps
+    the words) and the general light-cone kernel (leaves them stale; the next
+    speculative call rebuilds them): every call equals separate level arrays,
+    and after speculative calls the words equal a recomputation from the
+    records' rows and level-1 words."""
+    n, d, p, c, R = 3000, 3, 2, 1, 150
+    adj = mjx_mod.random_regular_graph(d, n, seed=11)
+    a = mjx_mod.SAReplicas(adj, p, c, list(range(R)), mode="lightcone", layout="rec")
+    b = mjx_mod.SAReplicas(adj, p, c, list(range(R)), mode="lightcone", layout="levels")
+    assert _rec_neighbour_words_ok(a.cone, n, a.W)             # as packed
+    general = mjx_mod._lib.MJX_SA_NO_SPEC | mjx_mod._lib.MJX_SA_NO_CONE2
+    for k, flags in ((700, 0), (300, general), (900, 0), (5, general), (400, 0)):
+        a._state.opt_flags = flags
+        ta, tb = a.steps(k, trace=True), b.steps(k, trace=True)
+        for key in ("i", "accept", "sum_end", "dE"):
+            assert torch.equal(ta[key], tb[key]), (k, flags, key)
+        assert a._state.rec_nb == (0 if flags else 1)
+        if not flags:
+            torch.cuda.synchronize()
+            assert _rec_neighbour_words_ok(a.cone, n, a.W), k
+    assert torch.equal(a.s, b.s)
+    for la, lb in zip(a.levels, b.levels):
+        assert torch.equal(la, lb)
+
+
 def test_sa_run_matches_full_reference_script(mjx_mod):
     full = load_golden("sa_fullscript.npz")
     N = full["n200_d4_p3_graphs"][0]
