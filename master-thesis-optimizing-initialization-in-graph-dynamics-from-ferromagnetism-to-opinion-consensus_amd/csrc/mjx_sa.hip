@@ -1585,13 +1585,18 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
         atomicXor((uint32_t*)(cone - lo + colo + (int64_t)v * NS) + nbo / 4, slots << nbs);
     };
     auto maj = [&](int ones, uint32_t own) -> uint32_t { return (2 * ones > D) ? 1u : ((2 * ones < D) ? 0u : own); };
-    // the two slots of v: its low 11 bits, and bits 11..21 (xor the next 11)
+    // the two slots of v: its low 11 bits, and bits 11..21 (node ids of a
+    // random graph are random; ids past 2^22 only alias, never miss)
     auto fslot1 = [](int32_t v) { return (uint32_t)v & (uint32_t)(SPEC_FS - 1); };
-    auto fslot2 = [](int32_t v) { return (((uint32_t)v >> 11) ^ ((uint32_t)v >> 22)) & (uint32_t)(SPEC_FS - 1); };
+    auto fslot2 = [](int32_t v) { return ((uint32_t)v >> 11) & (uint32_t)(SPEC_FS - 1); };
     const uint32_t kbit = 1u << k;
     const uint32_t below = kbit - 1u;                        // the earlier proposals' bits
     auto fword = [&](int tbl, uint32_t h) -> uint32_t* { return ftab + tbl * FTW + h / SPW; };
     auto fshift = [](uint32_t h) -> uint32_t { return (h % SPW) * K; };
+    // lookups read the K-bit slots themselves (ds_read_u8 / _u16: no shifts)
+    using FS = typename std::conditional<(K == 8), uint8_t, uint16_t>::type;
+    const FS* fs1 = reinterpret_cast<const FS*>(ftab);
+    const FS* fs2 = fs1 + SPEC_FS;
     auto fins = [&](int32_t v) {                             // proposal k may write v
         const uint32_t h1 = fslot1(v), h2 = fslot2(v);
         atomicOr(fword(0, h1), kbit << fshift(h1));
@@ -1613,15 +1618,12 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
         uint32_t e1[N], e2[N];
 #pragma unroll
         for (int q = 0; q < N; ++q) {
-            e1[q] = *fword(0, fslot1(vv[q]));
-            e2[q] = *fword(1, fslot2(vv[q]));
+            e1[q] = fs1[fslot1(vv[q])];
+            e2[q] = fs2[fslot2(vv[q])];
         }
         uint32_t hit = 0;
 #pragma unroll
-        for (int q = 0; q < N; ++q) {
-            const uint32_t m = (e1[q] >> fshift(fslot1(vv[q]))) & (e2[q] >> fshift(fslot2(vv[q])));
-            hit |= mm[q] ? m : 0u;
-        }
+        for (int q = 0; q < N; ++q) hit |= mm[q] ? (e1[q] & e2[q]) : 0u;
         return (hit & below) != 0u;
     };
 #ifdef MJX_SA_PROF
