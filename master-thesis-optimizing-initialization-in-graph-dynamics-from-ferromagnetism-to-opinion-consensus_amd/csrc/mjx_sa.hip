@@ -1546,7 +1546,8 @@ __global__ void __launch_bounds__(64) k_sa_spec(const int32_t* __restrict__ adj,
     const int64_t r = col * 64 + rl;
     const bool live = r < R;
     const u64 bit = 1ull << (rl & 63);
-    const int64_t NS = L.ns, colo = col * L.cs;
+    // words per (node, column): the NB records are 8 (a shift, not a multiply)
+    const int64_t NS = NB ? 8 : L.ns, colo = col * L.cs;
     const u64* cone = L.s[0];
     uint32_t* lists = lc_lists + lane;
     uint32_t* ftab = lc_lists + hoff + g * 2 * FTW;           // this replica's two tables
