@@ -5,6 +5,7 @@ LDS-resident replicas (every LDS kernel) vs the HBM cone layout.
     python tools/sa_probe3.py [--no-cone] [--R 64] [--n 10000]
 """
 import argparse
+import os
 import sys
 import time
 
@@ -30,6 +31,9 @@ VARIANTS = {
     "lds-single": ("lds", {"lds_single": True}),            # one wave, one proposal per step
     "cone": ("cone", None),
 }
+ap2 = os.environ.get("SA_VARIANTS")                      # e.g. "lds,lds-wg8": only these
+if ap2:
+    VARIANTS = {k: v for k, v in VARIANTS.items() if k in ap2.split(",")}
 for pc in args.pc.split(";"):
     p, c = (int(x) for x in pc.split(","))
     for name, (layout, kern) in VARIANTS.items():
