@@ -9,7 +9,11 @@ Arguments of --build: the tag, then -D/-f flags, *.patch files (unified diffs
 against csrc/, applied to a copy: timing builds with wrong results, e.g.
 tools/variants/spec_nohash.patch, live only there) and the units to rebuild.
 The variant's build id is not a source hash, so it is opened unverified here
-and refused by the product loader."""
+and refused by the product loader.  --build first brings the product build up
+to date with the working tree (the variant links its other units' objects):
+an experiment edited into csrc/ and reverted afterwards needs
+__graft_entry__.build() again, or the in-tree libmjx.so no longer matches the
+sources and the product loader refuses it."""
 import os
 import runpy
 import sys
