@@ -133,6 +133,7 @@ class MjxSaState(ctypes.Structure):
 
 MJX_SA_NO_SPEC, MJX_SA_NO_CONE2, MJX_SA_LDS_SERIAL, MJX_SA_LDS_SINGLE, MJX_SA_LDS_PAIR = 1, 2, 4, 8, 16  # opt_flags (include/mjx.h)
 MJX_SA_LDS_WAVE = 32
+MJX_SA_LDS_CU = 64
 
 
 class MjxError(RuntimeError):

@@ -2368,6 +2368,519 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_wg(const int32_t* __restrict
 }
 
 // ---------------------------------------------------------------------------
+// The whole CU, level-synchronous (k_sa_lds_cu<D, T>, round 6; kernel option
+// lds_cu).  k_sa_lds_wg gives each of its 15 proposals a wave and walks that
+// wave through levels 1..T, so every level costs 15 waves' instruction
+// streams for a handful of live lanes each (at SA_RRG.py's p = 3: ~5 of 64 at
+// level 1) -- the round was VALU-issue bound at four waves a SIMD.  Here the
+// round's proposals are evaluated together, one level at a time: the
+// (proposal, candidate) items of a level are packed densely over the CU's
+// lanes (level 1: proposal q's i_q and its d neighbours; level l: every member
+// of C_{l-1} of every proposal and its d neighbours), so a level costs as many
+// waves as it has items / 64.  Members go to one CU-wide list per level (node,
+// proposal, cached value), appended with one LDS atomic per wave; a barrier
+// separates the levels, so a level-l item reads the complete level-(l-1)
+// marks and its conflict word (what it read that an earlier proposal changed)
+// is final when it is read -- no second pass after the levels.  The marks, the
+// change rule, the taken prefix and the accept test are k_sa_lds_wg's; the
+// level-0 conflicts (closed neighbourhoods of i_q and i_j meet) are items of
+// the level-1 pass, one per pair j < q.  Wave 15 parses the stream into the
+// ring exactly as k_sa_lds_wg's parse wave.  Same draws, accepts and state.
+struct GeoC {
+    int nw;         // uint32 bit words per level
+    int cap[4];     // list capacity of levels 1..T (index l)
+    int off_lev;
+    int off_mk;     // T * nw * 32 16-bit marks (bit q = proposal q, bit 15 = the level value)
+    int off_lev0;
+    int off_mt;
+    int off_list;   // levels 1..T, cap[l] uint32 each: node | q << 16 | cached value << 20
+    int off_q;      // ring: i[64], end[64], u[64]
+    int off_res;    // per proposal: conflict word, packed word, a, b, dE, ds, cf; counters
+    int bytes;
+};
+
+static bool geometry_cu(int64_t n, int d, int T, GeoC* g) {
+    if (n < 2 || n > 65535 || d < 3 || d > 4 || T < 2 || T > 3) return false;
+    g->nw = (int)(((n + 63) / 64) * 2);
+    // level 1: 15 proposals x (d + 1); inner levels keep repeats: (d + 1) x the
+    // level before; the last level is distinct per proposal: 15 x the ball
+    g->cap[0] = 0;
+    g->cap[1] = 15 * (d + 1);
+    g->cap[2] = (T == 2) ? (int)std::min<int64_t>((int64_t)(d + 1) * g->cap[1], 15 * ball(d, 2))
+                         : (d + 1) * g->cap[1];
+    g->cap[3] = (T == 3) ? (int)std::min<int64_t>((int64_t)(d + 1) * g->cap[2], 15 * ball(d, 3)) : 0;
+    int64_t off = ((int64_t)n * 4 * 2 + 15) / 16 * 16;
+    g->off_lev = (int)off;   off += (int64_t)g->nw * 4;
+    g->off_mk = (int)off;    off += (int64_t)T * g->nw * 32 * 2;
+    g->off_lev0 = (int)off;  off += (int64_t)g->nw * 4;
+    g->off_mt = (int)off;    off += MT_N * 4;
+    g->off_list = (int)off;  off += (int64_t)(g->cap[1] + g->cap[2] + g->cap[3]) * 4;
+    off = (off + 15) / 16 * 16;
+    g->off_q = (int)off;     off += 64 * 4 + 64 * 4 + 64 * 8;
+    g->off_res = (int)off;   off += 16 * (4 + 4 + 8 + 8 + 8 + 4 + 4) + 2 * 4 * 4 + 4 * 4;
+    g->bytes = (int)off;
+    return (size_t)off <= kLdsMax;
+}
+
+template <int D, int T, bool TRACE>
+__global__ void __launch_bounds__(1024) k_sa_lds_cu(const int32_t* __restrict__ adj, int64_t n, int64_t R,
+                                                   int64_t W, u64* __restrict__ s, mjx_sa_state st, int64_t nsteps,
+                                                   double par_a, double par_b, double a_cap, double b_cap,
+                                                   int64_t t_cap, GeoC geo) {
+    static_assert((D == 3 || D == 4) && (T == 2 || T == 3), "level-synchronous LDS SA: d = 3, 4; p+c-1 = 2, 3");
+    using MK = uint16_t;
+    constexpr int NW = 16, NE = 15, NT = 64 * NW, LVB = 15, DP1 = D + 1;
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int tid = threadIdx.x;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lane = tid & 63;
+    const u64 ltmask = (1ull << lane) - 1ull;
+    const int64_t r = blockIdx.x;
+    const int nw = geo.nw;
+    const int mkl = nw * 32;
+    uint16_t* rows = reinterpret_cast<uint16_t*>(smem);
+    uint32_t* lev = reinterpret_cast<uint32_t*>(smem + geo.off_lev);
+    MK* mk = reinterpret_cast<MK*>(smem + geo.off_mk);
+    uint32_t* lev0s = reinterpret_cast<uint32_t*>(smem + geo.off_lev0);
+    uint32_t* mt = reinterpret_cast<uint32_t*>(smem + geo.off_mt);
+    uint32_t* gl[T + 1];                               // the CU-wide change lists of levels 1..T
+    gl[0] = nullptr;
+    gl[1] = reinterpret_cast<uint32_t*>(smem + geo.off_list);
+#pragma unroll
+    for (int l = 2; l <= T; ++l) gl[l] = gl[l - 1] + geo.cap[l - 1];
+    int* q_i = reinterpret_cast<int*>(smem + geo.off_q);
+    int* q_end = q_i + 64;
+    double* q_u = reinterpret_cast<double*>(q_end + 64);
+    uint32_t* res_cf = reinterpret_cast<uint32_t*>(smem + geo.off_res);   // per proposal: conflict bits
+    uint32_t* res = res_cf + 16;                                            // packed result
+    double* res_a = reinterpret_cast<double*>(res + 16);
+    double* res_b = res_a + 16;
+    double* res_dE = res_b + 16;
+    int* dsv = reinterpret_cast<int*>(res_dE + 16);                         // sum(s_end) change per proposal
+    uint32_t* cfv = reinterpret_cast<uint32_t*>(dsv + 16);                  // conflict bits, being ORed
+    uint32_t* cnt = cfv + 16;                                               // [2][4] list lengths by round parity
+    int* ctl = reinterpret_cast<int*>(cnt + 8);
+
+    auto bit_of = [&](int v) -> uint32_t { return (lev[v >> 5] >> (v & 31)) & 1u; };
+    auto lvl = [&](int t, int v) -> uint32_t { return ((uint32_t)mk[(t - 1) * mkl + v] >> LVB) & 1u; };
+    auto mark_word = [&](int t, int v) -> uint32_t* { return reinterpret_cast<uint32_t*>(mk + (t - 1) * mkl + (v & ~1)); };
+    auto nbrs = [&](int v, int (&o)[D]) {
+        const uint2 x = *reinterpret_cast<const uint2*>(rows + v * 4);
+        o[0] = (int)(x.x & 0xffffu);
+        o[1] = (int)(x.x >> 16);
+        o[2] = (int)(x.y & 0xffffu);
+        if constexpr (D > 3) o[3] = (int)(x.y >> 16);
+    };
+    auto maj = [&](int ones, uint32_t own) -> uint32_t {       // always-stay majority (code/SA_RRG.py:19-20)
+        return (2 * ones > D) ? 1u : ((2 * ones < D) ? 0u : own);
+    };
+    // the wave's items appended to a list: one LDS atomic per wave
+    auto append = [&](uint32_t* list, uint32_t* counter, bool add, uint32_t entry) {
+        const u64 m = __ballot(add);
+        if (!m) return;
+        uint32_t base = 0;
+        if (lane == (int)(__ffsll((unsigned long long)m) - 1)) base = atomicAdd(counter, (uint32_t)__popcll(m));
+        base = (uint32_t)__builtin_amdgcn_readlane((int)base, __ffsll((unsigned long long)m) - 1);
+        if (add) list[base + (uint32_t)__popcll(m & ltmask)] = entry;
+    };
+
+    // ---- launch setup (k_sa_lds_wg's): rows, level 0, marks cleared, MT state; levels 1..T
+    {
+        const int32_t* g = adj + (st.rep_graph ? (int64_t)st.rep_graph[r] : 0) * n * D;
+        for (int64_t q = tid; q < n * D; q += NT) {
+            const int64_t v = q / D;
+            rows[v * 4 + (q - v * D)] = (uint16_t)g[q];
+        }
+        for (int q = tid; q < nw; q += NT) lev[q] = 0u;
+        for (int q = tid; q < T * nw * 16; q += NT) reinterpret_cast<uint32_t*>(mk)[q] = 0u;
+        for (int q = tid; q < MT_N; q += NT) mt[q] = st.mt[r * MT_N + q];
+        if (tid < 16) {
+            dsv[tid] = 0;
+            cfv[tid] = 0u;
+        }
+        if (tid < 8) cnt[tid] = 0u;
+        const int64_t col = r >> 6;
+        const u64 rbit = 1ull << (r & 63);
+        __syncthreads();
+        for (int64_t v0 = (int64_t)w * 64; v0 < (int64_t)nw * 32; v0 += NT) {
+            const int64_t v = v0 + lane;
+            const bool b = v < n && (s[v * W + col] & rbit);
+            const u64 m = __ballot(b);
+            if (lane < 2) {
+                const uint32_t x = (uint32_t)(m >> (32 * lane));
+                lev[(v0 >> 5) + lane] = x;
+                lev0s[(v0 >> 5) + lane] = x;
+            }
+        }
+        __syncthreads();
+        for (int t = 1; t <= T; ++t) {
+            for (int v = tid; v < n; v += NT) {
+                int nv[D];
+                nbrs(v, nv);
+                int ones = 0;
+#pragma unroll
+                for (int q = 0; q < D; ++q) ones += (int)(t == 1 ? bit_of(nv[q]) : lvl(t - 1, nv[q]));
+                const uint32_t nb = maj(ones, t == 1 ? bit_of(v) : lvl(t - 1, v));
+                mk[(t - 1) * mkl + v] = (MK)(nb << LVB);
+            }
+            __syncthreads();
+        }
+    }
+
+    double a = st.a[r], b = st.b[r];
+    int64_t t = st.t[r], sum_end = st.sum_end[r];
+    int done = st.done[r];
+    int idx = st.mt_idx[r];
+    int ties = 0;
+    const uint32_t rng = (uint32_t)(n - 1);
+    uint32_t mask = rng;
+    mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+    double inv_n = 1.0 / (double)n;
+    asm volatile("" : "+v"(a), "+v"(b), "+v"(par_a), "+v"(par_b), "+v"(a_cap), "+v"(b_cap), "+v"(inv_n));
+
+    // ---- the proposal ring, parsed by wave NE (k_sa_lds_wg's, unchanged)
+    uint32_t npend = 0, pk = 0;
+    int gen = 0;
+    const int idx0 = idx;
+    auto twist = [&]() {
+        for (int q = lane; q < MT_N; q += 64) st.mt[r * MT_N + q] = mt[q];
+        lds_twist(mt, lane);
+        idx = 0;
+        gen ^= 1;
+    };
+    auto twist_ok = [&]() -> bool {
+        const int lg = (pk > 0u) ? ((q_end[(pk - 1u) & 63u] >> 10) & 1) : 0;
+        return lg == gen || npend == pk;
+    };
+    auto parse_window = [&](uint32_t room) -> bool {
+        if (idx >= MT_N) {
+            if (!twist_ok()) return false;
+            twist();
+        }
+        const int lim = (MT_N - idx < 64) ? MT_N - idx : 64;
+        uint32_t tw = 0, y = 0;
+        bool ok = false;
+        if (lane < lim) {
+            tw = mt_temper(mt[idx + lane]);
+            y = tw & mask;
+            ok = y <= rng;
+        }
+        const u64 okm = __ballot(ok);
+        u64 stm = mt_window_starts(ok) & ((lim >= 2) ? ((1ull << (lim - 2)) - 1ull) : 0ull);
+        while ((uint32_t)__popcll(stm) > room) stm &= ~(1ull << (63 - __clzll(stm)));
+        const uint32_t got = (uint32_t)__popcll(stm);
+        const int pos = got ? 66 - __clzll(stm) : 0;
+        if (got > 0) {
+            const uint32_t x1 = mt_next_lane(tw);
+            const uint32_t x2 = mt_next_lane(x1);
+            if ((stm >> lane) & 1ull) {
+                const int q = (int)((npend + (uint32_t)__popcll(stm & ltmask)) & 63u);
+                q_i[q] = (int)y;
+                q_u[q] = mt_double(x1, x2);
+                q_end[q] = (idx + lane + 3) | (gen << 10);
+            }
+            npend += got;
+            idx += pos;
+            return true;
+        }
+        if (room == 0) return true;
+        if (!okm) { idx += lim; return true; }
+        const int f = __ffsll((unsigned long long)okm) - 1;
+        if (f > 0) { idx += f; return true; }
+        if (idx + 2 >= MT_N && !twist_ok()) return false;
+        const int iv = __builtin_amdgcn_readlane((int)y, 0);
+        idx += 1;
+        if (idx >= MT_N) twist();
+        const uint32_t w1 = mt_temper(mt[idx]);
+        idx += 1;
+        if (idx >= MT_N) twist();
+        const uint32_t w2 = mt_temper(mt[idx]);
+        idx += 1;
+        if (lane == 0) {
+            const int q = (int)(npend & 63u);
+            q_i[q] = iv;
+            q_u[q] = mt_double(w1, w2);
+            q_end[q] = idx | (gen << 10);
+        }
+        npend += 1;
+        return true;
+    };
+    auto room = [&]() -> uint32_t { return 63u - (npend - pk); };
+
+    int64_t k = 0;
+    int par = 0;                                       // round parity: the list-length set in use
+    while (k < nsteps && done == 0) {
+        if (w == NE) {
+            while (npend - pk < (uint32_t)NE)
+                if (!parse_window(room())) break;
+            if (lane == 0) ctl[0] = (int)npend;
+        }
+        __syncthreads();                                   // the round's proposals are published
+        const uint32_t npd = (uint32_t)__builtin_amdgcn_readfirstlane(ctl[0]);
+        int nq = (int)(npd - pk);
+        if (nq > NE) nq = NE;
+        if ((int64_t)nq > nsteps - k) nq = (int)(nsteps - k);
+        uint32_t* cn = cnt + 4 * par;                      // this round's list lengths (zeroed)
+        // ---- level 1 (items q*(d+1) + j), and the level-0 conflicts (items: pairs j < q)
+        if (w < NE) {
+            const int n1 = nq * DP1, np = nq * (nq - 1) / 2;
+            for (int base = 64 * w; base < n1 + np; base += 64 * NE) {
+                const int it = base + lane;
+                bool add = false;
+                uint32_t entry = 0;
+                if (it < n1) {
+                    const int q = it / DP1, j = it - q * DP1;
+                    const int iv = q_i[(pk + (uint32_t)q) & 63u];
+                    int ri[D];
+                    nbrs(iv, ri);
+                    const int cand = (j == 0) ? iv : ri[j > 0 ? j - 1 : 0];
+                    int first = D;
+#pragma unroll
+                    for (int e = D - 1; e >= 0; --e)
+                        if (ri[e] == cand) first = e;
+                    const bool dup = j > 0 && (cand == iv || first + 1 < j);
+                    int nv[D];
+                    nbrs(cand, nv);
+                    int ones = 0;
+#pragma unroll
+                    for (int e = 0; e < D; ++e) ones += (int)(bit_of(nv[e]) ^ (nv[e] == iv));
+                    const uint32_t own = bit_of(cand) ^ (cand == iv);
+                    const uint32_t nb = maj(ones, own);
+                    const uint32_t cur = lvl(1, cand);
+                    add = !dup && nb != cur;
+                    if (add) atomicOr(mark_word(1, cand), (1u << q) << (16 * (cand & 1)));
+                    entry = (uint32_t)cand | ((uint32_t)q << 16) | (cur << 20);
+                } else if (it < n1 + np) {
+                    // pair (q, j < q): the closed neighbourhoods of i_q and i_j meet
+                    const int k2 = it - n1;
+                    int q = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)k2)) * 0.5f);
+                    if (q * (q - 1) / 2 > k2) --q;
+                    if ((q + 1) * q / 2 <= k2) ++q;
+                    const int j = k2 - q * (q - 1) / 2;
+                    const int iq = q_i[(pk + (uint32_t)q) & 63u], ij = q_i[(pk + (uint32_t)j) & 63u];
+                    int rq[D], rj[D];
+                    nbrs(iq, rq);
+                    nbrs(ij, rj);
+                    bool meet = iq == ij;
+#pragma unroll
+                    for (int e = 0; e < D; ++e) meet |= (rj[e] == iq) | (ij == rq[e]);
+#pragma unroll
+                    for (int e = 0; e < D; ++e)
+#pragma unroll
+                        for (int f = 0; f < D; ++f) meet |= rj[e] == rq[f];
+                    if (meet) atomicOr(&cfv[q], 1u << j);
+                }
+                append(gl[1], &cn[1], add, entry);
+            }
+        } else {
+            for (int it = 0; it < 2 && room() >= 8u; ++it)
+                if (!parse_window(room())) break;
+        }
+        __syncthreads();                                   // level-1 marks and C_1 lists complete
+        // ---- levels 2..T: every member of C_{l-1} of every proposal and its d neighbours
+#pragma unroll
+        for (int l = 2; l <= T; ++l) {
+            if (w < NE) {
+                const int nm = (int)cn[l - 1];
+                for (int base = 64 * w; base < nm * DP1; base += 64 * NE) {
+                    const int it = base + lane;
+                    bool add = false;
+                    uint32_t entry = 0;
+                    if (it < nm * DP1) {
+                        const int mi = it / DP1, j = it - mi * DP1;
+                        const uint32_t me = gl[l - 1][mi];
+                        const int mc = (int)(me & 0xffffu), q = (int)((me >> 16) & 15u);
+                        const int c2 = (j == 0) ? mc : (int)rows[mc * 4 + (j > 0 ? j - 1 : 0)];
+                        const uint32_t early = (1u << q) - 1u;
+                        int nv2[D];
+                        nbrs(c2, nv2);
+                        int ones = 0;
+                        uint32_t cfm = 0;
+                        // node v at level l-1 as proposal q sees it; the earlier proposals' marks into cfm
+                        auto look = [&](int v) -> uint32_t {
+                            const uint32_t mb = mk[(l - 2) * mkl + v];
+                            cfm |= mb & early;
+                            return ((mb >> LVB) ^ (mb >> q)) & 1u;
+                        };
+#pragma unroll
+                        for (int e = 0; e < D; ++e) ones += (int)look(nv2[e]);
+                        const uint32_t own = look(c2);
+                        if (cfm) atomicOr(&cfv[q], cfm);
+                        const uint32_t nb = maj(ones, own);
+                        const uint32_t cur = lvl(l, c2);
+                        const bool chg = nb != cur;
+                        const uint32_t mb = (1u << q) << (16 * (c2 & 1));
+                        add = chg;
+                        if (l == T) {
+                            // the last level counts distinct nodes: the first mark wins
+                            if (chg) add = (atomicOr(mark_word(l, c2), mb) & mb) == 0u;
+                            if (add) atomicAdd(&dsv[q], cur == 0u ? 2 : -2);
+                        } else if (chg) {
+                            atomicOr(mark_word(l, c2), mb);
+                        }
+                        entry = (uint32_t)c2 | ((uint32_t)q << 16) | (cur << 20);
+                    }
+                    append(gl[l], &cn[l], add, entry);
+                }
+            } else if (l == 2) {
+                for (int it = 0; it < 2 && room() >= 8u; ++it)
+                    if (!parse_window(room())) break;
+            }
+            __syncthreads();                               // level-l marks, C_l lists, conflict bits complete
+        }
+        // ---- delta_H and the Metropolis test of each proposal (lane q of wave 0)
+        // (code/SA_RRG.py:37,74-76); the schedule after q steps (:80-81)
+        if (w == 0) {
+            const bool lq = lane < nq;
+            const int q = lq ? lane : 0;
+            const int iv = q_i[(pk + (uint32_t)q) & 63u];
+            const double u = q_u[(pk + (uint32_t)q) & 63u];
+            const uint32_t old_i = bit_of(iv);
+            const int64_t ds = (int64_t)dsv[q];
+            double ah = a, bh = b;
+            if (!(ah >= a_cap && bh >= b_cap)) {
+                for (int qq = 0; qq < NE; ++qq) {
+                    if (qq < q) {
+                        if (ah < a_cap) ah = par_a * ah;
+                        if (bh < b_cap) bh = par_b * bh;
+                    }
+                }
+            }
+            const double anx = (ah < a_cap) ? par_a * ah : ah;
+            const double bnx = (bh < b_cap) ? par_b * bh : bh;
+            const double si = old_i ? 1.0 : -1.0;
+            const double t1 = (-2.0 * ah) * si;
+            const double t2 = bh * (double)(-ds);
+            const double num = t1 + t2;
+            bool acc;
+            bool tie = false;
+            double dE = 0.0;
+            const float xf = (float)(-num * inv_n);
+            const float ef = __expf(xf);
+            const float mg = ef * (1e-6f * (1.0f + fabsf(xf))) + 1e-37f;
+            if (fabs(u - (double)ef) > (double)mg) {
+                acc = u < (double)ef;
+                if (TRACE && st.tr_dE) dE = num / (double)n;
+            } else {
+                dE = num / (double)n;
+                const double e = exp(-dE);
+                const double prob = (e < 1.0) ? e : 1.0;
+                acc = u < prob;
+                tie = e < 1.0 && fabs(u - e) <= 4.0 * (nextafter(e, 2.0) - e);
+            }
+            if (lq) {
+                res_cf[q] = cfv[q];
+                res[q] = (acc ? 1u : 0u) | (tie ? 2u : 0u) | ((uint32_t)(ds & 0xffff) << 16);
+                res_a[q] = anx;
+                res_b[q] = bnx;
+                res_dE[q] = dE;
+            }
+            // the next round's accumulators and list lengths (nobody reads them any more this round)
+            if (lane < 16) {
+                dsv[lane] = 0;
+                cfv[lane] = 0u;
+            }
+            if (lane < 4) cnt[4 * (par ^ 1) + lane] = 0u;
+        }
+        __syncthreads();                                   // every proposal's result
+        // ---- resolve in proposal order (every wave alike, k_sa_lds_wg's rule)
+        const bool lq = lane < nq;
+        const uint32_t pq = lq ? res[lane] : 0u;
+        const uint32_t pcf = lq ? res_cf[lane] : 0u;
+        const bool aq = pq & 1u;
+        const uint32_t accm = (uint32_t)__ballot(lq && aq);
+        const u64 clm = __ballot(lq && (pcf & accm) != 0u);
+        int qstop = nq;
+        if (clm) {
+            const int qc = __ffsll((unsigned long long)clm) - 1;
+            if (qc < qstop) qstop = qc;
+        }
+        int pre = (lq && aq) ? (int)(int16_t)(pq >> 16) : 0;
+        pre += __builtin_amdgcn_update_dpp(0, pre, 0x111, 0xf, 0xf, false);     // row_shr:1
+        pre += __builtin_amdgcn_update_dpp(0, pre, 0x112, 0xf, 0xf, false);     // row_shr:2
+        pre += __builtin_amdgcn_update_dpp(0, pre, 0x114, 0xf, 0xf, false);     // row_shr:4
+        pre += __builtin_amdgcn_update_dpp(0, pre, 0x118, 0xf, 0xf, false);     // row_shr:8
+        const int64_t sum_after = sum_end + (int64_t)pre;
+        const int dnq = (t + lane + 1 > t_cap) ? 2 : ((sum_after == n) ? 1 : 0);
+        const u64 stq = __ballot(lane < qstop && dnq != 0);            // (code/SA_RRG.py:84), m == 1
+        int taken = qstop;
+        if (stq) {
+            const int qs = __ffsll((unsigned long long)stq) - 1;
+            if (qs + 1 < taken) taken = qs + 1;
+        }
+        ties += __popcll(__ballot(lane < taken && ((pq >> 1) & 1u)));
+        if constexpr (TRACE) {
+            if (w == 0 && lane < taken) {
+                const int64_t kk = k + lane;
+                const int iv = q_i[(pk + (uint32_t)lane) & 63u];
+                if (st.tr_i) st.tr_i[kk * R + r] = iv;
+                if (st.tr_acc) st.tr_acc[kk * R + r] = ((accm >> lane) & 1u) ? 1 : 0;
+                if (st.tr_sum) st.tr_sum[kk * R + r] = sum_after;
+                if (st.tr_dE) st.tr_dE[kk * R + r] = res_dE[lane];
+            }
+        }
+        sum_end = rl64(sum_after, taken - 1);
+        done = __builtin_amdgcn_readlane(dnq, taken - 1);
+        t += taken;                                                 // (code/SA_RRG.py:77,82)
+        a = res_a[taken - 1];                                       // (:80-81) after the taken steps
+        b = res_b[taken - 1];
+        // ---- the taken accepted proposals' changes (the level bit of the mark set,
+        // its proposal bits cleared); every other proposal clears its own bits
+        if (w == 0 && lane < taken && ((accm >> lane) & 1u)) {
+            const int iv = q_i[(pk + (uint32_t)lane) & 63u];
+            atomicXor(&lev[iv >> 5], 1u << (iv & 31));
+        }
+        if (w < NE) {
+            const int c1 = (int)cn[1];
+            const int c2 = c1 + (int)cn[2];
+            const int c3 = c2 + (T == 3 ? (int)cn[3] : 0);
+            for (int it = 64 * w + lane; it < c3; it += 64 * NE) {
+                const int l = (it < c1) ? 1 : ((it < c2) ? 2 : 3);
+                const uint32_t e = gl[l][it - ((l == 1) ? 0 : ((l == 2) ? c1 : c2))];
+                const int v = (int)(e & 0xffffu), q = (int)((e >> 16) & 15u);
+                const uint32_t cur = (e >> 20) & 1u;
+                const bool mine = q < taken && ((accm >> q) & 1u);
+                if (mine) mk[(l - 1) * mkl + v] = (MK)((cur ^ 1u) << LVB);    // (repeats store alike)
+                else atomicAnd(mark_word(l, v), ~((1u << q) << (16 * (v & 1))));
+            }
+        }
+        k += taken;
+        pk += (uint32_t)taken;
+        par ^= 1;
+    }
+    if (TRACE && tid == 0) {
+        for (; k < nsteps; ++k) {
+            if (st.tr_i) st.tr_i[k * R + r] = -1;
+            if (st.tr_acc) st.tr_acc[k * R + r] = -1;
+            if (st.tr_sum) st.tr_sum[k * R + r] = sum_end;
+            if (st.tr_dE) st.tr_dE[k * R + r] = 0.0;
+        }
+    }
+    __syncthreads();
+    {
+        const int64_t col = r >> 6;
+        for (int64_t v = tid; v < n; v += NT) {
+            if (((lev[v >> 5] ^ lev0s[v >> 5]) >> (v & 31)) & 1u)
+                atomicXor((unsigned long long*)&s[v * W + col], 1ull << (r & 63));
+        }
+    }
+    if (w == NE) {
+        const int e = (pk > 0) ? q_end[(pk - 1u) & 63u] : idx0;
+        if (((e >> 10) & 1) == gen)
+            for (int q = lane; q < MT_N; q += 64) st.mt[r * MT_N + q] = mt[q];
+        if (lane == 0) st.mt_idx[r] = e & 1023;
+    }
+    if (tid == 0) {
+        st.a[r] = a;
+        st.b[r] = b;
+        st.t[r] = t;
+        st.sum_end[r] = sum_end;
+        st.done[r] = done;
+        if (st.tr_tie) st.tr_tie[r] += ties;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // The whole CU at p + c - 1 = 1 (k_sa_lds_wg1<D, NW, NQ>, configs[0]'s
 // SA_RRG.py p = c = 1): NW waves of NQ lane groups, k_sa_lds_multi's step in
 // every wave, K = NW * NQ consecutive proposals per round.  Proposal q's
@@ -2839,7 +3352,11 @@ extern "C" int64_t mjx_sa_lds_plan(int64_t n, int d, int p, int c, uint32_t flag
     salds::Geo g2;
     const int nwv = salds::wg_waves(n, d, T, split);
     salds::GeoW1 gw1;
-    if (!(flags & (MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE | MJX_SA_LDS_PAIR | MJX_SA_LDS_WAVE)) && small_d && T == 1 &&
+    salds::GeoC gc;
+    if ((flags & MJX_SA_LDS_CU) && small_d && salds::geometry_cu(n, d, T, &gc)) {
+        th = 1024;                                  // k_sa_lds_cu: 15 item waves + the parser
+        bytes = gc.bytes;
+    } else if (!(flags & (MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE | MJX_SA_LDS_PAIR | MJX_SA_LDS_WAVE)) && small_d && T == 1 &&
         salds::geometry_wg1(n, d, 32, &gw1)) {
         th = 320;                                   // k_sa_lds_wg1: 4 waves x 8 proposals + the parser
         bytes = gw1.bytes;
@@ -2867,13 +3384,30 @@ extern "C" int mjx_sa_lds_steps(const int32_t* adj, int64_t n, int d, int p, int
     if (!salds::geometry(n, d, T, &g)) return MJX_ERANGE;
     const mjx_sa_state st = *stp;
     if (!st.mt || !st.mt_idx || !st.a || !st.b || !st.t || !st.sum_end || !st.done) return MJX_EINVAL;
-    if (st.opt_flags &
-        ~(MJX_SA_NO_SPEC | MJX_SA_NO_CONE2 | MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE | MJX_SA_LDS_PAIR | MJX_SA_LDS_WAVE))
+    if (st.opt_flags & ~(MJX_SA_NO_SPEC | MJX_SA_NO_CONE2 | MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE | MJX_SA_LDS_PAIR |
+                         MJX_SA_LDS_WAVE | MJX_SA_LDS_CU))
         return MJX_EINVAL;
     if (nsteps == 0) return MJX_OK;
     if (R > INT32_MAX) return MJX_ERANGE;
     const int64_t W = (R + 63) / 64;
     hipStream_t hs = as_stream(stream);
+    salds::GeoC gc;
+    if ((st.opt_flags & MJX_SA_LDS_CU) && (d == 3 || d == 4) && salds::geometry_cu(n, d, T, &gc)) {
+        const bool trc = st.tr_i || st.tr_acc || st.tr_sum || st.tr_dE;
+        auto goc = [&](auto kern) -> int {
+            MJX_HIP(set_max_lds(kern, gc.bytes), "sa_lds lds");
+            kern<<<(unsigned)R, 1024, (size_t)gc.bytes, hs>>>(adj, n, R, W, (u64*)s, st, nsteps, par_a, par_b, a_cap,
+                                                              b_cap, t_cap, gc);     // 15 item waves + the parser
+            MJX_LAUNCH_CHECK("k_sa_lds_cu");
+            return MJX_OK;
+        };
+#define MJX_LDS_CU(DD)                                                                                      \
+        if (T == 2) return trc ? goc(salds::k_sa_lds_cu<DD, 2, true>) : goc(salds::k_sa_lds_cu<DD, 2, false>); \
+        return trc ? goc(salds::k_sa_lds_cu<DD, 3, true>) : goc(salds::k_sa_lds_cu<DD, 3, false>);
+        if (d == 3) { MJX_LDS_CU(3) }
+        MJX_LDS_CU(4)
+#undef MJX_LDS_CU
+    }
     auto go = [&](auto kern) -> int {
         MJX_HIP(set_max_lds(kern, g.bytes), "sa_lds lds");
         kern<<<(unsigned)R, 64, (size_t)g.bytes, hs>>>(adj, d, n, T, R, W, (u64*)s, st, nsteps, par_a, par_b, a_cap,

@@ -47,7 +47,8 @@ def schedule_constants(n):
 
 
 KERNEL_FLAGS = {"no_spec": _lib.MJX_SA_NO_SPEC, "no_cone2": _lib.MJX_SA_NO_CONE2, "lds_serial": _lib.MJX_SA_LDS_SERIAL,
-                "lds_single": _lib.MJX_SA_LDS_SINGLE, "lds_pair": _lib.MJX_SA_LDS_PAIR, "lds_wave": _lib.MJX_SA_LDS_WAVE}
+                "lds_single": _lib.MJX_SA_LDS_SINGLE, "lds_pair": _lib.MJX_SA_LDS_PAIR, "lds_wave": _lib.MJX_SA_LDS_WAVE,
+                "lds_cu": _lib.MJX_SA_LDS_CU}
 
 
 def _graph_stack(N, R, graph_of):
@@ -115,7 +116,8 @@ class SAReplicas:
         selection passed to the ABI (tests, tuning): ``split`` (waves per word
         column), ``spec_k`` (8 or 16), ``no_spec``, ``no_cone2``, ``lds_serial``, ``lds_single``, ``lds_pair``,
         ``lds_wave`` (one wave per replica instead of the whole-CU kernel at
-        p+c-1 >= 2; ``split`` = 4 or 8 waves for the latter); the results
+        p+c-1 >= 2; ``split`` = 4 or 8 waves for the latter), ``lds_cu`` (the
+        whole CU level by level, d = 3, 4 at p+c-1 = 2, 3); the results
         never depend on it.  ``rng``: ``"mt19937"`` replays numpy's seeded
         stream (the reference's proposals, bit for bit); ``"philox"`` is the
         NON-parity throughput mode: the proposal of step t of

@@ -61,6 +61,11 @@ def _check(tr, conf, t, graphs, graph_of, seeds, p, c, K, replicas):
     (3, 64, 2, 1, 40, 400, {"split": 8}, "lightcone", "lds"),
     (4, 64, 2, 2, 40, 400, {"lds_wave": True}, "lightcone", "lds"),
     (3, 64, 2, 1, 40, 400, {"split": 4}, "lightcone", "lds"),               # many conflicts, 4 waves
+    (4, 300, 3, 1, 65, 300, {"lds_cu": True}, "lightcone", "lds"),          # level-synchronous whole CU
+    (4, 40, 3, 1, 40, 600, {"lds_cu": True}, "lightcone", "lds"),
+    (3, 64, 2, 1, 40, 400, {"lds_cu": True}, "lightcone", "lds"),
+    (4, 64, 2, 2, 40, 400, {"lds_cu": True}, "lightcone", "lds"),           # T = 3
+    (3, 30, 2, 2, 40, 600, {"lds_cu": True}, "lightcone", "lds"),           # T = 3, balls cover the graph
     (4, 40, 3, 1, 40, 600, {}, "lightcone", "lds"),                         # n=40: most rounds conflict
     (3, 30, 2, 2, 40, 600, {}, "lightcone", "lds"),
     (4, 200, 1, 1, 5, 40, {}, "rollout", None),
@@ -142,6 +147,7 @@ def test_sa_run_distinct_graphs_to_consensus(mjx_mod, n, N_stat, seed, graph_see
     (4, 64, 3, 1, {}), (4, 1000, 3, 1, {}), (3, 500, 2, 1, {}),                       # k_sa_lds_wg<D,T,16,false>
     (4, 1000, 3, 1, {"split": 8}), (4, 64, 3, 1, {"split": 8}),                      # k_sa_lds_wg<D,T,8,false>
     (4, 1000, 3, 1, {"split": 4}), (4, 1000, 3, 1, {"lds_wave": True}), (4, 1000, 1, 1, {"lds_wave": True}),
+    (4, 1000, 3, 1, {"lds_cu": True}), (4, 64, 3, 1, {"lds_cu": True}), (3, 500, 2, 1, {"lds_cu": True}),
 ])
 def test_lds_no_trace_matches_oracle(mjx_mod, d, n, p, c, kernel):
     """The kernels run() and the bench use (no trace buffers: TRACE=false

@@ -36,6 +36,8 @@ def _plan(mjx_mod, n, p, c, sa):
 @pytest.mark.parametrize("p,c,K1,K2,threads_want,kernel", [
     (3, 1, 1900, 1133, 1024, None),          # SA_RRG.py's p=3, c=1: k_sa_lds_wg<4,3,16,false>, 16 waves
     (3, 1, 1900, 1133, 512, {"split": 8}),   # the 8-wave form (byte marks)
+    (3, 1, 1900, 1133, 1024, {"lds_cu": True}),   # k_sa_lds_cu<4,3,false>, level-synchronous
+    (2, 2, 1900, 1133, 1024, {"lds_cu": True}),   # k_sa_lds_cu<4,3,false>, T = 3 via c = 2
     (1, 1, 2900, 1733, 320, None),           # configs[0]'s p=c=1: k_sa_lds_wg1<4,4,8,false>, 4 waves + the parser
 ])
 def test_script_size_no_trace_matches_oracle(mjx_mod, p, c, K1, K2, threads_want, kernel):

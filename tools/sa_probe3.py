@@ -26,6 +26,7 @@ VARIANTS = {
     "lds": ("lds", None),                                   # the default LDS kernel for (p, c)
     "lds-wg8": ("lds", {"split": 8}),                       # whole CU, 8 waves (p+c-1 >= 2; default 16 where it fits)
     "lds-wg4": ("lds", {"split": 4}),                       # whole CU, 4 waves (p+c-1 >= 2)
+    "lds-cu": ("lds", {"lds_cu": True}),                    # whole CU, level-synchronous (d 3/4, T 2/3)
     "lds-wave": ("lds", {"lds_wave": True}),                # one wave: 8 proposals (T = 1) / 2 (T >= 2) per step
     "lds-pair": ("lds", {"lds_wave": True, "lds_pair": True}),   # one wave, two proposals per step
     "lds-single": ("lds", {"lds_single": True}),            # one wave, one proposal per step
