@@ -212,9 +212,11 @@ typedef struct mjx_sa_state {
 #define MJX_SA_LDS_SINGLE 8u  /* LDS layout: one proposal per step (k_sa_lds_fast), not two (k_sa_lds_pair) */
 #define MJX_SA_LDS_PAIR  16u  /* LDS layout at p+c-1 = 1: two proposals per step, not eight (k_sa_lds_multi) */
 #define MJX_SA_LDS_WAVE  32u  /* LDS layout at p+c-1 >= 2: one wave per replica (k_sa_lds_pair), not the whole
-                                 CU (k_sa_lds_wg: opt_split = 4 or 8 waves, one proposal each; default 8) */
-#define MJX_SA_LDS_CU    64u  /* LDS layout at p+c-1 = 2, 3, d = 3, 4: the whole CU level by level
-                                 (k_sa_lds_cu: every proposal's candidates of a level packed over 15 waves) */
+                                 CU (k_sa_lds_wg: opt_split = 4, 8 or 16 waves, one proposal each) */
+#define MJX_SA_LDS_CU    64u  /* LDS layout at p+c-1 = 2, 3, d = 3, 4: the whole CU level by level (k_sa_lds_cu:
+                                 15 proposals a round, each level's candidates packed over the waves; 8 waves,
+                                 16 with opt_split = 16).  The default there where it fits and no other
+                                 option is given; opt_split = 4, 8 or 16 alone select k_sa_lds_wg */
 
 /* Seed replica r with seeds[r] (device uint32[R]), draw s0 into the
  * replica-packed spins s[n*W], set a=a0, b=b0, t=0, done=0, and

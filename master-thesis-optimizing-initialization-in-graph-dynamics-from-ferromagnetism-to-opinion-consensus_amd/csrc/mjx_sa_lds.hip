@@ -2395,9 +2395,26 @@ struct GeoC {
     int off_mt;
     int off_list;   // levels 1..T, cap[l] uint32 each: node | q << 16 | cached value << 20
     int off_q;      // ring: i[64], end[64], u[64]
-    int off_res;    // per proposal: conflict word, packed word, a, b, dE, ds, cf; counters
+    int off_qc;     // ring, per proposal and candidate j = 0..d: node | dup << 16 | (its neighbours == i) << 17 | (== i) << 21
+    int off_qr;     // ring, per proposal and candidate: its row (uint2)
+    int off_gln;    // levels 1..T-1: each list entry's row (uint2)
+    int off_res;    // per proposal: -2 a s_i, b, u, a and b after; ds, cf and list lengths by parity
     int bytes;
 };
+
+// waves of k_sa_lds_cu: 8 (a cheaper barrier, the items fit), 16 with split = 16
+static int cu_waves(int split) { return split == 16 ? 16 : 8; }
+
+static bool geometry_cu(int64_t n, int d, int T, GeoC* g);
+
+// k_sa_lds_cu is the LDS kernel at d = 3, 4, p+c-1 = 2, 3 where it fits: by
+// default (no kernel options), or asked for (MJX_SA_LDS_CU, split 8 or 16);
+// split = 4 / 8 / 16 alone keep k_sa_lds_wg with that many waves
+static bool use_cu(int64_t n, int d, int T, uint32_t flags, int split, GeoC* g) {
+    if (!(d == 3 || d == 4) || !(T == 2 || T == 3) || !geometry_cu(n, d, T, g)) return false;
+    if (flags & MJX_SA_LDS_CU) return true;
+    return split == 0 && !(flags & (MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE | MJX_SA_LDS_PAIR | MJX_SA_LDS_WAVE));
+}
 
 static bool geometry_cu(int64_t n, int d, int T, GeoC* g) {
     if (n < 2 || n > 65535 || d < 3 || d > 4 || T < 2 || T > 3) return false;
@@ -2417,19 +2434,25 @@ static bool geometry_cu(int64_t n, int d, int T, GeoC* g) {
     g->off_list = (int)off;  off += (int64_t)(g->cap[1] + g->cap[2] + g->cap[3]) * 4;
     off = (off + 15) / 16 * 16;
     g->off_q = (int)off;     off += 64 * 4 + 64 * 4 + 64 * 8;
-    g->off_res = (int)off;   off += 16 * (4 + 4 + 8 + 8 + 8 + 4 + 4) + 2 * 4 * 4 + 4 * 4;
+    g->off_qc = (int)off;    off += 64 * 5 * 4;
+    g->off_qr = (int)off;    off += 64 * 5 * 8;
+    g->off_gln = (int)off;   off += (int64_t)(g->cap[1] + (T == 3 ? g->cap[2] : 0)) * 8;
+    g->off_res = (int)off;   off += 5 * 16 * 8 + 2 * 2 * 16 * 4 + 2 * 4 * 4 + 4 * 4;
     g->bytes = (int)off;
     return (size_t)off <= kLdsMax;
 }
 
-template <int D, int T, bool TRACE>
-__global__ void __launch_bounds__(1024) k_sa_lds_cu(const int32_t* __restrict__ adj, int64_t n, int64_t R,
+template <int D, int T, int NW, bool TRACE>
+__global__ void __launch_bounds__(64 * NW) k_sa_lds_cu(const int32_t* __restrict__ adj, int64_t n, int64_t R,
                                                    int64_t W, u64* __restrict__ s, mjx_sa_state st, int64_t nsteps,
                                                    double par_a, double par_b, double a_cap, double b_cap,
                                                    int64_t t_cap, GeoC geo) {
     static_assert((D == 3 || D == 4) && (T == 2 || T == 3), "level-synchronous LDS SA: d = 3, 4; p+c-1 = 2, 3");
     using MK = uint16_t;
-    constexpr int NW = 16, NE = 15, NT = 64 * NW, LVB = 15, DP1 = D + 1;
+    static_assert(NW == 8 || NW == 16, "8 or 16 waves");
+    // NQ proposals a round; waves 0..NI-1 take items, wave TW also the test
+    // set-up, wave PW parses the stream
+    constexpr int NQ = 15, NI = NW - 1, TW = NW - 2, PW = NW - 1, NT = 64 * NW, LVB = 15, DP1 = D + 1;
     extern __shared__ __align__(16) unsigned char smem[];
     const int tid = threadIdx.x;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2451,37 +2474,77 @@ __global__ void __launch_bounds__(1024) k_sa_lds_cu(const int32_t* __restrict__ 
     int* q_i = reinterpret_cast<int*>(smem + geo.off_q);
     int* q_end = q_i + 64;
     double* q_u = reinterpret_cast<double*>(q_end + 64);
-    uint32_t* res_cf = reinterpret_cast<uint32_t*>(smem + geo.off_res);   // per proposal: conflict bits
-    uint32_t* res = res_cf + 16;                                            // packed result
-    double* res_a = reinterpret_cast<double*>(res + 16);
-    double* res_b = res_a + 16;
-    double* res_dE = res_b + 16;
-    int* dsv = reinterpret_cast<int*>(res_dE + 16);                         // sum(s_end) change per proposal
-    uint32_t* cfv = reinterpret_cast<uint32_t*>(dsv + 16);                  // conflict bits, being ORed
-    uint32_t* cnt = cfv + 16;                                               // [2][4] list lengths by round parity
+    uint32_t* q_cn = reinterpret_cast<uint32_t*>(smem + geo.off_qc);
+    uint2* q_cr = reinterpret_cast<uint2*>(smem + geo.off_qr);
+    uint2* gln[T + 1];                                 // the rows of the list entries of levels 1..T-1
+    gln[0] = nullptr;
+    gln[1] = reinterpret_cast<uint2*>(smem + geo.off_gln);
+    gln[2] = (T == 3) ? gln[1] + geo.cap[1] : nullptr;
+    gln[T] = nullptr;
+    // per proposal, by the test wave at round start: -2 a_q s_i, b_q, u, the
+    // schedule after the step
+    double* pre_t1 = reinterpret_cast<double*>(smem + geo.off_res);
+    double* pre_bh = pre_t1 + 16;
+    double* pre_u = pre_bh + 16;
+    double* pre_anx = pre_u + 16;
+    double* pre_bnx = pre_anx + 16;
+    int* dsv = reinterpret_cast<int*>(pre_bnx + 16);                        // [2][16] sum(s_end) change by parity
+    uint32_t* cfv = reinterpret_cast<uint32_t*>(dsv + 32);                  // [2][16] conflict bits, being ORed
+    uint32_t* cnt = cfv + 32;                                               // [2][4] list lengths by round parity
     int* ctl = reinterpret_cast<int*>(cnt + 8);
 
     auto bit_of = [&](int v) -> uint32_t { return (lev[v >> 5] >> (v & 31)) & 1u; };
     auto lvl = [&](int t, int v) -> uint32_t { return ((uint32_t)mk[(t - 1) * mkl + v] >> LVB) & 1u; };
     auto mark_word = [&](int t, int v) -> uint32_t* { return reinterpret_cast<uint32_t*>(mk + (t - 1) * mkl + (v & ~1)); };
-    auto nbrs = [&](int v, int (&o)[D]) {
-        const uint2 x = *reinterpret_cast<const uint2*>(rows + v * 4);
+    auto row = [&](int v) -> uint2 { return *reinterpret_cast<const uint2*>(rows + v * 4); };
+    auto unpack = [&](uint2 x, int (&o)[D]) {
         o[0] = (int)(x.x & 0xffffu);
         o[1] = (int)(x.x >> 16);
         o[2] = (int)(x.y & 0xffffu);
         if constexpr (D > 3) o[3] = (int)(x.y >> 16);
     };
+    auto nbrs = [&](int v, int (&o)[D]) { unpack(row(v), o); };
     auto maj = [&](int ones, uint32_t own) -> uint32_t {       // always-stay majority (code/SA_RRG.py:19-20)
         return (2 * ones > D) ? 1u : ((2 * ones < D) ? 0u : own);
     };
-    // the wave's items appended to a list: one LDS atomic per wave
-    auto append = [&](uint32_t* list, uint32_t* counter, bool add, uint32_t entry) {
+    // the wave's items appended to a list (with their rows below the last
+    // level): one LDS atomic per wave
+    auto append = [&](uint32_t* list, uint2* lrow, uint32_t* counter, bool add, uint32_t entry, uint2 erow) {
         const u64 m = __ballot(add);
         if (!m) return;
         uint32_t base = 0;
         if (lane == (int)(__ffsll((unsigned long long)m) - 1)) base = atomicAdd(counter, (uint32_t)__popcll(m));
         base = (uint32_t)__builtin_amdgcn_readlane((int)base, __ffsll((unsigned long long)m) - 1);
-        if (add) list[base + (uint32_t)__popcll(m & ltmask)] = entry;
+        if (add) {
+            const uint32_t at = base + (uint32_t)__popcll(m & ltmask);
+            list[at] = entry;
+            if (lrow) lrow[at] = erow;
+        }
+    };
+    // a ring entry's static neighbourhood, by the parse wave when it is parsed:
+    // candidate j = 0..d of level 1 (i, then its neighbours), its row, whether
+    // it repeats an earlier candidate, which of its neighbours are i
+    auto prep = [&](int slot, int iv) {
+        const uint2 xi = row(iv);
+        int ri[D];
+        unpack(xi, ri);
+#pragma unroll
+        for (int j = 0; j <= D; ++j) {
+            const int cand = (j == 0) ? iv : ri[j > 0 ? j - 1 : 0];
+            int first = D;
+#pragma unroll
+            for (int e = D - 1; e >= 0; --e)
+                if (ri[e] == cand) first = e;
+            const bool dup = j > 0 && (cand == iv || first + 1 < j);
+            const uint2 xc = (j == 0) ? xi : row(cand);
+            int nv[D];
+            unpack(xc, nv);
+            uint32_t eqm = 0;
+#pragma unroll
+            for (int e = 0; e < D; ++e) eqm |= (nv[e] == iv ? 1u : 0u) << e;
+            q_cn[slot * DP1 + j] = (uint32_t)cand | (dup ? 1u << 16 : 0u) | (eqm << 17) | ((cand == iv) ? 1u << 21 : 0u);
+            q_cr[slot * DP1 + j] = xc;
+        }
     };
 
     // ---- launch setup (k_sa_lds_wg's): rows, level 0, marks cleared, MT state; levels 1..T
@@ -2494,7 +2557,7 @@ __global__ void __launch_bounds__(1024) k_sa_lds_cu(const int32_t* __restrict__ 
         for (int q = tid; q < nw; q += NT) lev[q] = 0u;
         for (int q = tid; q < T * nw * 16; q += NT) reinterpret_cast<uint32_t*>(mk)[q] = 0u;
         for (int q = tid; q < MT_N; q += NT) mt[q] = st.mt[r * MT_N + q];
-        if (tid < 16) {
+        if (tid < 32) {
             dsv[tid] = 0;
             cfv[tid] = 0u;
         }
@@ -2538,7 +2601,7 @@ __global__ void __launch_bounds__(1024) k_sa_lds_cu(const int32_t* __restrict__ 
     double inv_n = 1.0 / (double)n;
     asm volatile("" : "+v"(a), "+v"(b), "+v"(par_a), "+v"(par_b), "+v"(a_cap), "+v"(b_cap), "+v"(inv_n));
 
-    // ---- the proposal ring, parsed by wave NE (k_sa_lds_wg's, unchanged)
+    // ---- the proposal ring, parsed by wave PW (k_sa_lds_wg's, and each entry's prep)
     uint32_t npend = 0, pk = 0;
     int gen = 0;
     const int idx0 = idx;
@@ -2578,6 +2641,7 @@ __global__ void __launch_bounds__(1024) k_sa_lds_cu(const int32_t* __restrict__ 
                 q_i[q] = (int)y;
                 q_u[q] = mt_double(x1, x2);
                 q_end[q] = (idx + lane + 3) | (gen << 10);
+                prep(q, (int)y);
             }
             npend += got;
             idx += pos;
@@ -2601,6 +2665,7 @@ __global__ void __launch_bounds__(1024) k_sa_lds_cu(const int32_t* __restrict__ 
             q_i[q] = iv;
             q_u[q] = mt_double(w1, w2);
             q_end[q] = idx | (gen << 10);
+            prep(q, iv);
         }
         npend += 1;
         return true;
@@ -2609,45 +2674,82 @@ __global__ void __launch_bounds__(1024) k_sa_lds_cu(const int32_t* __restrict__ 
 
     int64_t k = 0;
     int par = 0;                                       // round parity: the list-length set in use
+#ifdef MJX_SA_PROF
+    // (slots: 0 publish barrier, 1 level work, 2 level barriers, 3 accept test,
+    // 5 resolve + apply; 6 rounds; 7 taken; 8..10 |C_1..3|; wave 0's own at 16 + slot)
+    unsigned int _acc[16] = {};
+    unsigned long long _t0 = __builtin_amdgcn_s_memtime();
+#endif
     while (k < nsteps && done == 0) {
-        if (w == NE) {
-            while (npend - pk < (uint32_t)NE)
+        if (w == PW) {
+            while (npend - pk < (uint32_t)NQ)
                 if (!parse_window(room())) break;
             if (lane == 0) ctl[0] = (int)npend;
         }
         __syncthreads();                                   // the round's proposals are published
+        LDS_STAMP(0);
         const uint32_t npd = (uint32_t)__builtin_amdgcn_readfirstlane(ctl[0]);
         int nq = (int)(npd - pk);
-        if (nq > NE) nq = NE;
+        if (nq > NQ) nq = NQ;
         if ((int64_t)nq > nsteps - k) nq = (int)(nsteps - k);
         uint32_t* cn = cnt + 4 * par;                      // this round's list lengths (zeroed)
+        int* dsp = dsv + 16 * par;                         // this round's accumulators (zeroed)
+        uint32_t* cfp = cfv + 16 * par;
         // ---- level 1 (items q*(d+1) + j), and the level-0 conflicts (items: pairs j < q)
-        if (w < NE) {
+        if (w < NI) {
+            if (w == TW) {
+                // each proposal's schedule, -2 a s_i and u (code/SA_RRG.py:74-76,80-81)
+                // for the accept test after the levels; the other parity's
+                // accumulators and list lengths cleared for the next round
+                const bool lq = lane < nq;
+                const int q = lq ? lane : 0;
+                const int iv = q_i[(pk + (uint32_t)q) & 63u];
+                const double u = q_u[(pk + (uint32_t)q) & 63u];
+                const uint32_t old_i = bit_of(iv);
+                double ah = a, bh = b;
+                if (!(ah >= a_cap && bh >= b_cap)) {
+                    for (int qq = 0; qq < NQ; ++qq) {
+                        if (qq < q) {
+                            if (ah < a_cap) ah = par_a * ah;
+                            if (bh < b_cap) bh = par_b * bh;
+                        }
+                    }
+                }
+                const double si = old_i ? 1.0 : -1.0;
+                if (lq) {
+                    pre_t1[q] = (-2.0 * ah) * si;
+                    pre_bh[q] = bh;
+                    pre_u[q] = u;
+                    pre_anx[q] = (ah < a_cap) ? par_a * ah : ah;
+                    pre_bnx[q] = (bh < b_cap) ? par_b * bh : bh;
+                }
+                if (lane < 16) {
+                    dsv[16 * (par ^ 1) + lane] = 0;
+                    cfv[16 * (par ^ 1) + lane] = 0u;
+                }
+                if (lane < 4) cnt[4 * (par ^ 1) + lane] = 0u;
+            }
             const int n1 = nq * DP1, np = nq * (nq - 1) / 2;
-            for (int base = 64 * w; base < n1 + np; base += 64 * NE) {
+            for (int base = 64 * w; base < n1 + np; base += 64 * NI) {
                 const int it = base + lane;
                 bool add = false;
                 uint32_t entry = 0;
+                uint2 xc = make_uint2(0u, 0u);
                 if (it < n1) {
                     const int q = it / DP1, j = it - q * DP1;
-                    const int iv = q_i[(pk + (uint32_t)q) & 63u];
-                    int ri[D];
-                    nbrs(iv, ri);
-                    const int cand = (j == 0) ? iv : ri[j > 0 ? j - 1 : 0];
-                    int first = D;
-#pragma unroll
-                    for (int e = D - 1; e >= 0; --e)
-                        if (ri[e] == cand) first = e;
-                    const bool dup = j > 0 && (cand == iv || first + 1 < j);
+                    const int slot = (int)((pk + (uint32_t)q) & 63u);
+                    const uint32_t ce = q_cn[slot * DP1 + j];
+                    xc = q_cr[slot * DP1 + j];
+                    const int cand = (int)(ce & 0xffffu);
                     int nv[D];
-                    nbrs(cand, nv);
+                    unpack(xc, nv);
                     int ones = 0;
 #pragma unroll
-                    for (int e = 0; e < D; ++e) ones += (int)(bit_of(nv[e]) ^ (nv[e] == iv));
-                    const uint32_t own = bit_of(cand) ^ (cand == iv);
+                    for (int e = 0; e < D; ++e) ones += (int)(bit_of(nv[e]) ^ ((ce >> (17 + e)) & 1u));
+                    const uint32_t own = bit_of(cand) ^ ((ce >> 21) & 1u);
                     const uint32_t nb = maj(ones, own);
                     const uint32_t cur = lvl(1, cand);
-                    add = !dup && nb != cur;
+                    add = !((ce >> 16) & 1u) && nb != cur;
                     if (add) atomicOr(mark_word(1, cand), (1u << q) << (16 * (cand & 1)));
                     entry = (uint32_t)cand | ((uint32_t)q << 16) | (cur << 20);
                 } else if (it < n1 + np) {
@@ -2657,10 +2759,11 @@ __global__ void __launch_bounds__(1024) k_sa_lds_cu(const int32_t* __restrict__ 
                     if (q * (q - 1) / 2 > k2) --q;
                     if ((q + 1) * q / 2 <= k2) ++q;
                     const int j = k2 - q * (q - 1) / 2;
-                    const int iq = q_i[(pk + (uint32_t)q) & 63u], ij = q_i[(pk + (uint32_t)j) & 63u];
+                    const int sq = (int)((pk + (uint32_t)q) & 63u), sj = (int)((pk + (uint32_t)j) & 63u);
+                    const int iq = (int)(q_cn[sq * DP1] & 0xffffu), ij = (int)(q_cn[sj * DP1] & 0xffffu);
                     int rq[D], rj[D];
-                    nbrs(iq, rq);
-                    nbrs(ij, rj);
+                    unpack(q_cr[sq * DP1], rq);
+                    unpack(q_cr[sj * DP1], rj);
                     bool meet = iq == ij;
 #pragma unroll
                     for (int e = 0; e < D; ++e) meet |= (rj[e] == iq) | (ij == rq[e]);
@@ -2668,32 +2771,38 @@ __global__ void __launch_bounds__(1024) k_sa_lds_cu(const int32_t* __restrict__ 
                     for (int e = 0; e < D; ++e)
 #pragma unroll
                         for (int f = 0; f < D; ++f) meet |= rj[e] == rq[f];
-                    if (meet) atomicOr(&cfv[q], 1u << j);
+                    if (meet) atomicOr(&cfp[q], 1u << j);
                 }
-                append(gl[1], &cn[1], add, entry);
+                append(gl[1], gln[1], &cn[1], add, entry, xc);
             }
-        } else {
-            for (int it = 0; it < 2 && room() >= 8u; ++it)
-                if (!parse_window(room())) break;
+        } else if (room() >= 8u) {
+            parse_window(room());                          // one window a level: its prep outlasts a level's items
         }
+        LDS_STAMP(1);
         __syncthreads();                                   // level-1 marks and C_1 lists complete
+        LDS_STAMP(2);
         // ---- levels 2..T: every member of C_{l-1} of every proposal and its d neighbours
 #pragma unroll
         for (int l = 2; l <= T; ++l) {
-            if (w < NE) {
+            if (w < NI) {
                 const int nm = (int)cn[l - 1];
-                for (int base = 64 * w; base < nm * DP1; base += 64 * NE) {
+                for (int base = 64 * w; base < nm * DP1; base += 64 * NI) {
                     const int it = base + lane;
                     bool add = false;
                     uint32_t entry = 0;
+                    uint2 xc = make_uint2(0u, 0u);
                     if (it < nm * DP1) {
                         const int mi = it / DP1, j = it - mi * DP1;
                         const uint32_t me = gl[l - 1][mi];
+                        const uint2 xm = gln[l - 1][mi];
                         const int mc = (int)(me & 0xffffu), q = (int)((me >> 16) & 15u);
-                        const int c2 = (j == 0) ? mc : (int)rows[mc * 4 + (j > 0 ? j - 1 : 0)];
+                        int nm2[D];
+                        unpack(xm, nm2);
+                        const int c2 = (j == 0) ? mc : nm2[j > 0 ? j - 1 : 0];
                         const uint32_t early = (1u << q) - 1u;
+                        xc = row(c2);
                         int nv2[D];
-                        nbrs(c2, nv2);
+                        unpack(xc, nv2);
                         int ones = 0;
                         uint32_t cfm = 0;
                         // node v at level l-1 as proposal q sees it; the earlier proposals' marks into cfm
@@ -2705,7 +2814,7 @@ __global__ void __launch_bounds__(1024) k_sa_lds_cu(const int32_t* __restrict__ 
 #pragma unroll
                         for (int e = 0; e < D; ++e) ones += (int)look(nv2[e]);
                         const uint32_t own = look(c2);
-                        if (cfm) atomicOr(&cfv[q], cfm);
+                        if (cfm) atomicOr(&cfp[q], cfm);
                         const uint32_t nb = maj(ones, own);
                         const uint32_t cur = lvl(l, c2);
                         const bool chg = nb != cur;
@@ -2714,47 +2823,49 @@ __global__ void __launch_bounds__(1024) k_sa_lds_cu(const int32_t* __restrict__ 
                         if (l == T) {
                             // the last level counts distinct nodes: the first mark wins
                             if (chg) add = (atomicOr(mark_word(l, c2), mb) & mb) == 0u;
-                            if (add) atomicAdd(&dsv[q], cur == 0u ? 2 : -2);
+                            if (add) atomicAdd(&dsp[q], cur == 0u ? 2 : -2);
                         } else if (chg) {
                             atomicOr(mark_word(l, c2), mb);
                         }
                         entry = (uint32_t)c2 | ((uint32_t)q << 16) | (cur << 20);
                     }
-                    append(gl[l], &cn[l], add, entry);
+                    append(gl[l], gln[l], &cn[l], add, entry, xc);
                 }
-            } else if (l == 2) {
-                for (int it = 0; it < 2 && room() >= 8u; ++it)
-                    if (!parse_window(room())) break;
+            } else if (w == PW && room() >= 8u) {
+                parse_window(room());
             }
+            LDS_STAMP(1);
             __syncthreads();                               // level-l marks, C_l lists, conflict bits complete
+            LDS_STAMP(2);
         }
-        // ---- delta_H and the Metropolis test of each proposal (lane q of wave 0)
-        // (code/SA_RRG.py:37,74-76); the schedule after q steps (:80-81)
-        if (w == 0) {
-            const bool lq = lane < nq;
-            const int q = lq ? lane : 0;
-            const int iv = q_i[(pk + (uint32_t)q) & 63u];
-            const double u = q_u[(pk + (uint32_t)q) & 63u];
-            const uint32_t old_i = bit_of(iv);
-            const int64_t ds = (int64_t)dsv[q];
-            double ah = a, bh = b;
-            if (!(ah >= a_cap && bh >= b_cap)) {
-                for (int qq = 0; qq < NE; ++qq) {
-                    if (qq < q) {
-                        if (ah < a_cap) ah = par_a * ah;
-                        if (bh < b_cap) bh = par_b * bh;
-                    }
-                }
-            }
-            const double anx = (ah < a_cap) ? par_a * ah : ah;
-            const double bnx = (bh < b_cap) ? par_b * bh : bh;
-            const double si = old_i ? 1.0 : -1.0;
-            const double t1 = (-2.0 * ah) * si;
-            const double t2 = bh * (double)(-ds);
-            const double num = t1 + t2;
-            bool acc;
-            bool tie = false;
-            double dE = 0.0;
+        // the lists' first entries this wave applies below, read ahead of the test
+        const int c1 = (int)cn[1];
+        const int c2 = c1 + (int)cn[2];
+        const int c3 = c2 + (T == 3 ? (int)cn[3] : 0);
+        auto list_at = [&](int it, int& l) -> uint32_t {
+            l = (it < c1) ? 1 : ((it < c2) ? 2 : 3);
+            return gl[l][it - ((l == 1) ? 0 : ((l == 2) ? c1 : c2))];
+        };
+        int l0 = 1;
+        const int it0 = 64 * w + lane;
+        const uint32_t e0 = (w < PW && it0 < c3) ? list_at(it0, l0) : 0u;
+        // ---- delta_H and the Metropolis test of each proposal, lane q of every wave
+        // (code/SA_RRG.py:37,74-76): the same arithmetic in every wave, so no
+        // barrier hands the results over
+        const bool lq = lane < nq;
+        const int ql = lq ? lane : 0;
+        const int64_t ds = (int64_t)dsp[ql];
+        const uint32_t pcf = lq ? cfp[ql] : 0u;
+        const double bh = pre_bh[ql];
+        const double t1 = pre_t1[ql];
+        const double u = pre_u[ql];
+        const double anx = pre_anx[ql], bnx = pre_bnx[ql];
+        const double t2 = bh * (double)(-ds);
+        const double num = t1 + t2;
+        bool acc;
+        bool tie = false;
+        double dE = 0.0;
+        {
             const float xf = (float)(-num * inv_n);
             const float ef = __expf(xf);
             const float mg = ef * (1e-6f * (1.0f + fabsf(xf))) + 1e-37f;
@@ -2768,34 +2879,18 @@ __global__ void __launch_bounds__(1024) k_sa_lds_cu(const int32_t* __restrict__ 
                 acc = u < prob;
                 tie = e < 1.0 && fabs(u - e) <= 4.0 * (nextafter(e, 2.0) - e);
             }
-            if (lq) {
-                res_cf[q] = cfv[q];
-                res[q] = (acc ? 1u : 0u) | (tie ? 2u : 0u) | ((uint32_t)(ds & 0xffff) << 16);
-                res_a[q] = anx;
-                res_b[q] = bnx;
-                res_dE[q] = dE;
-            }
-            // the next round's accumulators and list lengths (nobody reads them any more this round)
-            if (lane < 16) {
-                dsv[lane] = 0;
-                cfv[lane] = 0u;
-            }
-            if (lane < 4) cnt[4 * (par ^ 1) + lane] = 0u;
         }
-        __syncthreads();                                   // every proposal's result
+        LDS_STAMP(3);
         // ---- resolve in proposal order (every wave alike, k_sa_lds_wg's rule)
-        const bool lq = lane < nq;
-        const uint32_t pq = lq ? res[lane] : 0u;
-        const uint32_t pcf = lq ? res_cf[lane] : 0u;
-        const bool aq = pq & 1u;
-        const uint32_t accm = (uint32_t)__ballot(lq && aq);
+        const bool aq = lq && acc;
+        const uint32_t accm = (uint32_t)__ballot(aq);
         const u64 clm = __ballot(lq && (pcf & accm) != 0u);
         int qstop = nq;
         if (clm) {
             const int qc = __ffsll((unsigned long long)clm) - 1;
             if (qc < qstop) qstop = qc;
         }
-        int pre = (lq && aq) ? (int)(int16_t)(pq >> 16) : 0;
+        int pre = aq ? (int)ds : 0;
         pre += __builtin_amdgcn_update_dpp(0, pre, 0x111, 0xf, 0xf, false);     // row_shr:1
         pre += __builtin_amdgcn_update_dpp(0, pre, 0x112, 0xf, 0xf, false);     // row_shr:2
         pre += __builtin_amdgcn_update_dpp(0, pre, 0x114, 0xf, 0xf, false);     // row_shr:4
@@ -2808,46 +2903,66 @@ __global__ void __launch_bounds__(1024) k_sa_lds_cu(const int32_t* __restrict__ 
             const int qs = __ffsll((unsigned long long)stq) - 1;
             if (qs + 1 < taken) taken = qs + 1;
         }
-        ties += __popcll(__ballot(lane < taken && ((pq >> 1) & 1u)));
+        ties += __popcll(__ballot(lane < taken && tie));
         if constexpr (TRACE) {
             if (w == 0 && lane < taken) {
                 const int64_t kk = k + lane;
                 const int iv = q_i[(pk + (uint32_t)lane) & 63u];
                 if (st.tr_i) st.tr_i[kk * R + r] = iv;
-                if (st.tr_acc) st.tr_acc[kk * R + r] = ((accm >> lane) & 1u) ? 1 : 0;
+                if (st.tr_acc) st.tr_acc[kk * R + r] = acc ? 1 : 0;
                 if (st.tr_sum) st.tr_sum[kk * R + r] = sum_after;
-                if (st.tr_dE) st.tr_dE[kk * R + r] = res_dE[lane];
+                if (st.tr_dE) st.tr_dE[kk * R + r] = dE;
             }
         }
         sum_end = rl64(sum_after, taken - 1);
         done = __builtin_amdgcn_readlane(dnq, taken - 1);
         t += taken;                                                 // (code/SA_RRG.py:77,82)
-        a = res_a[taken - 1];                                       // (:80-81) after the taken steps
-        b = res_b[taken - 1];
+        a = __longlong_as_double(rl64(__double_as_longlong(anx), taken - 1));   // (:80-81) after the taken steps
+        b = __longlong_as_double(rl64(__double_as_longlong(bnx), taken - 1));
         // ---- the taken accepted proposals' changes (the level bit of the mark set,
         // its proposal bits cleared); every other proposal clears its own bits
-        if (w == 0 && lane < taken && ((accm >> lane) & 1u)) {
+        if (w == 0 && lane < taken && aq) {
             const int iv = q_i[(pk + (uint32_t)lane) & 63u];
             atomicXor(&lev[iv >> 5], 1u << (iv & 31));
         }
-        if (w < NE) {
-            const int c1 = (int)cn[1];
-            const int c2 = c1 + (int)cn[2];
-            const int c3 = c2 + (T == 3 ? (int)cn[3] : 0);
-            for (int it = 64 * w + lane; it < c3; it += 64 * NE) {
-                const int l = (it < c1) ? 1 : ((it < c2) ? 2 : 3);
-                const uint32_t e = gl[l][it - ((l == 1) ? 0 : ((l == 2) ? c1 : c2))];
+        if (w < PW) {
+            auto apply = [&](uint32_t e, int l) {
                 const int v = (int)(e & 0xffffu), q = (int)((e >> 16) & 15u);
                 const uint32_t cur = (e >> 20) & 1u;
                 const bool mine = q < taken && ((accm >> q) & 1u);
                 if (mine) mk[(l - 1) * mkl + v] = (MK)((cur ^ 1u) << LVB);    // (repeats store alike)
                 else atomicAnd(mark_word(l, v), ~((1u << q) << (16 * (v & 1))));
+            };
+            if (it0 < c3) apply(e0, l0);
+            for (int it = it0 + 64 * PW; it < c3; it += 64 * PW) {
+                int l;
+                const uint32_t e = list_at(it, l);
+                apply(e, l);
             }
         }
+        LDS_STAMP(5);
+#ifdef MJX_SA_PROF
+        _acc[6] += 1;
+        _acc[7] += (unsigned int)taken;
+        _acc[8] += cn[1];
+        _acc[9] += cn[2];
+        _acc[10] += (T == 3) ? cn[3] : 0u;
+#endif
         k += taken;
         pk += (uint32_t)taken;
         par ^= 1;
     }
+#ifdef MJX_SA_PROF
+    if (lane == 0 && w < PW)
+        for (int q = 0; q < 11; ++q) atomicAdd(&mjx_sa_lds_prof[q + (w == 0 ? 16 : 0)], (unsigned long long)_acc[q]);   // (16.. wave 0)
+    if (lane == 0 && w == PW) {                    // the parse wave's phases at 11..15
+        atomicAdd(&mjx_sa_lds_prof[11], (unsigned long long)_acc[0]);
+        atomicAdd(&mjx_sa_lds_prof[12], (unsigned long long)_acc[1]);
+        atomicAdd(&mjx_sa_lds_prof[13], (unsigned long long)_acc[2]);
+        atomicAdd(&mjx_sa_lds_prof[14], (unsigned long long)_acc[3]);
+        atomicAdd(&mjx_sa_lds_prof[15], (unsigned long long)_acc[5]);
+    }
+#endif
     if (TRACE && tid == 0) {
         for (; k < nsteps; ++k) {
             if (st.tr_i) st.tr_i[k * R + r] = -1;
@@ -2864,7 +2979,7 @@ __global__ void __launch_bounds__(1024) k_sa_lds_cu(const int32_t* __restrict__ 
                 atomicXor((unsigned long long*)&s[v * W + col], 1ull << (r & 63));
         }
     }
-    if (w == NE) {
+    if (w == PW) {
         const int e = (pk > 0) ? q_end[(pk - 1u) & 63u] : idx0;
         if (((e >> 10) & 1) == gen)
             for (int q = lane; q < MT_N; q += 64) st.mt[r * MT_N + q] = mt[q];
@@ -3353,8 +3468,8 @@ extern "C" int64_t mjx_sa_lds_plan(int64_t n, int d, int p, int c, uint32_t flag
     const int nwv = salds::wg_waves(n, d, T, split);
     salds::GeoW1 gw1;
     salds::GeoC gc;
-    if ((flags & MJX_SA_LDS_CU) && small_d && salds::geometry_cu(n, d, T, &gc)) {
-        th = 1024;                                  // k_sa_lds_cu: 15 item waves + the parser
+    if (salds::use_cu(n, d, T, flags, split, &gc)) {
+        th = 64 * salds::cu_waves(split);           // k_sa_lds_cu: item waves + the parser
         bytes = gc.bytes;
     } else if (!(flags & (MJX_SA_LDS_SERIAL | MJX_SA_LDS_SINGLE | MJX_SA_LDS_PAIR | MJX_SA_LDS_WAVE)) && small_d && T == 1 &&
         salds::geometry_wg1(n, d, 32, &gw1)) {
@@ -3392,20 +3507,25 @@ extern "C" int mjx_sa_lds_steps(const int32_t* adj, int64_t n, int d, int p, int
     const int64_t W = (R + 63) / 64;
     hipStream_t hs = as_stream(stream);
     salds::GeoC gc;
-    if ((st.opt_flags & MJX_SA_LDS_CU) && (d == 3 || d == 4) && salds::geometry_cu(n, d, T, &gc)) {
+    if (salds::use_cu(n, d, T, st.opt_flags, st.opt_split, &gc)) {
         const bool trc = st.tr_i || st.tr_acc || st.tr_sum || st.tr_dE;
+        const int nwc = salds::cu_waves(st.opt_split);
         auto goc = [&](auto kern) -> int {
             MJX_HIP(set_max_lds(kern, gc.bytes), "sa_lds lds");
-            kern<<<(unsigned)R, 1024, (size_t)gc.bytes, hs>>>(adj, n, R, W, (u64*)s, st, nsteps, par_a, par_b, a_cap,
-                                                              b_cap, t_cap, gc);     // 15 item waves + the parser
+            kern<<<(unsigned)R, 64 * nwc, (size_t)gc.bytes, hs>>>(adj, n, R, W, (u64*)s, st, nsteps, par_a, par_b,
+                                                                  a_cap, b_cap, t_cap, gc);   // item waves + the parser
             MJX_LAUNCH_CHECK("k_sa_lds_cu");
             return MJX_OK;
         };
-#define MJX_LDS_CU(DD)                                                                                      \
-        if (T == 2) return trc ? goc(salds::k_sa_lds_cu<DD, 2, true>) : goc(salds::k_sa_lds_cu<DD, 2, false>); \
-        return trc ? goc(salds::k_sa_lds_cu<DD, 3, true>) : goc(salds::k_sa_lds_cu<DD, 3, false>);
-        if (d == 3) { MJX_LDS_CU(3) }
-        MJX_LDS_CU(4)
+#define MJX_LDS_CU(DD, NN)                                                                                          \
+        if (T == 2) return trc ? goc(salds::k_sa_lds_cu<DD, 2, NN, true>) : goc(salds::k_sa_lds_cu<DD, 2, NN, false>); \
+        return trc ? goc(salds::k_sa_lds_cu<DD, 3, NN, true>) : goc(salds::k_sa_lds_cu<DD, 3, NN, false>);
+        if (nwc == 16) {
+            if (d == 3) { MJX_LDS_CU(3, 16) }
+            MJX_LDS_CU(4, 16)
+        }
+        if (d == 3) { MJX_LDS_CU(3, 8) }
+        MJX_LDS_CU(4, 8)
 #undef MJX_LDS_CU
     }
     auto go = [&](auto kern) -> int {

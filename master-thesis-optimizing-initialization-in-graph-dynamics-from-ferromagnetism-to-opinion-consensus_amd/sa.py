@@ -115,10 +115,11 @@ class SAReplicas:
         same results in every layout.  ``kernel``: light-cone kernel
         selection passed to the ABI (tests, tuning): ``split`` (waves per word
         column), ``spec_k`` (8 or 16), ``no_spec``, ``no_cone2``, ``lds_serial``, ``lds_single``, ``lds_pair``,
-        ``lds_wave`` (one wave per replica instead of the whole-CU kernel at
-        p+c-1 >= 2; ``split`` = 4 or 8 waves for the latter), ``lds_cu`` (the
-        whole CU level by level, d = 3, 4 at p+c-1 = 2, 3); the results
-        never depend on it.  ``rng``: ``"mt19937"`` replays numpy's seeded
+        ``lds_wave`` (one wave per replica instead of the whole-CU kernels at
+        p+c-1 >= 2), ``lds_cu`` (the whole CU level by level: the default at
+        d = 3, 4, p+c-1 = 2, 3 where it fits; ``split`` = 16 for its 16-wave
+        form), ``split`` = 4, 8 or 16 alone (the whole CU a proposal per wave,
+        k_sa_lds_wg); the results never depend on it.  ``rng``: ``"mt19937"`` replays numpy's seeded
         stream (the reference's proposals, bit for bit); ``"philox"`` is the
         NON-parity throughput mode: the proposal of step t of
         replica r comes from Philox-4x32-10 keyed by its seed (a pure function

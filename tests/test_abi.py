@@ -126,19 +126,26 @@ def test_device_memo_selftest_without_gpu(mjx_mod):
 def test_sa_lds_plan_names_the_kernel_that_runs(mjx_mod):
     """mjx_sa_lds_plan reports the LDS bytes and workgroup size of the kernel
     mjx_sa_lds_steps selects (the auto layout sized occupancy
-    with the one-plane bytes): the whole-CU kernel at p+c-1 >= 2 (8 or 4
-    waves; 16 where they fit, SA_RRG.py's n = 1e4), the paired one-wave kernel with lds_wave; at p+c-1 = 1 the
-    whole-CU 32-proposal kernel, or the one-wave eight-proposal one."""
+    with the one-plane bytes): at p+c-1 = 2, 3, d = 3, 4 the level-synchronous
+    whole-CU kernel where it fits (8 waves; 16 with split = 16), else, or with
+    split = 4 / 8 / 16 alone, the whole-CU kernel a proposal per wave (16 waves
+    where they fit), the paired one-wave kernel with lds_wave; at p+c-1 = 1
+    the whole-CU 32-proposal kernel, or the one-wave eight-proposal one."""
     import ctypes
     lib = mjx_mod.load_library()
     L = mjx_mod._lib
     th = ctypes.c_int(0)
     one = lib.mjx_sa_lds_bytes(10_000, 4, 3, 1)
-    wg16 = lib.mjx_sa_lds_plan(10_000, 4, 3, 1, 0, 0, ctypes.byref(th))      # 16 waves, 16-bit marks
-    assert th.value == 1024 and one < wg16 <= 160 * 1024
+    cu = lib.mjx_sa_lds_plan(10_000, 4, 3, 1, 0, 0, ctypes.byref(th))        # k_sa_lds_cu, 8 waves
+    assert th.value == 512 and one < cu <= 160 * 1024
+    assert lib.mjx_sa_lds_plan(10_000, 4, 3, 1, L.MJX_SA_LDS_CU, 16, ctypes.byref(th)) == cu and th.value == 1024
+    assert lib.mjx_sa_lds_plan(10_000, 3, 2, 1, 0, 0, ctypes.byref(th)) > 0 and th.value == 512
+    wg16 = lib.mjx_sa_lds_plan(10_000, 4, 3, 1, 0, 16, ctypes.byref(th))     # k_sa_lds_wg, 16 waves, 16-bit marks
+    assert th.value == 1024 and one < wg16 <= 160 * 1024 and wg16 != cu
     wg8 = lib.mjx_sa_lds_plan(10_000, 4, 3, 1, 0, 8, ctypes.byref(th))
     assert th.value == 512 and one < wg8 < wg16
-    assert lib.mjx_sa_lds_plan(12_000, 4, 3, 1, 0, 0, ctypes.byref(th)) > 0 and th.value == 512   # 16 do not fit
+    assert lib.mjx_sa_lds_plan(12_000, 4, 3, 1, 0, 0, ctypes.byref(th)) > 0 and th.value == 512   # wg, 16 do not fit
+    assert lib.mjx_sa_lds_plan(10_000, 4, 4, 1, 0, 0, ctypes.byref(th)) > 0 and th.value in (512, 1024)   # T = 4: wg
     wg4 = lib.mjx_sa_lds_plan(10_000, 4, 3, 1, 0, 4, ctypes.byref(th))
     assert th.value == 256 and wg4 < wg8
     pair = lib.mjx_sa_lds_plan(10_000, 4, 3, 1, L.MJX_SA_LDS_WAVE, 0, ctypes.byref(th))

@@ -56,16 +56,21 @@ def _check(tr, conf, t, graphs, graph_of, seeds, p, c, K, replicas):
     (3, 30, 1, 1, 40, 800, {}, "lightcone", "lds"),                          # n=30: 32 in flight, most cut
     (4, 300, 3, 1, 65, 300, {"lds_wave": True}, "lightcone", "lds"),       # one wave per replica (pair)
     (4, 300, 3, 1, 65, 300, {"split": 4}, "lightcone", "lds"),              # whole CU, 4 waves
-    (4, 300, 3, 1, 65, 300, {"split": 8}, "lightcone", "lds"),              # whole CU, 8 waves (16 by default here)
+    (4, 300, 3, 1, 65, 300, {"split": 8}, "lightcone", "lds"),              # whole CU, 8 waves
+    (4, 300, 3, 1, 65, 300, {"split": 16}, "lightcone", "lds"),             # whole CU, a proposal per wave, 16 waves
+    (3, 64, 2, 1, 40, 400, {"split": 16}, "lightcone", "lds"),
+    (4, 64, 2, 2, 40, 400, {"split": 16}, "lightcone", "lds"),
     (4, 40, 3, 1, 40, 600, {"split": 8}, "lightcone", "lds"),
     (3, 64, 2, 1, 40, 400, {"split": 8}, "lightcone", "lds"),
     (4, 64, 2, 2, 40, 400, {"lds_wave": True}, "lightcone", "lds"),
     (3, 64, 2, 1, 40, 400, {"split": 4}, "lightcone", "lds"),               # many conflicts, 4 waves
-    (4, 300, 3, 1, 65, 300, {"lds_cu": True}, "lightcone", "lds"),          # level-synchronous whole CU
+    (4, 300, 3, 1, 65, 300, {"lds_cu": True}, "lightcone", "lds"),          # level-synchronous whole CU (the default)
     (4, 40, 3, 1, 40, 600, {"lds_cu": True}, "lightcone", "lds"),
     (3, 64, 2, 1, 40, 400, {"lds_cu": True}, "lightcone", "lds"),
     (4, 64, 2, 2, 40, 400, {"lds_cu": True}, "lightcone", "lds"),           # T = 3
     (3, 30, 2, 2, 40, 600, {"lds_cu": True}, "lightcone", "lds"),           # T = 3, balls cover the graph
+    (4, 300, 3, 1, 65, 300, {"lds_cu": True, "split": 16}, "lightcone", "lds"),   # 16 waves
+    (3, 64, 2, 1, 40, 400, {"lds_cu": True, "split": 16}, "lightcone", "lds"),
     (4, 40, 3, 1, 40, 600, {}, "lightcone", "lds"),                         # n=40: most rounds conflict
     (3, 30, 2, 2, 40, 600, {}, "lightcone", "lds"),
     (4, 200, 1, 1, 5, 40, {}, "rollout", None),
@@ -144,10 +149,12 @@ def test_sa_run_distinct_graphs_to_consensus(mjx_mod, n, N_stat, seed, graph_see
 
 @pytest.mark.parametrize("d,n,p,c,kernel", [
     (3, 64, 1, 1, {}), (4, 64, 1, 1, {}), (3, 1000, 1, 1, {}), (4, 1000, 1, 1, {}),   # k_sa_lds_wg1<D,4,8,false>
-    (4, 64, 3, 1, {}), (4, 1000, 3, 1, {}), (3, 500, 2, 1, {}),                       # k_sa_lds_wg<D,T,16,false>
+    (4, 64, 3, 1, {}), (4, 1000, 3, 1, {}), (3, 500, 2, 1, {}),                       # k_sa_lds_cu<D,T,8,false>
+    (4, 64, 3, 1, {"split": 16}), (4, 1000, 3, 1, {"split": 16}), (3, 500, 2, 1, {"split": 16}),   # k_sa_lds_wg<D,T,16,false>
     (4, 1000, 3, 1, {"split": 8}), (4, 64, 3, 1, {"split": 8}),                      # k_sa_lds_wg<D,T,8,false>
     (4, 1000, 3, 1, {"split": 4}), (4, 1000, 3, 1, {"lds_wave": True}), (4, 1000, 1, 1, {"lds_wave": True}),
     (4, 1000, 3, 1, {"lds_cu": True}), (4, 64, 3, 1, {"lds_cu": True}), (3, 500, 2, 1, {"lds_cu": True}),
+    (4, 1000, 3, 1, {"lds_cu": True, "split": 16}),
 ])
 def test_lds_no_trace_matches_oracle(mjx_mod, d, n, p, c, kernel):
     """The kernels run() and the bench use (no trace buffers: TRACE=false

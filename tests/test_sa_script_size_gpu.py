@@ -4,9 +4,10 @@ replica (:58-62), against the C restatement of the reference's loop
 (oracle/orc_majority.c, :63-88) on the same graphs and seeds.
 
 At n = 1e4 the LDS kernels run far past the sizes of the other SA tests: the
-whole-CU kernel k_sa_lds_wg<4,3,8> holds ~138 KB of LDS per replica (rows as
-uint16 node ids, levels, byte marks, list sets), so offsets pass 64 KB and node
-ids pass 8192; k_sa_lds_wg1<4,4,8> (p = c = 1) the same graph at T = 1.  Every
+level-synchronous whole-CU kernel k_sa_lds_cu<4,3,8> (the default here) holds
+~156 KB of LDS per replica (rows as uint16 node ids, levels, 16-bit marks, the
+level lists), k_sa_lds_wg<4,3,8> ~138 KB, so offsets pass 64 KB and node ids
+pass 8192; k_sa_lds_wg1<4,4,8> (p = c = 1) the same graph at T = 1.  Every
 check is bit for bit: conf, t, the MT19937 stream each replica hands back
 (two ragged calls), and with the trace the per-step proposal, accept,
 sum(s_end) and delta_H."""
@@ -34,10 +35,12 @@ def _plan(mjx_mod, n, p, c, sa):
 
 
 @pytest.mark.parametrize("p,c,K1,K2,threads_want,kernel", [
-    (3, 1, 1900, 1133, 1024, None),          # SA_RRG.py's p=3, c=1: k_sa_lds_wg<4,3,16,false>, 16 waves
-    (3, 1, 1900, 1133, 512, {"split": 8}),   # the 8-wave form (byte marks)
-    (3, 1, 1900, 1133, 1024, {"lds_cu": True}),   # k_sa_lds_cu<4,3,false>, level-synchronous
-    (2, 2, 1900, 1133, 1024, {"lds_cu": True}),   # k_sa_lds_cu<4,3,false>, T = 3 via c = 2
+    (3, 1, 1900, 1133, 512, None),           # SA_RRG.py's p=3, c=1: k_sa_lds_cu<4,3,8,false>
+    (3, 1, 1900, 1133, 1024, {"split": 16}),  # k_sa_lds_wg<4,3,16,false>, a proposal per wave
+    (3, 1, 1900, 1133, 512, {"split": 8}),   # its 8-wave form (byte marks)
+    (3, 1, 1900, 1133, 512, {"lds_cu": True}),   # k_sa_lds_cu<4,3,8,false>, level-synchronous
+    (2, 2, 1900, 1133, 512, {"lds_cu": True}),   # k_sa_lds_cu<4,3,8,false>, T = 3 via c = 2
+    (3, 1, 1900, 1133, 1024, {"lds_cu": True, "split": 16}),   # k_sa_lds_cu<4,3,16,false>
     (1, 1, 2900, 1733, 320, None),           # configs[0]'s p=c=1: k_sa_lds_wg1<4,4,8,false>, 4 waves + the parser
 ])
 def test_script_size_no_trace_matches_oracle(mjx_mod, p, c, K1, K2, threads_want, kernel):

@@ -24,9 +24,11 @@ graphs = [mjx.random_regular_graph(d, n, seed=7000 + k) for k in range(R)]
 VARIANTS = {
     # name: (layout, kernel options)
     "lds": ("lds", None),                                   # the default LDS kernel for (p, c)
-    "lds-wg8": ("lds", {"split": 8}),                       # whole CU, 8 waves (p+c-1 >= 2; default 16 where it fits)
+    "lds-wg16": ("lds", {"split": 16}),                     # whole CU a proposal per wave, 16 waves (p+c-1 >= 2)
+    "lds-wg8": ("lds", {"split": 8}),                       # the same, 8 waves
     "lds-wg4": ("lds", {"split": 4}),                       # whole CU, 4 waves (p+c-1 >= 2)
     "lds-cu": ("lds", {"lds_cu": True}),                    # whole CU, level-synchronous (d 3/4, T 2/3)
+    "lds-cu16": ("lds", {"lds_cu": True, "split": 16}),     # the same with 16 waves
     "lds-wave": ("lds", {"lds_wave": True}),                # one wave: 8 proposals (T = 1) / 2 (T >= 2) per step
     "lds-pair": ("lds", {"lds_wave": True, "lds_pair": True}),   # one wave, two proposals per step
     "lds-single": ("lds", {"lds_single": True}),            # one wave, one proposal per step
@@ -40,7 +42,7 @@ for pc in args.pc.split(";"):
     for name, (layout, kern) in VARIANTS.items():
         if name == "cone" and args.no_cone:
             continue
-        if name in ("lds-wg4", "lds-wg8") and p + c - 1 < 2:
+        if name in ("lds-wg4", "lds-wg8", "lds-wg16", "lds-cu", "lds-cu16") and p + c - 1 < 2:
             continue
         K = 20000 if (layout == "lds" or p == 1) else 1000
         sa = mjx.SAReplicas(graphs, p, c, list(range(R)), layout=layout, kernel=kern)
