@@ -458,7 +458,7 @@ def bench_sa_global(args, rank, world, dist, dev):
     d=4 random regular graph, p=3, c=1, until m_final = 1 -- mjx.sa_run(...,
     stream="global"), replica k+1's draws continuing where replica k's last
     rand() left the stream.  One replica at a time is one workgroup: the
-    whole-CU LDS kernel (k_sa_lds_wg).  Per replica: wall time to consensus,
+    whole-CU LDS kernel (k_sa_lds_cu).  Per replica: wall time to consensus,
     num_steps, mag_reached, us per proposal.  (Each rank runs its own seed.)"""
     import mjx
     n, d, p, c = args.global_n, 4, 3, 1

@@ -2781,6 +2781,12 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_cu(const int32_t* __restrict
         LDS_STAMP(1);
         __syncthreads();                                   // level-1 marks and C_1 lists complete
         LDS_STAMP(2);
+        // the test wave's values, read while the levels run
+        const int ql = (lane < nq) ? lane : 0;
+        const double bh = pre_bh[ql];
+        const double t1 = pre_t1[ql];
+        const double u = pre_u[ql];
+        const double anx = pre_anx[ql], bnx = pre_bnx[ql];
         // ---- levels 2..T: every member of C_{l-1} of every proposal and its d neighbours
 #pragma unroll
         for (int l = 2; l <= T; ++l) {
@@ -2853,13 +2859,8 @@ __global__ void __launch_bounds__(64 * NW) k_sa_lds_cu(const int32_t* __restrict
         // (code/SA_RRG.py:37,74-76): the same arithmetic in every wave, so no
         // barrier hands the results over
         const bool lq = lane < nq;
-        const int ql = lq ? lane : 0;
         const int64_t ds = (int64_t)dsp[ql];
         const uint32_t pcf = lq ? cfp[ql] : 0u;
-        const double bh = pre_bh[ql];
-        const double t1 = pre_t1[ql];
-        const double u = pre_u[ql];
-        const double anx = pre_anx[ql], bnx = pre_bnx[ql];
         const double t2 = bh * (double)(-ds);
         const double num = t1 + t2;
         bool acc;
