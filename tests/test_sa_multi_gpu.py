@@ -232,3 +232,40 @@ def test_checkpoint_resume_equals_uninterrupted(mjx_mod, tmp_path, d, n, p, c, m
     m1, i1 = res.mt_state()
     m2, i2 = ref.mt_state()
     assert np.array_equal(m1, m2) and np.array_equal(i1, i2)
+
+
+@pytest.mark.parametrize("d,n,p,c,layout,kernel", [
+    (4, 300, 3, 1, "lds", None),                       # k_sa_lds_cu, T = 3
+    (3, 300, 2, 1, "lds", None),                       # k_sa_lds_cu, T = 2
+    (4, 300, 3, 1, "lds", {"split": 16}),              # k_sa_lds_wg
+    (4, 300, 3, 1, "lds", {"lds_wave": True}),         # one wave per replica
+    (4, 400, 1, 1, "lds", None),                       # k_sa_lds_wg1
+    (3, 500, 2, 1, "cone", None),                      # speculative batches
+    (3, 500, 2, 1, "cone", {"no_spec": True}),         # one round trip
+])
+@pytest.mark.parametrize("cap", [29, 137])
+def test_t_cap_stops_like_the_reference(mjx_mod, d, n, p, c, layout, kernel, cap):
+    """The loop's other exit, t > 2n^3 (code/SA_RRG.py:84), on the device: with
+    the cap lowered to `cap` every replica takes step cap+1, stops there with
+    done = 2 and takes no step in later calls; its configuration and MT19937
+    stream equal the reference loop's after cap+1 steps (orc_sa_loop, which
+    breaks after the same step)."""
+    R = 8
+    graphs = [mjx_mod.random_regular_graph(d, n, seed=9100 + 10 * d + k) for k in range(R)]
+    seeds = list(range(700, 700 + R))
+    sa = mjx_mod.SAReplicas(graphs, p, c, seeds, layout=layout, kernel=kernel)
+    sa.t_cap = cap
+    sa.steps(cap // 2 + 3)                         # the cap lands inside the second call
+    sa.steps(400)
+    sa.steps(50)                                   # nothing left to take
+    t, done = sa.t.cpu().numpy(), sa.done.cpu().numpy()
+    conf = sa.conf().cpu().numpy()
+    mt, idx = sa.mt_state() if layout == "lds" else (None, None)     # (a tape draws ahead of the stop)
+    for r in range(R):
+        st = np.random.RandomState(seeds[r]).get_state()
+        o = fast.sa_loop(graphs[r], p, c, seeds[r], max_steps=cap + 1, mt_state=(st[1], st[2]))
+        assert o["done"] == 0 and o["num_steps"] == cap + 1, r      # (no consensus this early)
+        assert t[r] == cap + 1 and done[r] == 2, (r, t[r], done[r])
+        assert np.array_equal(conf[r], o["conf"]), r
+        if mt is not None:
+            assert np.array_equal(mt[r], o["mt_state"][0]) and idx[r] == o["mt_state"][1], r
