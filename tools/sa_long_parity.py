@@ -6,7 +6,7 @@ reference's loop (oracle/orc_majority.c) run in worker processes: conf, t and
 the MT19937 stream must be equal.  A one-off check beyond the test suite's
 3033 steps (the oracle needs ~1.4 ms a step on one core).
 
-    python tools/sa_long_parity.py        (GPU box)
+    python tools/sa_long_parity.py        (GPU box; SA_LONG_PC="p,c", SA_LONG_K, SA_LONG_R)
 """
 import multiprocessing as mp
 import os
@@ -18,7 +18,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-D, N, P, C = 4, 10_000, 3, 1
+D, N = 4, 10_000
+P, C = (int(x) for x in os.environ.get("SA_LONG_PC", "3,1").split(","))   # e.g. "1,1": configs[0]'s kernel
 K = int(os.environ.get("SA_LONG_K", 60000))
 R = int(os.environ.get("SA_LONG_R", 2))
 
@@ -68,7 +69,7 @@ def main():
         print(f"replica {r}: t {t[r]} (oracle {o['num_steps']}), conf equal {np.array_equal(conf[r], o['conf'])}, "
               f"MT19937 state equal {np.array_equal(mt[r], o['mt_state'][0]) and idx[r] == o['mt_state'][1]}, "
               f"m(s) {conf[r].mean():+.4f}; oracle {cpu_s:.1f} s on one core", flush=True)
-    print(f"{K} steps in {len(chunks)} calls, {R} replicas: GPU {gpu_s:.2f} s; {'EQUAL' if ok else 'DIFFERENT'}",
+    print(f"p={P} c={C}: {K} steps in {len(chunks)} calls, {R} replicas: GPU {gpu_s:.2f} s; {'EQUAL' if ok else 'DIFFERENT'}",
           flush=True)
     sys.exit(0 if ok else 1)
 
